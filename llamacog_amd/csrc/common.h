@@ -1,0 +1,96 @@
+// common.h — shared definitions for the MI355X (gfx950, CDNA4) ggml backend.
+//
+// The backend is compiled against the reference's public ggml ABI headers
+// (ggml/include/ggml.h, ggml-backend.h and ggml/src/ggml-backend-impl.h); nothing
+// from ggml-cuda / ggml-hip is used.  Quant block layouts are restated here with
+// static_asserts against the sizes fixed in ggml/src/ggml-common.h:167-334.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+#include <cstddef>
+#include <cstring>
+
+#include "ggml.h"
+#include "ggml-backend.h"
+
+extern "C" void ggml_log_internal(enum ggml_log_level level, const char * format, ...);
+
+#define MI_LOG_INFO(...)  ggml_log_internal(GGML_LOG_LEVEL_INFO,  __VA_ARGS__)
+#define MI_LOG_WARN(...)  ggml_log_internal(GGML_LOG_LEVEL_WARN,  __VA_ARGS__)
+#define MI_LOG_ERROR(...) ggml_log_internal(GGML_LOG_LEVEL_ERROR, __VA_ARGS__)
+#define MI_LOG_DEBUG(...) ggml_log_internal(GGML_LOG_LEVEL_DEBUG, __VA_ARGS__)
+
+// Fatal HIP error: mirrors the reference's CUDA_CHECK -> ggml_cuda_error -> abort
+// (ggml/src/ggml-cuda/ggml-cuda.cu:70-81) with the HIP error string.
+#define MI_CHECK(expr)                                                                      \
+    do {                                                                                    \
+        hipError_t mi_err_ = (expr);                                                        \
+        if (mi_err_ != hipSuccess) {                                                        \
+            ggml_abort(__FILE__, __LINE__, "MI355X: %s failed: %s", #expr,                 \
+                       hipGetErrorString(mi_err_));                                         \
+        }                                                                                   \
+    } while (0)
+
+namespace mi355x {
+
+constexpr int WAVE = 64;   // CDNA wavefront width
+constexpr int QK_K = 256;  // K-quant super-block
+
+// ---- quant blocks (byte-exact restatement of ggml-common.h) ------------------------------
+struct blk_q4_0 { uint16_t d; uint8_t qs[16]; };
+struct blk_q8_0 { uint16_t d; int8_t qs[32]; };
+struct blk_q4_K { uint16_t d; uint16_t dmin; uint8_t scales[12]; uint8_t qs[128]; };
+struct blk_q5_K { uint16_t d; uint16_t dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; };
+struct blk_q6_K { uint8_t ql[128]; uint8_t qh[64]; int8_t scales[16]; uint16_t d; };
+struct blk_q8_K { float d; int8_t qs[256]; int16_t bsums[16]; };
+
+static_assert(sizeof(blk_q4_0) == 18,  "q4_0");
+static_assert(sizeof(blk_q8_0) == 34,  "q8_0");
+static_assert(sizeof(blk_q4_K) == 144, "q4_K");
+static_assert(sizeof(blk_q5_K) == 176, "q5_K");
+static_assert(sizeof(blk_q6_K) == 210, "q6_K");
+static_assert(sizeof(blk_q8_K) == 292, "q8_K");
+
+// ---- device helpers ------------------------------------------------------------------------
+__device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __half_as_ushort(__float2half_rn(f)); }
+
+// 16/8/4-byte loads from arbitrarily aligned addresses.  gfx950 under ROCm runs in
+// unaligned-access mode, so the compiler lowers these to single dwordx4/x2/dword loads.
+__device__ __forceinline__ uint4 ld16(const void * p) { uint4 v; __builtin_memcpy(&v, p, 16); return v; }
+__device__ __forceinline__ uint2 ld8(const void * p)  { uint2 v; __builtin_memcpy(&v, p, 8);  return v; }
+__device__ __forceinline__ uint32_t ld4(const void * p) { uint32_t v; __builtin_memcpy(&v, p, 4); return v; }
+__device__ __forceinline__ uint16_t ld2(const void * p) { uint16_t v; __builtin_memcpy(&v, p, 2); return v; }
+
+__device__ __forceinline__ int dot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+
+// 6-bit scale/min unpack of Q4_K/Q5_K (ggml-quants.c:625 get_scale_min_k4)
+__device__ __forceinline__ void scale_min_k4(int j, const uint8_t * q, int & d, int & m) {
+    if (j < 4) {
+        d = q[j] & 63;
+        m = q[j + 4] & 63;
+    } else {
+        d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        m = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4);
+    }
+}
+
+// ---- host helpers ----------------------------------------------------------------------------
+static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace mi355x

@@ -1,0 +1,545 @@
+// k_elem.hip — the small ops of the LLaMA graph: broadcast binary ops, scale, unary
+// (SiLU/GELU/...), copies/casts (incl. the f32 -> f16 / q8_0 KV-cache store), get_rows,
+// RMS norm (optionally fused with the following norm-weight MUL), RoPE and soft_max.
+//
+// Each op follows the CPU backend's arithmetic (ggml/src/ggml-cpu/ops.cpp,
+// binary-ops.cpp, unary-ops.cpp, vec.h) — operation order per element is kept, reductions
+// use wider accumulators where the CPU does (rms_norm sums in ggml_float = double).
+// They are HBM/latency-bound; all use 256-thread blocks with one row per block.
+#include "ops.h"
+
+#include <cmath>
+
+namespace mi355x {
+
+struct t4 { int64_t ne[4]; int64_t nb[4]; };
+static t4 mk(const ggml_tensor * t) {
+    t4 r;
+    for (int i = 0; i < 4; ++i) { r.ne[i] = t->ne[i]; r.nb[i] = (int64_t) t->nb[i]; }
+    return r;
+}
+
+// ------------------------------------------------------------------------------------------
+// binary broadcast: dst = op(src0, src1), src1 repeats across dims (ggml-cpu/binary-ops.cpp)
+// ------------------------------------------------------------------------------------------
+enum bin_op { BIN_ADD = 0, BIN_SUB, BIN_MUL, BIN_DIV };
+
+template <int OP>
+__device__ __forceinline__ float bin_apply(float a, float b) {
+    if constexpr (OP == BIN_ADD) return a + b;
+    else if constexpr (OP == BIN_SUB) return a - b;
+    else if constexpr (OP == BIN_MUL) return a * b;
+    else return a / b;
+}
+
+template <int OP>
+__global__ __launch_bounds__(256) void k_binary(const char * __restrict__ a, t4 ta, const char * __restrict__ b, t4 tb,
+                                                char * __restrict__ d, t4 td) {
+    const int64_t r = blockIdx.x;  // row over (i1, i2, i3) of dst
+    const int64_t i1 = r % td.ne[1], i2 = (r / td.ne[1]) % td.ne[2], i3 = r / (td.ne[1] * td.ne[2]);
+    const char * ar = a + i1 * ta.nb[1] + i2 * ta.nb[2] + i3 * ta.nb[3];
+    const char * br = b + (i1 % tb.ne[1]) * tb.nb[1] + (i2 % tb.ne[2]) * tb.nb[2] + (i3 % tb.ne[3]) * tb.nb[3];
+    char * dr = d + i1 * td.nb[1] + i2 * td.nb[2] + i3 * td.nb[3];
+    const int64_t ne0 = td.ne[0], ne10 = tb.ne[0];
+    for (int64_t i0 = threadIdx.x; i0 < ne0; i0 += blockDim.x) {
+        const float x = *(const float *) (ar + i0 * ta.nb[0]);
+        const float y = *(const float *) (br + (i0 % ne10) * tb.nb[0]);
+        *(float *) (dr + i0 * td.nb[0]) = bin_apply<OP>(x, y);
+    }
+}
+
+void op_binary(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * s0 = dst->src[0];
+    const ggml_tensor * s1 = dst->src[1];
+    const int64_t nrows = dst->ne[1] * dst->ne[2] * dst->ne[3];
+    if (nrows == 0 || dst->ne[0] == 0) return;
+    const unsigned thr = dst->ne[0] >= 256 ? 256 : 64;
+    auto A = mk(s0), B = mk(s1), D = mk(dst);
+    switch (dst->op) {
+        case GGML_OP_ADD: hipLaunchKernelGGL(k_binary<BIN_ADD>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
+        case GGML_OP_SUB: hipLaunchKernelGGL(k_binary<BIN_SUB>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
+        case GGML_OP_MUL: hipLaunchKernelGGL(k_binary<BIN_MUL>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
+        case GGML_OP_DIV: hipLaunchKernelGGL(k_binary<BIN_DIV>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
+        default: GGML_ABORT("mi355x: bad binary op");
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// scale (ops.cpp ggml_compute_forward_scale_f32: y = x*s) and unary ops
+// ------------------------------------------------------------------------------------------
+enum un_op { UN_SILU = 0, UN_GELU, UN_RELU, UN_NEG, UN_TANH, UN_SIGMOID, UN_SCALE, UN_GELU_QUICK, UN_EXP, UN_ABS, UN_SGN, UN_STEP, UN_GELU_ERF };
+
+template <int OP>
+__device__ __forceinline__ float un_apply(float x, float s) {
+    if constexpr (OP == UN_SILU) return x / (1.0f + expf(-x));                       // vec.h ggml_silu_f32
+    else if constexpr (OP == UN_RELU) return x > 0.0f ? x : 0.0f;
+    else if constexpr (OP == UN_NEG) return -x;
+    else if constexpr (OP == UN_TANH) return tanhf(x);
+    else if constexpr (OP == UN_SIGMOID) return 1.0f / (1.0f + expf(-x));
+    else if constexpr (OP == UN_SCALE) return x * s;
+    else if constexpr (OP == UN_EXP) return expf(x);
+    else if constexpr (OP == UN_ABS) return fabsf(x);
+    else if constexpr (OP == UN_SGN) return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f);
+    else if constexpr (OP == UN_STEP) return (x > 0.f) ? 1.f : 0.f;
+    else if constexpr (OP == UN_GELU_QUICK) return x * (1.0f / (1.0f + expf(-1.702f * x)));
+    else if constexpr (OP == UN_GELU_ERF) return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+    else {  // GELU tanh approximation (vec.h ggml_gelu_f32)
+        const float GELU_COEF_A = 0.044715f, SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+        return 0.5f * x * (1.0f + tanhf(SQRT_2_OVER_PI * x * (1.0f + GELU_COEF_A * x * x)));
+    }
+}
+
+template <int OP>
+__global__ __launch_bounds__(256) void k_unary(const char * __restrict__ a, t4 ta, char * __restrict__ d, t4 td, float s) {
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % td.ne[1], i2 = (r / td.ne[1]) % td.ne[2], i3 = r / (td.ne[1] * td.ne[2]);
+    const char * ar = a + i1 * ta.nb[1] + i2 * ta.nb[2] + i3 * ta.nb[3];
+    char * dr = d + i1 * td.nb[1] + i2 * td.nb[2] + i3 * td.nb[3];
+    for (int64_t i0 = threadIdx.x; i0 < td.ne[0]; i0 += blockDim.x) {
+        *(float *) (dr + i0 * td.nb[0]) = un_apply<OP>(*(const float *) (ar + i0 * ta.nb[0]), s);
+    }
+}
+
+template <int OP>
+static void launch_unary(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst, float s) {
+    const int64_t nrows = dst->ne[1] * dst->ne[2] * dst->ne[3];
+    if (nrows == 0 || dst->ne[0] == 0) return;
+    const unsigned thr = dst->ne[0] >= 256 ? 256 : 64;
+    hipLaunchKernelGGL(k_unary<OP>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) src->data, mk(src),
+                       (char *) dst->data, mk(dst), s);
+}
+
+void op_scale(exec_ctx & ctx, ggml_tensor * dst) {
+    float s;
+    memcpy(&s, dst->op_params, sizeof(float));
+    launch_unary<UN_SCALE>(ctx, dst->src[0], dst, s);
+}
+
+void op_unary(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * src = dst->src[0];
+    switch (ggml_get_unary_op(dst)) {
+        case GGML_UNARY_OP_SILU:       launch_unary<UN_SILU>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_GELU:       launch_unary<UN_GELU>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_GELU_ERF:   launch_unary<UN_GELU_ERF>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_GELU_QUICK: launch_unary<UN_GELU_QUICK>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_RELU:       launch_unary<UN_RELU>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_NEG:        launch_unary<UN_NEG>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_TANH:       launch_unary<UN_TANH>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_SIGMOID:    launch_unary<UN_SIGMOID>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_EXP:        launch_unary<UN_EXP>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_ABS:        launch_unary<UN_ABS>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_SGN:        launch_unary<UN_SGN>(ctx, src, dst, 0.f); break;
+        case GGML_UNARY_OP_STEP:       launch_unary<UN_STEP>(ctx, src, dst, 0.f); break;
+        default: GGML_ABORT("mi355x: unsupported unary op");
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// copies / casts: element i of src (row-major order) -> element i of dst (row-major order),
+// the semantics of ggml_compute_forward_dup for non-quantized types.
+// ------------------------------------------------------------------------------------------
+template <typename TS, typename TD>
+__device__ __forceinline__ TD cvt(TS v);
+template <> __device__ __forceinline__ float    cvt<float, float>(float v) { return v; }
+template <> __device__ __forceinline__ uint16_t cvt<float, uint16_t>(float v) { return f2h(v); }
+template <> __device__ __forceinline__ float    cvt<uint16_t, float>(uint16_t v) { return h2f(v); }
+template <> __device__ __forceinline__ uint16_t cvt<uint16_t, uint16_t>(uint16_t v) { return v; }
+template <> __device__ __forceinline__ int32_t  cvt<int32_t, int32_t>(int32_t v) { return v; }
+
+template <typename TS, typename TD>
+__global__ __launch_bounds__(256) void k_cpy(const char * __restrict__ s, t4 ts, char * __restrict__ d, t4 td, int64_t n) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        int64_t r = i;
+        const int64_t s0 = r % ts.ne[0]; r /= ts.ne[0];
+        const int64_t s1 = r % ts.ne[1]; r /= ts.ne[1];
+        const int64_t s2 = r % ts.ne[2]; const int64_t s3 = r / ts.ne[2];
+        r = i;
+        const int64_t d0 = r % td.ne[0]; r /= td.ne[0];
+        const int64_t d1 = r % td.ne[1]; r /= td.ne[1];
+        const int64_t d2 = r % td.ne[2]; const int64_t d3 = r / td.ne[2];
+        const TS v = *(const TS *) (s + s0 * ts.nb[0] + s1 * ts.nb[1] + s2 * ts.nb[2] + s3 * ts.nb[3]);
+        *(TD *) (d + d0 * td.nb[0] + d1 * td.nb[1] + d2 * td.nb[2] + d3 * td.nb[3]) = cvt<TS, TD>(v);
+    }
+}
+
+// contiguous f32 -> f16 fast path (KV store of K/V rows, mask cast)
+__global__ __launch_bounds__(256) void k_cpy_f32_f16_contig(const float * __restrict__ s, uint16_t * __restrict__ d, int64_t n) {
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        d[i] = f2h(s[i]);
+    }
+}
+
+// f32 rows -> q8_0 blocks (x86 quantize_row_q8_0 semantics, see k_mmv.hip); one wave per 8 blocks
+__global__ __launch_bounds__(64) void k_cpy_f32_q8_0(const char * __restrict__ s, t4 ts, char * __restrict__ d, t4 td) {
+    const int lane = threadIdx.x;
+    const int64_t r = blockIdx.y;  // source row
+    const int64_t i1 = r % ts.ne[1], i2 = (r / ts.ne[1]) % ts.ne[2], i3 = r / (ts.ne[1] * ts.ne[2]);
+    const char * srow = s + i1 * ts.nb[1] + i2 * ts.nb[2] + i3 * ts.nb[3];
+    // destination row with the same flat row index
+    const int64_t j1 = r % td.ne[1], j2 = (r / td.ne[1]) % td.ne[2], j3 = r / (td.ne[1] * td.ne[2]);
+    char * drow = d + j1 * td.nb[1] + j2 * td.nb[2] + j3 * td.nb[3];
+    const int64_t e0 = (int64_t) blockIdx.x * 256 + 4 * lane;
+    const bool valid = e0 < ts.ne[0];
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = *(const float *) (srow + (e0 + k) * ts.nb[0]);
+    }
+    float amax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, WAVE));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, WAVE));
+    amax = fmaxf(amax, __shfl_xor(amax, 4, WAVE));
+    const float dd = amax / 127.0f;
+    const float id = amax != 0.0f ? 127.0f / amax : 0.0f;
+    if (!valid) return;
+    blk_q8_0 * blk = (blk_q8_0 *) (drow + (e0 / 32) * sizeof(blk_q8_0));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int iv = (int) rintf(__fmul_rn(v[k], id));
+        iv = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
+        blk->qs[(e0 % 32) + k] = (int8_t) iv;
+    }
+    if ((lane & 7) == 0) blk->d = f2h(dd);
+}
+
+void op_cpy(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst) {
+    const int64_t n = ggml_nelements(src);
+    if (n == 0) return;
+    const t4 S = mk(src), D = mk(dst);
+    const unsigned grid = (unsigned) std::min<int64_t>(ceil_div(n, 256), 8192);
+    if (src->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_F16 && ggml_is_contiguous(src) && ggml_is_contiguous(dst)) {
+        hipLaunchKernelGGL(k_cpy_f32_f16_contig, dim3(grid), dim3(256), 0, ctx.stream, (const float *) src->data, (uint16_t *) dst->data, n);
+        return;
+    }
+    if (src->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_Q8_0) {
+        const int64_t nrows = src->ne[1] * src->ne[2] * src->ne[3];
+        dim3 g((unsigned) ceil_div(src->ne[0], 256), (unsigned) nrows);
+        hipLaunchKernelGGL(k_cpy_f32_q8_0, g, dim3(64), 0, ctx.stream, (const char *) src->data, S, (char *) dst->data, D);
+        return;
+    }
+#define CPY_CASE(TS_, TD_, ts, td) \
+    if (src->type == TS_ && dst->type == TD_) { hipLaunchKernelGGL((k_cpy<ts, td>), dim3(grid), dim3(256), 0, ctx.stream, (const char *) src->data, S, (char *) dst->data, D, n); return; }
+    CPY_CASE(GGML_TYPE_F32, GGML_TYPE_F32, float, float)
+    CPY_CASE(GGML_TYPE_F32, GGML_TYPE_F16, float, uint16_t)
+    CPY_CASE(GGML_TYPE_F16, GGML_TYPE_F32, uint16_t, float)
+    CPY_CASE(GGML_TYPE_F16, GGML_TYPE_F16, uint16_t, uint16_t)
+    CPY_CASE(GGML_TYPE_I32, GGML_TYPE_I32, int32_t, int32_t)
+#undef CPY_CASE
+    GGML_ABORT("mi355x: unsupported cpy %s -> %s", ggml_type_name(src->type), ggml_type_name(dst->type));
+}
+
+// ------------------------------------------------------------------------------------------
+// get_rows: dst[:, i10, i11, i12] = dequant(src0[:, rows[i10,i11,i12], i11, i12])
+// ------------------------------------------------------------------------------------------
+__device__ float dequant_elem(int type, const char * row, int64_t i) {
+    switch (type) {
+        case GGML_TYPE_F32: return *(const float *) (row + 4 * i);
+        case GGML_TYPE_F16: return h2f(*(const uint16_t *) (row + 2 * i));
+        case GGML_TYPE_Q8_0: {
+            const blk_q8_0 * b = (const blk_q8_0 *) (row) + i / 32;
+            return h2f(ld2(&b->d)) * b->qs[i % 32];
+        }
+        case GGML_TYPE_Q4_0: {
+            const blk_q4_0 * b = (const blk_q4_0 *) (row) + i / 32;
+            const int j = i % 32;
+            const int q = j < 16 ? (b->qs[j] & 0xF) : (b->qs[j - 16] >> 4);
+            return (q - 8) * h2f(ld2(&b->d));
+        }
+        case GGML_TYPE_Q4_K: {
+            const blk_q4_K * b = (const blk_q4_K *) (row) + i / 256;
+            const int j = i % 256, g = j / 64, l = j % 32, hi = (j % 64) >= 32;
+            int sc, m;
+            scale_min_k4(2 * g + hi, b->scales, sc, m);
+            const int q = hi ? (b->qs[32 * g + l] >> 4) : (b->qs[32 * g + l] & 0xF);
+            return h2f(ld2(&b->d)) * sc * q - h2f(ld2(&b->dmin)) * m;
+        }
+        case GGML_TYPE_Q5_K: {
+            const blk_q5_K * b = (const blk_q5_K *) (row) + i / 256;
+            const int j = i % 256, g = j / 64, l = j % 32, hi = (j % 64) >= 32;
+            int sc, m;
+            scale_min_k4(2 * g + hi, b->scales, sc, m);
+            int q = hi ? (b->qs[32 * g + l] >> 4) : (b->qs[32 * g + l] & 0xF);
+            q += ((b->qh[l] >> (2 * g + hi)) & 1) << 4;
+            return h2f(ld2(&b->d)) * sc * q - h2f(ld2(&b->dmin)) * m;
+        }
+        case GGML_TYPE_Q6_K: {
+            const blk_q6_K * b = (const blk_q6_K *) (row) + i / 256;
+            const int j = i % 256, n = j / 128, jj = j % 128, grp = jj / 32, l = jj % 32;
+            const uint8_t * ql = b->ql + 64 * n;
+            const uint8_t * qh = b->qh + 32 * n;
+            int q;
+            switch (grp) {
+                case 0: q = (ql[l] & 0xF) | (((qh[l] >> 0) & 3) << 4); break;
+                case 1: q = (ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4); break;
+                case 2: q = (ql[l] >> 4) | (((qh[l] >> 4) & 3) << 4); break;
+                default: q = (ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4); break;
+            }
+            const int is = 8 * n + l / 16 + 2 * grp;
+            return h2f(ld2(&b->d)) * b->scales[is] * (q - 32);
+        }
+        default: return 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_get_rows(const char * __restrict__ s0, t4 t0, int type,
+                                                  const char * __restrict__ s1, t4 t1, char * __restrict__ d, t4 td) {
+    const int64_t r = blockIdx.x;  // over (i10, i11, i12)
+    const int64_t i10 = r % t1.ne[0], i11 = (r / t1.ne[0]) % t1.ne[1], i12 = r / (t1.ne[0] * t1.ne[1]);
+    const int32_t row = *(const int32_t *) (s1 + i10 * t1.nb[0] + i11 * t1.nb[1] + i12 * t1.nb[2]);
+    const char * srow = s0 + row * t0.nb[1] + i11 * t0.nb[2] + i12 * t0.nb[3];
+    char * drow = d + i10 * td.nb[1] + i11 * td.nb[2] + i12 * td.nb[3];
+    for (int64_t i = threadIdx.x; i < t0.ne[0]; i += blockDim.x) {
+        *(float *) (drow + i * td.nb[0]) = dequant_elem(type, srow, i);
+    }
+}
+
+void op_get_rows(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * s0 = dst->src[0];
+    const ggml_tensor * s1 = dst->src[1];
+    const int64_t n = s1->ne[0] * s1->ne[1] * s1->ne[2];
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_get_rows, dim3((unsigned) n), dim3(256), 0, ctx.stream, (const char *) s0->data, mk(s0),
+                       (int) s0->type, (const char *) s1->data, mk(s1), (char *) dst->data, mk(dst));
+}
+
+// ------------------------------------------------------------------------------------------
+// RMS norm (ops.cpp:3270-3316): sum of x*x in double, mean = sum/ne0 (rounded to float),
+// scale = 1/sqrtf(mean+eps), y = x*scale; optionally y *= w (the following MUL node).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rms_norm(const char * __restrict__ x, t4 tx, char * __restrict__ y, t4 ty,
+                                                  const char * __restrict__ w, t4 tw, char * __restrict__ y2, t4 ty2,
+                                                  float eps) {
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % tx.ne[1], i2 = (r / tx.ne[1]) % tx.ne[2], i3 = r / (tx.ne[1] * tx.ne[2]);
+    const float * xr = (const float *) (x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3]);
+    float * yr = (float *) (y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
+    const int64_t ne0 = tx.ne[0];
+    double sum = 0.0;
+    for (int64_t i = threadIdx.x; i < ne0; i += 256) {
+        const float v = xr[i];
+        sum += (double) (v * v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
+    __shared__ double part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    sum = part[0] + part[1] + part[2] + part[3];
+    const float mean = (float) (sum / (double) ne0);
+    const float scale = 1.0f / sqrtf(mean + eps);
+    if (y2) {
+        // fused norm-weight MUL: the norm output is still stored (other readers stay
+        // correct, and an in-place MUL sees the same thread write y then y*w in order)
+        float * y2r = (float *) (y2 + i1 * ty2.nb[1] + i2 * ty2.nb[2] + i3 * ty2.nb[3]);
+        const char * wr = w + (i1 % tw.ne[1]) * tw.nb[1] + (i2 % tw.ne[2]) * tw.nb[2] + (i3 % tw.ne[3]) * tw.nb[3];
+        const int64_t nw = tw.ne[0];
+        for (int64_t i = threadIdx.x; i < ne0; i += 256) {
+            const float v = __fmul_rn(xr[i], scale);
+            yr[i] = v;
+            y2r[i] = __fmul_rn(v, *(const float *) (wr + (i % nw) * tw.nb[0]));
+        }
+    } else {
+        for (int64_t i = threadIdx.x; i < ne0; i += 256) yr[i] = xr[i] * scale;
+    }
+}
+
+void op_rms_norm(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mul_w, ggml_tensor * out) {
+    const ggml_tensor * src = dst->src[0];
+    float eps;
+    memcpy(&eps, dst->op_params, sizeof(float));
+    const int64_t nrows = src->ne[1] * src->ne[2] * src->ne[3];
+    if (nrows == 0) return;
+    t4 tw = {}, t2 = {};
+    for (int i = 0; i < 4; ++i) { tw.ne[i] = 1; t2.ne[i] = 1; }
+    if (mul_w) { tw = mk(mul_w); t2 = mk(out); }
+    hipLaunchKernelGGL(k_rms_norm, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, (const char *) src->data, mk(src),
+                       (char *) dst->data, mk(dst), mul_w ? (const char *) mul_w->data : nullptr, tw,
+                       mul_w ? (char *) out->data : nullptr, t2, eps);
+}
+
+// layer norm (ops.cpp ggml_compute_forward_norm_f32): mean/variance in double
+__global__ __launch_bounds__(256) void k_norm(const char * __restrict__ x, t4 tx, char * __restrict__ y, t4 ty, float eps) {
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % tx.ne[1], i2 = (r / tx.ne[1]) % tx.ne[2], i3 = r / (tx.ne[1] * tx.ne[2]);
+    const float * xr = (const float *) (x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3]);
+    float * yr = (float *) (y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
+    const int64_t ne0 = tx.ne[0];
+    __shared__ double part[4];
+    double sum = 0.0;
+    for (int64_t i = threadIdx.x; i < ne0; i += 256) sum += (double) xr[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    const float mean = (float) ((part[0] + part[1] + part[2] + part[3]) / (double) ne0);
+    __syncthreads();
+    double s2 = 0.0;
+    for (int64_t i = threadIdx.x; i < ne0; i += 256) {
+        const float v = xr[i] - mean;
+        s2 += (double) (v * v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, WAVE);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s2;
+    __syncthreads();
+    const float variance = (float) ((part[0] + part[1] + part[2] + part[3]) / (double) ne0);
+    const float scale = 1.0f / sqrtf(variance + eps);
+    for (int64_t i = threadIdx.x; i < ne0; i += 256) yr[i] = (xr[i] - mean) * scale;
+}
+
+void op_norm(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * src = dst->src[0];
+    float eps;
+    memcpy(&eps, dst->op_params, sizeof(float));
+    const int64_t nrows = src->ne[1] * src->ne[2] * src->ne[3];
+    if (nrows == 0) return;
+    hipLaunchKernelGGL(k_norm, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, (const char *) src->data, mk(src),
+                       (char *) dst->data, mk(dst), eps);
+}
+
+// ------------------------------------------------------------------------------------------
+// RoPE (ops.cpp:5080-5362).  theta for pair i is built exactly like ggml_rope_cache_init:
+// theta_0 = p, theta_{i+1} = theta_i * theta_scale (fp32, sequential), then rope_yarn.
+// ------------------------------------------------------------------------------------------
+struct rope_params {
+    int n_dims; int mode; float freq_scale, ext_factor, attn_factor; float corr0, corr1; float theta_scale;
+    int has_ff;
+};
+
+__device__ __forceinline__ void rope_yarn_dev(float theta_extrap, float freq_scale, float corr0, float corr1, int64_t i0,
+                                              float ext_factor, float mscale, float & c, float & s) {
+    const float theta_interp = freq_scale * theta_extrap;
+    float theta = theta_interp;
+    if (ext_factor != 0.0f) {
+        const float y = (i0 / 2 - corr0) / fmaxf(0.001f, corr1 - corr0);
+        const float ramp_mix = (1.0f - fminf(1.0f, fmaxf(0.0f, y))) * ext_factor;
+        theta = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
+        mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
+    }
+    c = cosf(theta) * mscale;
+    s = sinf(theta) * mscale;
+}
+
+__global__ __launch_bounds__(256) void k_rope(const char * __restrict__ x, t4 tx, char * __restrict__ y, t4 ty,
+                                              const int32_t * __restrict__ pos, const float * __restrict__ ff, rope_params rp) {
+    const int64_t r = blockIdx.x;  // row over (i1 head, i2 token, i3)
+    const int64_t i1 = r % tx.ne[1], i2 = (r / tx.ne[1]) % tx.ne[2], i3 = r / (tx.ne[1] * tx.ne[2]);
+    const char * xr = x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3];
+    char * yr = y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3];
+    const int64_t ne0 = tx.ne[0];
+    const float p = (float) pos[i2];
+    const bool neox = rp.mode & 2;
+    for (int64_t ip = threadIdx.x; ip < ne0 / 2; ip += blockDim.x) {
+        const int64_t i0 = 2 * ip;
+        if (i0 < rp.n_dims) {
+            float theta = p;
+            for (int64_t k = 0; k < ip; ++k) theta *= rp.theta_scale;
+            const float f = rp.has_ff ? ff[ip] : 1.0f;
+            float c, s;
+            rope_yarn_dev(theta / f, rp.freq_scale, rp.corr0, rp.corr1, i0, rp.ext_factor, rp.attn_factor, c, s);
+            int64_t a0, a1;
+            if (neox) { a0 = ip; a1 = ip + rp.n_dims / 2; }
+            else      { a0 = i0; a1 = i0 + 1; }
+            const float x0 = *(const float *) (xr + a0 * tx.nb[0]);
+            const float x1 = *(const float *) (xr + a1 * tx.nb[0]);
+            *(float *) (yr + a0 * ty.nb[0]) = x0 * c - x1 * s;
+            *(float *) (yr + a1 * ty.nb[0]) = x0 * s + x1 * c;
+        } else {
+            *(float *) (yr + i0 * ty.nb[0])       = *(const float *) (xr + i0 * tx.nb[0]);
+            *(float *) (yr + (i0 + 1) * ty.nb[0]) = *(const float *) (xr + (i0 + 1) * tx.nb[0]);
+        }
+    }
+}
+
+void op_rope(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * src = dst->src[0];
+    const ggml_tensor * pos = dst->src[1];
+    const ggml_tensor * ff  = dst->src[2];
+    const int32_t * op = dst->op_params;
+    rope_params rp;
+    rp.n_dims = op[1];
+    rp.mode = op[2];
+    const int n_ctx_orig = op[4];
+    float freq_base, beta_fast, beta_slow;
+    memcpy(&freq_base, op + 5, 4);
+    memcpy(&rp.freq_scale, op + 6, 4);
+    memcpy(&rp.ext_factor, op + 7, 4);
+    memcpy(&rp.attn_factor, op + 8, 4);
+    memcpy(&beta_fast, op + 9, 4);
+    memcpy(&beta_slow, op + 10, 4);
+    rp.theta_scale = powf(freq_base, -2.0f / rp.n_dims);
+    float corr[2];
+    ggml_rope_yarn_corr_dims(rp.n_dims, n_ctx_orig, freq_base, beta_fast, beta_slow, corr);
+    rp.corr0 = corr[0]; rp.corr1 = corr[1];
+    rp.has_ff = ff != nullptr;
+    const int64_t nrows = src->ne[1] * src->ne[2] * src->ne[3];
+    if (nrows == 0) return;
+    const unsigned thr = src->ne[0] / 2 >= 256 ? 256 : 64;
+    hipLaunchKernelGGL(k_rope, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) src->data, mk(src),
+                       (char *) dst->data, mk(dst), (const int32_t *) pos->data, ff ? (const float *) ff->data : nullptr, rp);
+}
+
+// ------------------------------------------------------------------------------------------
+// soft_max (ops.cpp:4731-4827): w = x*scale + slope*mask; y = exp(w-max)/sum (sum in double)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_soft_max(const char * __restrict__ x, t4 tx, char * __restrict__ y, t4 ty,
+                                                  const char * __restrict__ mask, t4 tm, int mask_f16,
+                                                  float scale, float max_bias, float m0, float m1, uint32_t n_head_log2) {
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % tx.ne[1], i2 = (r / tx.ne[1]) % tx.ne[2], i3 = r / (tx.ne[1] * tx.ne[2]);
+    const float * xr = (const float *) (x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3]);
+    float * yr = (float *) (y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
+    const int64_t nc = tx.ne[0];
+    const uint32_t h = (uint32_t) i2;  // head index = (flat_row / ne01) % ne02
+    const float slope = max_bias > 0.0f ? (h < n_head_log2 ? powf(m0, h + 1) : powf(m1, 2 * (h - n_head_log2) + 1)) : 1.0f;
+    const char * mr = mask ? mask + (i1 % tm.ne[1]) * tm.nb[1] : nullptr;
+
+    __shared__ float redf[4];
+    __shared__ double redd[4];
+    float mx = -INFINITY;
+    for (int64_t i = threadIdx.x; i < nc; i += 256) {
+        float w = xr[i] * scale;
+        if (mr) w += slope * (mask_f16 ? h2f(*(const uint16_t *) (mr + 2 * i)) : *(const float *) (mr + 4 * i));
+        yr[i] = w;
+        mx = fmaxf(mx, w);
+    }
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) redf[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    double sum = 0.0;
+    for (int64_t i = threadIdx.x; i < nc; i += 256) {
+        const float e = expf(yr[i] - mx);
+        yr[i] = e;
+        sum += (double) e;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
+    if ((threadIdx.x & 63) == 0) redd[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    sum = redd[0] + redd[1] + redd[2] + redd[3];
+    const float inv = (float) (1.0 / sum);
+    for (int64_t i = threadIdx.x; i < nc; i += 256) yr[i] *= inv;
+}
+
+void op_soft_max(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * src = dst->src[0];
+    const ggml_tensor * mask = dst->src[1];
+    float scale, max_bias;
+    memcpy(&scale, (const float *) dst->op_params + 0, 4);
+    memcpy(&max_bias, (const float *) dst->op_params + 1, 4);
+    const uint32_t n_head = (uint32_t) src->ne[2];
+    const uint32_t n_head_log2 = 1u << (uint32_t) floor(log2((double) n_head));
+    const float m0 = powf(2.0f, -(max_bias) / n_head_log2);
+    const float m1 = powf(2.0f, -(max_bias / 2.0f) / n_head_log2);
+    const int64_t nrows = src->ne[1] * src->ne[2] * src->ne[3];
+    if (nrows == 0) return;
+    t4 tm = {};
+    for (int i = 0; i < 4; ++i) tm.ne[i] = 1;
+    if (mask) tm = mk(mask);
+    hipLaunchKernelGGL(k_soft_max, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, (const char *) src->data, mk(src),
+                       (char *) dst->data, mk(dst), mask ? (const char *) mask->data : nullptr, tm,
+                       mask && mask->type == GGML_TYPE_F16 ? 1 : 0, scale, max_bias, m0, m1, n_head_log2);
+}
+
+}  // namespace mi355x

@@ -1,0 +1,305 @@
+// k_fattn.hip — FLASH_ATTN_EXT over an f16 or q8_0 KV cache.
+//
+// Semantics follow ggml_compute_forward_flash_attn_ext_f16 (ggml-cpu/ops.cpp:7015-7232):
+//   * Q is first converted to K's vec_dot_type: rounded to f16 for an f16 cache, quantized to
+//     Q8_0 (x86 rounding) for a q8_0 cache, and K·Q is taken in that representation;
+//   * s = (K·Q)*scale (softcap optional) + slope*mask, masked (-inf) positions are skipped;
+//   * online softmax, V accumulated with weights exp(s - M), output VKQ * (1/S).
+// The CPU accumulates VKQ for an f16 V in f16; we keep it in f32 (documented tolerance,
+// test-backend-ops bounds FA at NMSE 5e-4, tests/test-backend-ops.cpp:3334-3336).
+//
+// MI355X layout: one workgroup (4 waves) per (q row, q head, KV chunk).  A wave scores 64
+// KV positions at once with one position per lane (K rows read as 16-byte vectors, Q
+// broadcast from LDS), does the online-softmax update with wave reductions, then streams
+// the 64 V rows with lanes owning D/64 output dims each.  Long caches are split over
+// chunks (split-K) so decode fills the chip; a combine kernel merges the chunk partials.
+#include "ops.h"
+
+#include <cmath>
+
+namespace mi355x {
+
+struct fa_args {
+    const char * q; int64_t nbq1, nbq2, nbq3;
+    const char * k; int64_t nbk1, nbk2, nbk3;
+    const char * v; int64_t nbv1, nbv2, nbv3;
+    const char * mask; int64_t nbm1; int64_t mask_ne1;
+    int k_type, v_type;
+    int64_t D, n_kv, n_q, H, Hkv, chunk;
+    float scale, softcap, max_bias, m0, m1; uint32_t n_head_log2;
+    float * part;      // [nchunks][n_q][H][D+2]  (M, S, O[D])
+    float * dst;       // final output when nchunks == 1
+    int64_t nb1_dst, nb2_dst;
+    int nchunks;
+};
+
+template <int EPL>  // elements of D per lane (D = 64*EPL)
+__global__ __launch_bounds__(256) void k_fattn_vec(const fa_args a) {
+    constexpr int D = 64 * EPL;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t chunk = blockIdx.x;
+    const int64_t iq1 = blockIdx.y;
+    const int64_t h = blockIdx.z % a.H;
+    const int64_t iq3 = blockIdx.z / a.H;
+    const int64_t hk = h / (a.H / a.Hkv);
+
+    __shared__ float qf[D];          // Q as f32 (f16-rounded for an f16 K)
+    __shared__ int8_t qq[D];         // Q quantized to q8_0 (q8_0 K)
+    __shared__ float qd[D / 32];
+    __shared__ float red_m[4], red_s[4];
+    __shared__ float red_o[4][D];
+
+    const float * qrow = (const float *) (a.q + iq1 * a.nbq1 + h * a.nbq2 + iq3 * a.nbq3);
+    if (a.k_type == GGML_TYPE_Q8_0) {
+        if (wave == 0) {
+            // x86 quantize_row_q8_0 on the Q row (see k_mmv.hip); lane handles D/64 values
+            for (int b = 0; b < D / 32; ++b) {
+                const float x = lane < 32 ? qrow[b * 32 + lane] : 0.0f;
+                float amax = fabsf(x);
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, WAVE));
+                const float dd = amax / 127.0f;
+                const float id = amax != 0.0f ? 127.0f / amax : 0.0f;
+                if (lane < 32) {
+                    int iv = (int) rintf(__fmul_rn(x, id));
+                    iv = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
+                    qq[b * 32 + lane] = (int8_t) iv;
+                }
+                if (lane == 0) qd[b] = h2f(f2h(dd));
+            }
+        }
+    } else {
+        for (int i = threadIdx.x; i < D; i += 256) {
+            const float x = qrow[i];
+            qf[i] = a.k_type == GGML_TYPE_F16 ? h2f(f2h(x)) : x;
+        }
+    }
+    __syncthreads();
+
+    const int64_t kv0 = chunk * a.chunk;
+    const int64_t kv1 = min(a.n_kv, kv0 + a.chunk);
+    const uint32_t hh = (uint32_t) h;
+    const float slope = a.max_bias > 0.0f ? (hh < a.n_head_log2 ? powf(a.m0, hh + 1) : powf(a.m1, 2 * (hh - a.n_head_log2) + 1)) : 1.0f;
+    const char * mrow = a.mask ? a.mask + (iq1 % a.mask_ne1) * a.nbm1 : nullptr;
+
+    float M = -INFINITY, S = 0.0f;
+    float o[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) o[e] = 0.0f;
+
+    const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
+    const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
+
+    for (int64_t t0 = kv0 + 64 * wave; t0 < kv1; t0 += 256) {
+        const int64_t pos = t0 + lane;
+        float s = -INFINITY;
+        if (pos < kv1) {
+            const float mv = mrow ? slope * h2f(*(const uint16_t *) (mrow + 2 * pos)) : 0.0f;
+            if (mv != -INFINITY) {
+                const char * krow = kbase + pos * a.nbk1;
+                float dot = 0.0f;
+                if (a.k_type == GGML_TYPE_F16) {
+#pragma unroll 4
+                    for (int d8 = 0; d8 < D / 8; ++d8) {
+                        const uint4 kv = ld16(krow + 16 * d8);
+                        const float4 qa = *(const float4 *) &qf[8 * d8];
+                        const float4 qb = *(const float4 *) &qf[8 * d8 + 4];
+                        dot = fmaf(h2f(kv.x & 0xffff), qa.x, dot); dot = fmaf(h2f(kv.x >> 16), qa.y, dot);
+                        dot = fmaf(h2f(kv.y & 0xffff), qa.z, dot); dot = fmaf(h2f(kv.y >> 16), qa.w, dot);
+                        dot = fmaf(h2f(kv.z & 0xffff), qb.x, dot); dot = fmaf(h2f(kv.z >> 16), qb.y, dot);
+                        dot = fmaf(h2f(kv.w & 0xffff), qb.z, dot); dot = fmaf(h2f(kv.w >> 16), qb.w, dot);
+                    }
+                } else if (a.k_type == GGML_TYPE_Q8_0) {
+                    for (int b = 0; b < D / 32; ++b) {
+                        const char * kb = krow + 34 * b;
+                        const float dk = h2f(ld2(kb));
+                        const uint4 k0 = ld16(kb + 2), k1 = ld16(kb + 18);
+                        const int4 q0 = *(const int4 *) &qq[32 * b];
+                        const int4 q1 = *(const int4 *) &qq[32 * b + 16];
+                        int is = 0;
+                        is = dot4(k0.x, q0.x, is); is = dot4(k0.y, q0.y, is); is = dot4(k0.z, q0.z, is); is = dot4(k0.w, q0.w, is);
+                        is = dot4(k1.x, q1.x, is); is = dot4(k1.y, q1.y, is); is = dot4(k1.z, q1.z, is); is = dot4(k1.w, q1.w, is);
+                        dot += (float) is * (dk * qd[b]);
+                    }
+                } else {  // f32 K
+                    for (int d = 0; d < D; ++d) dot = fmaf(*(const float *) (krow + 4 * d), qf[d], dot);
+                }
+                s = dot * a.scale;
+                if (a.softcap != 0.0f) s = a.softcap * tanhf(s);
+                s += mv;
+            }
+        }
+        const float tmax = wave_max(s);
+        if (tmax == -INFINITY) continue;  // whole tile masked
+        const float Mnew = fmaxf(M, tmax);
+        const float ms = M == -INFINITY ? 0.0f : expf(M - Mnew);
+        const float p = s == -INFINITY ? 0.0f : expf(s - Mnew);
+        S = S * ms + wave_sum(p);
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) o[e] *= ms;
+        M = Mnew;
+        const int nvalid = (int) min((int64_t) 64, kv1 - t0);
+        for (int j = 0; j < nvalid; ++j) {
+            const float pj = __shfl(p, j, WAVE);
+            if (pj == 0.0f) continue;  // wave-uniform
+            const char * vrow = vbase + (t0 + j) * a.nbv1;
+            if (a.v_type == GGML_TYPE_F16) {
+                if constexpr (EPL == 2) {
+                    const uint32_t vv = ld4(vrow + 4 * lane);
+                    o[0] = fmaf(pj, h2f(vv & 0xffff), o[0]);
+                    o[1] = fmaf(pj, h2f(vv >> 16), o[1]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < EPL; ++e) o[e] = fmaf(pj, h2f(ld2(vrow + 2 * (lane * EPL + e))), o[e]);
+                }
+            } else if (a.v_type == GGML_TYPE_Q8_0) {
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) {
+                    const int d = lane * EPL + e;
+                    const char * vb = vrow + 34 * (d / 32);
+                    o[e] = fmaf(pj, h2f(ld2(vb)) * (float) (int8_t) vb[2 + d % 32], o[e]);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) o[e] = fmaf(pj, *(const float *) (vrow + 4 * (lane * EPL + e)), o[e]);
+            }
+        }
+    }
+
+    // combine the 4 waves of the workgroup
+    if (lane == 0) { red_m[wave] = M; red_s[wave] = S; }
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) red_o[wave][lane * EPL + e] = o[e];
+    __syncthreads();
+    if (wave == 0) {
+        float Mt = fmaxf(fmaxf(red_m[0], red_m[1]), fmaxf(red_m[2], red_m[3]));
+        float St = 0.0f;
+        float ot[EPL];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) ot[e] = 0.0f;
+        for (int w = 0; w < 4; ++w) {
+            const float f = (red_m[w] == -INFINITY) ? 0.0f : expf(red_m[w] - Mt);
+            St += red_s[w] * f;
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) ot[e] += red_o[w][lane * EPL + e] * f;
+        }
+        if (a.nchunks == 1) {
+            const float inv = 1.0f / St;
+            float * drow = (float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H + h * a.nb1_dst + iq3 * a.nb2_dst);
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) drow[lane * EPL + e] = ot[e] * inv;
+        } else {
+            float * pr = a.part + (((chunk * a.n_q + iq1) * a.H + h) + iq3 * a.n_q * a.H * a.nchunks) * (D + 2);
+            if (lane == 0) { pr[0] = Mt; pr[1] = St; }
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) pr[2 + lane * EPL + e] = ot[e];
+        }
+    }
+}
+
+template <int EPL>
+__global__ __launch_bounds__(64) void k_fattn_combine(const fa_args a) {
+    constexpr int D = 64 * EPL;
+    const int lane = threadIdx.x;
+    const int64_t iq1 = blockIdx.x, h = blockIdx.y % a.H, iq3 = blockIdx.y / a.H;
+    float Mt = -INFINITY;
+    for (int c = 0; c < a.nchunks; ++c) {
+        const float * pr = a.part + (((c * a.n_q + iq1) * a.H + h) + iq3 * a.n_q * a.H * a.nchunks) * (D + 2);
+        Mt = fmaxf(Mt, pr[0]);
+    }
+    float St = 0.0f, ot[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) ot[e] = 0.0f;
+    for (int c = 0; c < a.nchunks; ++c) {
+        const float * pr = a.part + (((c * a.n_q + iq1) * a.H + h) + iq3 * a.n_q * a.H * a.nchunks) * (D + 2);
+        const float f = pr[0] == -INFINITY ? 0.0f : expf(pr[0] - Mt);
+        St += pr[1] * f;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) ot[e] += pr[2 + lane * EPL + e] * f;
+    }
+    const float inv = 1.0f / St;
+    float * drow = (float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H + h * a.nb1_dst + iq3 * a.nb2_dst);
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) drow[lane * EPL + e] = ot[e] * inv;
+}
+
+bool fattn_supported(const ggml_tensor * op) {
+    const ggml_tensor * q = op->src[0];
+    const ggml_tensor * k = op->src[1];
+    const ggml_tensor * v = op->src[2];
+    const ggml_tensor * mask = op->src[3];
+    if (op->src[4] != nullptr) return false;  // attention sinks not supported
+    if (q->type != GGML_TYPE_F32) return false;
+    if (k->ne[0] != v->ne[0]) return false;
+    const int64_t D = k->ne[0];
+    if (D != 64 && D != 128 && D != 256) return false;
+    if (k->type != v->type) return false;
+    if (k->type != GGML_TYPE_F16 && k->type != GGML_TYPE_Q8_0) return false;
+    if (mask && mask->type != GGML_TYPE_F16) return false;
+    if (mask && (mask->ne[2] != 1 || mask->ne[3] != 1)) return false;
+    if (q->ne[2] % k->ne[2] != 0) return false;
+    if (k->ne[3] != q->ne[3] || v->ne[3] != q->ne[3]) return false;
+    float max_bias;
+    memcpy(&max_bias, (const float *) op->op_params + 1, 4);
+    return true;
+}
+
+void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * q = dst->src[0];
+    const ggml_tensor * k = dst->src[1];
+    const ggml_tensor * v = dst->src[2];
+    const ggml_tensor * mask = dst->src[3];
+    fa_args a;
+    a.q = (const char *) q->data; a.nbq1 = q->nb[1]; a.nbq2 = q->nb[2]; a.nbq3 = q->nb[3];
+    a.k = (const char *) k->data; a.nbk1 = k->nb[1]; a.nbk2 = k->nb[2]; a.nbk3 = k->nb[3];
+    a.v = (const char *) v->data; a.nbv1 = v->nb[1]; a.nbv2 = v->nb[2]; a.nbv3 = v->nb[3];
+    a.mask = mask ? (const char *) mask->data : nullptr;
+    a.nbm1 = mask ? mask->nb[1] : 0;
+    a.mask_ne1 = mask ? mask->ne[1] : 1;
+    a.k_type = k->type; a.v_type = v->type;
+    a.D = k->ne[0]; a.n_kv = k->ne[1]; a.n_q = q->ne[1]; a.H = q->ne[2]; a.Hkv = k->ne[2];
+    memcpy(&a.scale, (const float *) dst->op_params + 0, 4);
+    memcpy(&a.max_bias, (const float *) dst->op_params + 1, 4);
+    memcpy(&a.softcap, (const float *) dst->op_params + 2, 4);
+    if (a.softcap != 0.0f) a.scale /= a.softcap;
+    const uint32_t n_head = (uint32_t) a.H;
+    a.n_head_log2 = 1u << (uint32_t) floor(log2((double) n_head));
+    a.m0 = powf(2.0f, -(a.max_bias) / a.n_head_log2);
+    a.m1 = powf(2.0f, -(a.max_bias / 2.0f) / a.n_head_log2);
+    a.dst = (float *) dst->data;
+    a.nb1_dst = dst->nb[1];
+    a.nb2_dst = dst->nb[3];  // batch stride (dst ne = [D, H, n_q, ne3])
+    const int64_t nq3 = q->ne[3];
+
+    // split-K over the cache so that decode fills the 256 CUs
+    const int64_t rows = a.n_q * a.H * nq3;
+    int64_t nchunks = 1;
+    if (rows < 1024) nchunks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(a.n_kv, 256), ceil_div(1024, rows)));
+    a.chunk = ceil_div(ceil_div(a.n_kv, nchunks), 64) * 64;
+    nchunks = ceil_div(a.n_kv, a.chunk);
+    a.nchunks = (int) nchunks;
+    a.part = nullptr;
+    if (nchunks > 1) a.part = (float *) ctx.scratch(1, sizeof(float) * nchunks * rows * (a.D + 2));
+
+    hipEvent_t ev = nullptr;
+    const double bytes = (double) (ggml_nbytes(k) + ggml_nbytes(v)) + (double) ggml_nbytes(q) + (double) ggml_nbytes(dst);
+    if (ctx.timing) ctx.time_begin(TK_FATTN, bytes, ev);
+    dim3 grid((unsigned) nchunks, (unsigned) a.n_q, (unsigned) (a.H * nq3));
+    switch (a.D) {
+        case 64:  hipLaunchKernelGGL(k_fattn_vec<1>, grid, dim3(256), 0, ctx.stream, a); break;
+        case 128: hipLaunchKernelGGL(k_fattn_vec<2>, grid, dim3(256), 0, ctx.stream, a); break;
+        case 256: hipLaunchKernelGGL(k_fattn_vec<4>, grid, dim3(256), 0, ctx.stream, a); break;
+        default: GGML_ABORT("mi355x: FA head size");
+    }
+    if (nchunks > 1) {
+        dim3 g2((unsigned) a.n_q, (unsigned) (a.H * nq3));
+        switch (a.D) {
+            case 64:  hipLaunchKernelGGL(k_fattn_combine<1>, g2, dim3(64), 0, ctx.stream, a); break;
+            case 128: hipLaunchKernelGGL(k_fattn_combine<2>, g2, dim3(64), 0, ctx.stream, a); break;
+            case 256: hipLaunchKernelGGL(k_fattn_combine<4>, g2, dim3(64), 0, ctx.stream, a); break;
+        }
+    }
+    if (ctx.timing) ctx.time_end(TK_FATTN, bytes, ev);
+}
+
+}  // namespace mi355x
