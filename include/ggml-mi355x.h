@@ -40,6 +40,43 @@ void ggml_backend_mi355x_set_timing(int enable);
 void ggml_backend_mi355x_reset_timing(void);
 int  ggml_backend_mi355x_get_timing(int kind, double * ms, double * bytes, long * count);
 
+// ---- flat kernel ABI (llamacog_amd/csrc/capi.cpp) ---------------------------------------------
+// Plain device pointers + sizes + a HIP stream (NULL = private stream, synchronised on
+// return).  Each call builds the ggml node the reference graph would contain and runs the
+// same launcher graph_compute runs.  Layouts are row-major, outermost index first.
+void * mi355x_dev_alloc(size_t bytes);
+void   mi355x_dev_free(void * p);
+void   mi355x_h2d(void * dst, const void * src, size_t n);
+void   mi355x_d2h(void * dst, const void * src, size_t n);
+void   mi355x_memset(void * dst, int v, size_t n);
+void   mi355x_sync(void);
+
+// activation quantization (replaces ggml-cpu's from_float for the vec_dot_type,
+// ggml-cpu/ggml-cpu.c:1254-1289): vdt = 15 (Q8_K) or 8 (Q8_0); output is SoA:
+// qs[nrows][k] int8, d[nrows][k/blk] f32, s[nrows][k/16 (Q8_K) | k/32 (Q8_0)] int16
+int mi355x_quantize_rows(int vdt, const float * x, int64_t k, int64_t nrows, void * qs, void * d, void * s, void * stream);
+// MUL_MAT (ggml-cpu/ggml-cpu.c:1192-1384): y[T][M] = W[M][K] . X[T][K]
+int mi355x_mul_mat(int wtype, const void * w, int64_t K, int64_t M, const float * x, int64_t T, float * y, void * stream);
+// RMS_NORM (ops.cpp:3270-3316), optionally fused with the following MUL by w[ne0]
+int mi355x_rms_norm(const float * x, int64_t ne0, int64_t nrows, float eps, const float * w, float * y, float * y_mul,
+                    void * stream);
+// ROPE (ops.cpp:5178-5362), x [n_tok][n_head][ne0]
+int mi355x_rope(const float * x, int64_t ne0, int64_t n_head, int64_t n_tok, const int32_t * pos, int n_dims, int mode,
+                int n_ctx_orig, float freq_base, float freq_scale, float ext_factor, float attn_factor, float beta_fast,
+                float beta_slow, const float * ff, float * y, void * stream);
+// SOFT_MAX (ops.cpp:4731-4827), x viewed as [nr/mask_rows][mask_rows][nc]
+int mi355x_soft_max(const float * x, int64_t nc, int64_t nr, const float * mask, int64_t mask_rows, float scale, float * y,
+                    void * stream);
+// UNARY SILU (ops.cpp:2902, vec.cpp:233)
+int mi355x_silu(const float * x, int64_t ne0, int64_t nrows, float * y, void * stream);
+// FLASH_ATTN_EXT (ops.cpp:7015-7232): q [n_q][H][D] f32, k/v [n_kv][Hkv][D] f16 (1) or q8_0 (8),
+// mask [n_q][n_kv] f16 or NULL, out [n_q][H][D]
+// test hook: phase-1 scores of the CPU-exact flash attention (q [128] f32, k [n][128] f16)
+int mi355x_fa_scores_d128(const float * q, const uint16_t * k, int64_t n, float * s, void * stream);
+int mi355x_flash_attn(const float * q, const void * k, const void * v, const uint16_t * mask, int kv_type, int64_t D,
+                      int64_t n_q, int64_t H, int64_t n_kv, int64_t Hkv, float scale, float softcap, float * out,
+                      void * stream);
+
 #ifdef __cplusplus
 }
 #endif

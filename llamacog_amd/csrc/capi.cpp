@@ -1,0 +1,221 @@
+// capi.cpp — flat C ABI over the MI355X kernels for parity tests and microbenchmarks.
+//
+// Each entry point takes plain device pointers, sizes and a HIP stream (NULL = a private
+// stream), wraps them in stack-allocated ggml_tensor descriptors with the reference's
+// layout (ggml.h:576-608) and runs exactly the launcher graph_compute would run for that
+// node, so tests exercise the product path without a ggml context or graph.
+#include "ops.h"
+#include "../../include/ggml-mi355x.h"
+
+#include <cstring>
+
+using namespace mi355x;
+
+namespace mi355x {
+bool mmv_q_supported_type(ggml_type t);
+void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int64_t n, float * s);
+}
+
+static void init_tensor(ggml_tensor & t, ggml_type type, const int64_t ne[4], void * data) {
+    memset(&t, 0, sizeof(t));
+    t.type = type;
+    for (int i = 0; i < 4; ++i) t.ne[i] = ne[i];
+    t.nb[0] = ggml_type_size(type);
+    t.nb[1] = t.nb[0] * (t.ne[0] / ggml_blck_size(type));
+    for (int i = 2; i < 4; ++i) t.nb[i] = t.nb[i - 1] * t.ne[i - 1];
+    t.data = data;
+}
+
+struct scoped_ctx {
+    exec_ctx ex;
+    bool own = false;
+    explicit scoped_ctx(void * stream) {
+        if (stream) {
+            ex.stream = (hipStream_t) stream;
+        } else {
+            MI_CHECK(hipStreamCreateWithFlags(&ex.stream, hipStreamNonBlocking));
+            own = true;
+        }
+    }
+    ~scoped_ctx() {
+        MI_CHECK(hipStreamSynchronize(ex.stream));
+        ex.free_scratch();
+        if (own) MI_CHECK(hipStreamDestroy(ex.stream));
+    }
+};
+
+extern "C" {
+
+// ---- device memory helpers (so tests need no other HIP binding) ----------------------------
+GGML_BACKEND_API void * mi355x_dev_alloc(size_t bytes) {
+    void * p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    return p;
+}
+GGML_BACKEND_API void mi355x_dev_free(void * p) { MI_CHECK(hipFree(p)); }
+GGML_BACKEND_API void mi355x_h2d(void * dst, const void * src, size_t n) { MI_CHECK(hipMemcpy(dst, src, n, hipMemcpyHostToDevice)); }
+GGML_BACKEND_API void mi355x_d2h(void * dst, const void * src, size_t n) { MI_CHECK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost)); }
+GGML_BACKEND_API void mi355x_memset(void * dst, int v, size_t n) { MI_CHECK(hipMemset(dst, v, n)); }
+GGML_BACKEND_API void mi355x_sync(void) { MI_CHECK(hipDeviceSynchronize()); }
+
+// ---- activation quantization: nrows rows of k floats -> SoA (qs [nrows][k] int8,
+// d [nrows][k/blk] f32, s [nrows][k/grp] i16); vdt = GGML_TYPE_Q8_K (15) or Q8_0 (8)
+GGML_BACKEND_API int mi355x_quantize_rows(int vdt, const float * x, int64_t k, int64_t nrows, void * qs, void * d,
+                                          void * s, void * stream) {
+    const bool kq = vdt == GGML_TYPE_Q8_K;
+    if (!kq && vdt != GGML_TYPE_Q8_0) return -1;
+    if (k % (kq ? 256 : 32) != 0) return -2;
+    scoped_ctx sc(stream);
+    q8_act act;
+    act.qs = (int8_t *) qs; act.d = (float *) d; act.s = (int16_t *) s; act.K = k; act.ncols = nrows; act.k_quant = kq;
+    quantize_act_raw(sc.ex.stream, x, k, nrows, k, kq, act);
+    return 0;
+}
+
+// ---- y[T][M] = W[M][K] (ggml_type wtype rows) x X[T][K]  — MUL_MAT node ---------------------
+GGML_BACKEND_API int mi355x_mul_mat(int wtype, const void * w, int64_t K, int64_t M, const float * x, int64_t T, float * y,
+                                    void * stream) {
+    ggml_tensor W, X, Y;
+    const int64_t new_[4] = {K, M, 1, 1}, nex[4] = {K, T, 1, 1}, ney[4] = {M, T, 1, 1};
+    init_tensor(W, (ggml_type) wtype, new_, (void *) w);
+    init_tensor(X, GGML_TYPE_F32, nex, (void *) x);
+    init_tensor(Y, GGML_TYPE_F32, ney, y);
+    Y.op = GGML_OP_MUL_MAT;
+    Y.src[0] = &W;
+    Y.src[1] = &X;
+    if (!op_supported(&Y)) return -1;
+    scoped_ctx sc(stream);
+    op_mul_mat(sc.ex, &Y);
+    return 0;
+}
+
+// ---- rms_norm over nrows rows (optionally fused with a weight vector w[ne0]) ---------------
+GGML_BACKEND_API int mi355x_rms_norm(const float * x, int64_t ne0, int64_t nrows, float eps, const float * w, float * y,
+                                     float * y_mul, void * stream) {
+    ggml_tensor X, Y, Wt, Ym;
+    const int64_t ne[4] = {ne0, nrows, 1, 1}, new_[4] = {ne0, 1, 1, 1};
+    init_tensor(X, GGML_TYPE_F32, ne, (void *) x);
+    init_tensor(Y, GGML_TYPE_F32, ne, y);
+    Y.op = GGML_OP_RMS_NORM;
+    Y.src[0] = &X;
+    memcpy(Y.op_params, &eps, sizeof(float));
+    scoped_ctx sc(stream);
+    if (w) {
+        init_tensor(Wt, GGML_TYPE_F32, new_, (void *) w);
+        init_tensor(Ym, GGML_TYPE_F32, ne, y_mul);
+        op_rms_norm(sc.ex, &Y, &Wt, &Ym);
+    } else {
+        op_rms_norm(sc.ex, &Y, nullptr, nullptr);
+    }
+    return 0;
+}
+
+// ---- rope: x [n_tok][n_head][ne0] (ggml [ne0, n_head, n_tok]) -------------------------------
+GGML_BACKEND_API int mi355x_rope(const float * x, int64_t ne0, int64_t n_head, int64_t n_tok, const int32_t * pos,
+                                 int n_dims, int mode, int n_ctx_orig, float freq_base, float freq_scale, float ext_factor,
+                                 float attn_factor, float beta_fast, float beta_slow, const float * ff, float * y,
+                                 void * stream) {
+    ggml_tensor X, P, F, Y;
+    const int64_t ne[4] = {ne0, n_head, n_tok, 1}, nep[4] = {n_tok, 1, 1, 1}, nef[4] = {n_dims / 2, 1, 1, 1};
+    init_tensor(X, GGML_TYPE_F32, ne, (void *) x);
+    init_tensor(P, GGML_TYPE_I32, nep, (void *) pos);
+    init_tensor(Y, GGML_TYPE_F32, ne, y);
+    Y.op = GGML_OP_ROPE;
+    Y.src[0] = &X;
+    Y.src[1] = &P;
+    if (ff) {
+        init_tensor(F, GGML_TYPE_F32, nef, (void *) ff);
+        Y.src[2] = &F;
+    }
+    int32_t * op = Y.op_params;
+    op[1] = n_dims; op[2] = mode; op[4] = n_ctx_orig;
+    memcpy(op + 5, &freq_base, 4); memcpy(op + 6, &freq_scale, 4); memcpy(op + 7, &ext_factor, 4);
+    memcpy(op + 8, &attn_factor, 4); memcpy(op + 9, &beta_fast, 4); memcpy(op + 10, &beta_slow, 4);
+    if (!op_supported(&Y)) return -1;
+    scoped_ctx sc(stream);
+    op_rope(sc.ex, &Y);
+    return 0;
+}
+
+// ---- soft_max_ext: x viewed as ggml [nc, mask_rows, nr/mask_rows]; mask [mask_rows][nc] f32
+GGML_BACKEND_API int mi355x_soft_max(const float * x, int64_t nc, int64_t nr, const float * mask, int64_t mask_rows,
+                                     float scale, float * y, void * stream) {
+    ggml_tensor X, Mk, Y;
+    const int64_t ne[4] = {nc, mask_rows, nr / mask_rows, 1}, nem[4] = {nc, mask_rows, 1, 1};
+    init_tensor(X, GGML_TYPE_F32, ne, (void *) x);
+    init_tensor(Y, GGML_TYPE_F32, ne, y);
+    Y.op = GGML_OP_SOFT_MAX;
+    Y.src[0] = &X;
+    if (mask) {
+        init_tensor(Mk, GGML_TYPE_F32, nem, (void *) mask);
+        Y.src[1] = &Mk;
+    }
+    const float mb = 0.0f;
+    memcpy(Y.op_params, &scale, 4);
+    memcpy(Y.op_params + 1, &mb, 4);
+    scoped_ctx sc(stream);
+    op_soft_max(sc.ex, &Y);
+    return 0;
+}
+
+// ---- unary SiLU over n floats ------------------------------------------------------------------
+GGML_BACKEND_API int mi355x_silu(const float * x, int64_t ne0, int64_t nrows, float * y, void * stream) {
+    ggml_tensor X, Y;
+    const int64_t ne[4] = {ne0, nrows, 1, 1};
+    init_tensor(X, GGML_TYPE_F32, ne, (void *) x);
+    init_tensor(Y, GGML_TYPE_F32, ne, y);
+    Y.op = GGML_OP_UNARY;
+    Y.src[0] = &X;
+    Y.op_params[0] = GGML_UNARY_OP_SILU;
+    scoped_ctx sc(stream);
+    op_unary(sc.ex, &Y);
+    return 0;
+}
+
+// ---- flash_attn_ext: q [n_q][H][D] f32, k/v [n_kv][Hkv][D] (f16 or q8_0 rows),
+// mask [n_q][n_kv] f16 (rows padded to 64 internally by the caller or not at all),
+// out [n_q][H][D] f32 — the layout llama's graph hands to FLASH_ATTN_EXT
+GGML_BACKEND_API int mi355x_flash_attn(const float * q, const void * k, const void * v, const uint16_t * mask, int kv_type,
+                                       int64_t D, int64_t n_q, int64_t H, int64_t n_kv, int64_t Hkv, float scale,
+                                       float softcap, float * out, void * stream) {
+    ggml_tensor Q, K, V, Mk, O;
+    // q: [D, H, n_q] permuted to [D, n_q, H]
+    const int64_t neq[4] = {D, H, n_q, 1};
+    init_tensor(Q, GGML_TYPE_F32, neq, (void *) q);
+    std::swap(Q.ne[1], Q.ne[2]);
+    std::swap(Q.nb[1], Q.nb[2]);
+    const int64_t nek[4] = {D, Hkv, n_kv, 1};
+    init_tensor(K, (ggml_type) kv_type, nek, (void *) k);
+    std::swap(K.ne[1], K.ne[2]);
+    std::swap(K.nb[1], K.nb[2]);
+    init_tensor(V, (ggml_type) kv_type, nek, (void *) v);
+    std::swap(V.ne[1], V.ne[2]);
+    std::swap(V.nb[1], V.nb[2]);
+    const int64_t nem[4] = {n_kv, n_q, 1, 1};
+    const int64_t neo[4] = {D, H, n_q, 1};
+    init_tensor(O, GGML_TYPE_F32, neo, out);
+    O.op = GGML_OP_FLASH_ATTN_EXT;
+    O.src[0] = &Q; O.src[1] = &K; O.src[2] = &V;
+    if (mask) {
+        init_tensor(Mk, GGML_TYPE_F16, nem, (void *) mask);
+        O.src[3] = &Mk;
+    }
+    const float mb = 0.0f;
+    memcpy(O.op_params, &scale, 4);
+    memcpy(O.op_params + 1, &mb, 4);
+    memcpy(O.op_params + 2, &softcap, 4);
+    O.op_params[3] = GGML_PREC_F32;
+    if (!op_supported(&O)) return -1;
+    scoped_ctx sc(stream);
+    op_flash_attn(sc.ex, &O);
+    return 0;
+}
+
+// test hook: K·Q scores of the CPU-exact flash-attention kernel (f16 K rows of 128)
+GGML_BACKEND_API int mi355x_fa_scores_d128(const float * q, const uint16_t * k, int64_t n, float * s, void * stream) {
+    scoped_ctx sc(stream);
+    fattn_scores_d128(sc.ex.stream, q, k, n, s);
+    return 0;
+}
+
+}  // extern "C"

@@ -79,6 +79,33 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// ggml_v_expf of the AVX-512 CPU backend (ggml-cpu/vec.h:731-756), bit-exact: the
+// reference's SiLU and soft_max use it, not libm expf.
+__device__ __forceinline__ float v_expf_avx512(float x) {
+    const float r = 0x1.8p23f;
+    const float z = fmaf(x, 0x1.715476p+0f, r);
+    const float n = __fsub_rn(z, r);
+    const float b = fmaf(-n, 0x1.7f7d1cp-20f, fmaf(-n, 0x1.62e4p-1f, x));
+    const float u = __fmul_rn(b, b);
+    const float j = fmaf(fmaf(fmaf(0x1.0e4020p-7f, b, 0x1.573e2ep-5f), u, fmaf(0x1.555e66p-3f, b, 0x1.fffdb6p-2f)), u,
+                         fmaf(0x1.ffffecp-1f, b, 1.0f));
+    if (fabsf(n) > 192.0f) return n <= 0.0f ? 0.0f : INFINITY;
+    return ldexpf(j, (int) n);  // _mm512_scalef_ps(j, n)
+}
+
+// float(exp(double(x))): libm expf as used by the CPU backend's scalar paths
+__device__ __forceinline__ float expf_cr(float x) { return (float) exp((double) x); }
+
+// the _mm512_reduce_add_ps tree (GCC avx512fintrin.h) over 16 lane values
+__device__ __forceinline__ float reduce16_avx512(const float (&w)[16]) {
+    float t3[8], t6[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t3[i] = __fadd_rn(w[8 + i], w[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t6[i] = __fadd_rn(t3[4 + i], t3[i]);
+    return __fadd_rn(__fadd_rn(t6[0], t6[2]), __fadd_rn(t6[1], t6[3]));
+}
+
 // 6-bit scale/min unpack of Q4_K/Q5_K (ggml-quants.c:625 get_scale_min_k4)
 __device__ __forceinline__ void scale_min_k4(int j, const uint8_t * q, int & d, int & m) {
     if (j < 4) {

@@ -71,7 +71,7 @@ enum un_op { UN_SILU = 0, UN_GELU, UN_RELU, UN_NEG, UN_TANH, UN_SIGMOID, UN_SCAL
 
 template <int OP>
 __device__ __forceinline__ float un_apply(float x, float s) {
-    if constexpr (OP == UN_SILU) return x / (1.0f + expf(-x));                       // vec.h ggml_silu_f32
+    if constexpr (OP == UN_SILU) return x / (1.0f + v_expf_avx512(-x));              // vec.h:759 ggml_v_silu
     else if constexpr (OP == UN_RELU) return x > 0.0f ? x : 0.0f;
     else if constexpr (OP == UN_NEG) return -x;
     else if constexpr (OP == UN_TANH) return tanhf(x);
@@ -95,8 +95,13 @@ __global__ __launch_bounds__(256) void k_unary(const char * __restrict__ a, t4 t
     const int64_t i1 = r % td.ne[1], i2 = (r / td.ne[1]) % td.ne[2], i3 = r / (td.ne[1] * td.ne[2]);
     const char * ar = a + i1 * ta.nb[1] + i2 * ta.nb[2] + i3 * ta.nb[3];
     char * dr = d + i1 * td.nb[1] + i2 * td.nb[2] + i3 * td.nb[3];
+    const int64_t nvec = (td.ne[0] / 16) * 16;  // ggml_vec_silu_f32: 16-wide SIMD body, scalar tail
     for (int64_t i0 = threadIdx.x; i0 < td.ne[0]; i0 += blockDim.x) {
-        *(float *) (dr + i0 * td.nb[0]) = un_apply<OP>(*(const float *) (ar + i0 * ta.nb[0]), s);
+        const float x = *(const float *) (ar + i0 * ta.nb[0]);
+        float yv;
+        if constexpr (OP == UN_SILU) yv = i0 < nvec ? un_apply<OP>(x, s) : x / (1.0f + expf_cr(-x));
+        else yv = un_apply<OP>(x, s);
+        *(float *) (dr + i0 * td.nb[0]) = yv;
     }
 }
 
@@ -416,8 +421,9 @@ __device__ __forceinline__ void rope_yarn_dev(float theta_extrap, float freq_sca
         theta = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
         mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
     }
-    c = cosf(theta) * mscale;
-    s = sinf(theta) * mscale;
+    // libm cosf/sinf of the CPU backend: take them in double and round once
+    c = __fmul_rn((float) cos((double) theta), mscale);
+    s = __fmul_rn((float) sin((double) theta), mscale);
 }
 
 __global__ __launch_bounds__(256) void k_rope(const char * __restrict__ x, t4 tx, char * __restrict__ y, t4 ty,
@@ -442,8 +448,10 @@ __global__ __launch_bounds__(256) void k_rope(const char * __restrict__ x, t4 tx
             else      { a0 = i0; a1 = i0 + 1; }
             const float x0 = *(const float *) (xr + a0 * tx.nb[0]);
             const float x1 = *(const float *) (xr + a1 * tx.nb[0]);
-            *(float *) (yr + a0 * ty.nb[0]) = x0 * c - x1 * s;
-            *(float *) (yr + a1 * ty.nb[0]) = x0 * s + x1 * c;
+            // the reference's x86-64-v4 build contracts these as below (bit-exact vs
+            // tests/golden/rope.npz)
+            *(float *) (yr + a0 * ty.nb[0]) = fmaf(x0, c, -__fmul_rn(x1, s));
+            *(float *) (yr + a1 * ty.nb[0]) = fmaf(x0, s, __fmul_rn(x1, c));
         } else {
             *(float *) (yr + i0 * ty.nb[0])       = *(const float *) (xr + i0 * tx.nb[0]);
             *(float *) (yr + (i0 + 1) * ty.nb[0]) = *(const float *) (xr + (i0 + 1) * tx.nb[0]);
@@ -498,8 +506,8 @@ __global__ __launch_bounds__(256) void k_soft_max(const char * __restrict__ x, t
     __shared__ double redd[4];
     float mx = -INFINITY;
     for (int64_t i = threadIdx.x; i < nc; i += 256) {
-        float w = xr[i] * scale;
-        if (mr) w += slope * (mask_f16 ? h2f(*(const uint16_t *) (mr + 2 * i)) : *(const float *) (mr + 4 * i));
+        float w = __fmul_rn(xr[i], scale);
+        if (mr) w = __fadd_rn(w, __fmul_rn(slope, mask_f16 ? h2f(*(const uint16_t *) (mr + 2 * i)) : *(const float *) (mr + 4 * i)));
         yr[i] = w;
         mx = fmaxf(mx, w);
     }
@@ -507,19 +515,42 @@ __global__ __launch_bounds__(256) void k_soft_max(const char * __restrict__ x, t
     if ((threadIdx.x & 63) == 0) redf[threadIdx.x >> 6] = mx;
     __syncthreads();
     mx = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+    // ggml_vec_soft_max_f32 (vec.cpp:257-300, AVX-512): 16-wide chunks of ggml_v_expf, each
+    // chunk reduced by _mm512_reduce_add_ps and accumulated in double in chunk order; the
+    // n % 16 tail uses libm expf.  Chunk sums go to LDS and one thread adds them in order.
+    constexpr int MAXCH = 4096;
+    __shared__ float csum[MAXCH];
+    const int64_t nch = nc / 16;
     double sum = 0.0;
-    for (int64_t i = threadIdx.x; i < nc; i += 256) {
-        const float e = expf(yr[i] - mx);
-        yr[i] = e;
-        sum += (double) e;
+    for (int64_t c = threadIdx.x; c < nch; c += 256) {
+        float w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            w[k] = v_expf_avx512(__fsub_rn(yr[16 * c + k], mx));
+            yr[16 * c + k] = w[k];
+        }
+        const float cs = reduce16_avx512(w);
+        if (c < MAXCH) csum[c] = cs;
+        else sum += (double) cs;  // beyond MAXCH chunks: order-approximate double sum
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
     if ((threadIdx.x & 63) == 0) redd[threadIdx.x >> 6] = sum;
     __syncthreads();
-    sum = redd[0] + redd[1] + redd[2] + redd[3];
-    const float inv = (float) (1.0 / sum);
-    for (int64_t i = threadIdx.x; i < nc; i += 256) yr[i] *= inv;
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int64_t c = 0; c < min(nch, (int64_t) MAXCH); ++c) s += (double) csum[c];
+        s += redd[0] + redd[1] + redd[2] + redd[3];
+        for (int64_t i = 16 * nch; i < nc; ++i) {
+            const float e = expf_cr(__fsub_rn(yr[i], mx));
+            yr[i] = e;
+            s += (double) e;
+        }
+        redd[0] = s;
+    }
+    __syncthreads();
+    const float inv = (float) (1.0 / redd[0]);
+    for (int64_t i = threadIdx.x; i < nc; i += 256) yr[i] = __fmul_rn(yr[i], inv);
 }
 
 void op_soft_max(exec_ctx & ctx, ggml_tensor * dst) {

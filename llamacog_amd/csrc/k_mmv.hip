@@ -552,6 +552,45 @@ __global__ __launch_bounds__(256) void k_mmv_f(const mmv_f_args p) {
 }
 
 // ------------------------------------------------------------------------------------------
+// f16 / f32 weights, CPU-exact order: the CPU converts src1 to the weight's vec_dot_type
+// (f16 for f16 weights) and takes ggml_vec_dot_f16 / ggml_vec_dot_f32 (vec.cpp:191-231,
+// AVX-512: 16 lanes x 4 f32 accumulators, REDUCE tree, double leftovers).  One thread per
+// (row, column) reproduces that order exactly.  Used for the FA-off KQ / KQV products and
+// for f16/f32 weight matrices (not on the FA decode hot path).
+// ------------------------------------------------------------------------------------------
+template <typename WT>
+__global__ __launch_bounds__(256) void k_mmv_f_exact(const mmv_f_args p) {
+    const int64_t row = (int64_t) blockIdx.x * 256 + threadIdx.x;
+    const int64_t c = blockIdx.y;
+    const int64_t i12 = blockIdx.z % p.ne12, i13 = blockIdx.z / p.ne12;
+    if (row >= p.M) return;
+    const char * wrow = p.W + (i12 / p.r2) * p.nb02 + (i13 / p.r3) * p.nb03 + row * p.nb01;
+    const float * x = (const float *) (p.X + i12 * p.nb12 + i13 * p.nb13 + c * p.nb11);
+    auto wv = [&](int64_t k) -> float {
+        if constexpr (sizeof(WT) == 2) return h2f(ld2(wrow + 2 * k));
+        else return __uint_as_float(ld4(wrow + 4 * k));
+    };
+    auto xv = [&](int64_t k) -> float {
+        if constexpr (sizeof(WT) == 2) return h2f(f2h(x[k]));  // src1 -> f16 (vec_dot_type)
+        else return x[k];
+    };
+    const int64_t np = p.K & ~int64_t(63);
+    float acc[64];
+#pragma unroll
+    for (int s = 0; s < 64; ++s) acc[s] = 0.0f;
+    for (int64_t i = 0; i < np; i += 64) {
+#pragma unroll
+        for (int s = 0; s < 64; ++s) acc[s] = fmaf(wv(i + s), xv(i + s), acc[s]);
+    }
+    float w[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) w[l] = __fadd_rn(__fadd_rn(acc[l], acc[32 + l]), __fadd_rn(acc[16 + l], acc[48 + l]));
+    double sumf = (double) reduce16_avx512(w);
+    for (int64_t k = np; k < p.K; ++k) sumf += (double) __fmul_rn(wv(k), xv(k));
+    *(float *) ((char *) p.dst + i12 * p.nb2 + i13 * p.nb3 + c * p.nb1 + row * 4) = (float) sumf;
+}
+
+// ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
 static int64_t total_rows_waves(int64_t M, int64_t ncolgroups, int64_t nbatch) { return M * ncolgroups * nbatch; }
@@ -664,8 +703,15 @@ void mul_mat_vec(exec_ctx & ctx, ggml_tensor * dst, const q8_act * pre) {
         a.ne11 = src1->ne[1]; a.ne12 = src1->ne[2];
         a.r2 = src1->ne[2] / src0->ne[2]; a.r3 = src1->ne[3] / src0->ne[3];
         a.dst = (float *) dst->data; a.nb1 = dst->nb[1]; a.nb2 = dst->nb[2]; a.nb3 = dst->nb[3];
-        if (src0->type == GGML_TYPE_F16) launch_mmv_f<uint16_t>(ctx.stream, a, a.ne11, nbatch);
-        else launch_mmv_f<float>(ctx.stream, a, a.ne11, nbatch);
+        static const bool fast = getenv("GGML_MI355X_MMF_FAST") != nullptr;
+        if (fast) {
+            if (src0->type == GGML_TYPE_F16) launch_mmv_f<uint16_t>(ctx.stream, a, a.ne11, nbatch);
+            else launch_mmv_f<float>(ctx.stream, a, a.ne11, nbatch);
+        } else {
+            dim3 grid((unsigned) ceil_div(a.M, 256), (unsigned) a.ne11, (unsigned) nbatch);
+            if (src0->type == GGML_TYPE_F16) hipLaunchKernelGGL(k_mmv_f_exact<uint16_t>, grid, dim3(256), 0, ctx.stream, a);
+            else hipLaunchKernelGGL(k_mmv_f_exact<float>, grid, dim3(256), 0, ctx.stream, a);
+        }
     }
     if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
 }

@@ -1,0 +1,582 @@
+/*
+ * ggml_oracle.c — CPU restatement of the reference's quantized LLaMA hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libggml-mi355x.so, bench.py's GPU
+ * leg) links, loads or calls this file; only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may.  It is the parity checker for the HIP kernels.
+ *
+ * Every function restates the reference's scalar arithmetic (file:line in the reference
+ * tree /root/reference) so the integer parts are bit-exact with the CPU backend and the
+ * float parts follow the same operation order.  Pinned against golden vectors produced by
+ * the reference CPU backend itself (oracle/gen_golden.c, tests/golden/*.npz).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define QK_K 256
+#define MAXF(a, b) ((a) > (b) ? (a) : (b))
+#define MINF(a, b) ((a) < (b) ? (a) : (b))
+
+/* ggml_type ids, ggml/include/ggml.h:351-392 */
+enum { T_F32 = 0, T_F16 = 1, T_Q4_0 = 2, T_Q8_0 = 8, T_Q4_K = 12, T_Q5_K = 13, T_Q6_K = 14, T_Q8_K = 15 };
+
+/* ---- fp16 <-> fp32, round-to-nearest-even (F16C _cvtss_sh(x, 0) / _cvtsh_ss) ---------------- */
+static inline float fp32_from_bits(uint32_t w) { float f; memcpy(&f, &w, 4); return f; }
+static inline uint32_t fp32_to_bits(float f) { uint32_t w; memcpy(&w, &f, 4); return w; }
+
+float orc_fp16_to_fp32(uint16_t h) {
+    const uint32_t sign = (uint32_t) (h & 0x8000) << 16;
+    uint32_t exp = (h >> 10) & 0x1f, man = h & 0x3ff;
+    if (exp == 0) {
+        if (man == 0) return fp32_from_bits(sign);
+        /* subnormal */
+        float v = ldexpf((float) man, -24);
+        return sign ? -v : v;
+    }
+    if (exp == 31) return fp32_from_bits(sign | 0x7f800000u | (man << 13));
+    return fp32_from_bits(sign | ((exp + 112) << 23) | (man << 13));
+}
+
+uint16_t orc_fp32_to_fp16(float f) {
+    const uint32_t x = fp32_to_bits(f);
+    const uint32_t sign = (x >> 16) & 0x8000;
+    const uint32_t ax = x & 0x7fffffff;
+    if (ax >= 0x7f800000u) return (uint16_t) (sign | (ax > 0x7f800000u ? 0x7e00 : 0x7c00)); /* nan/inf */
+    if (ax >= 0x477ff000u) return (uint16_t) (sign | 0x7c00);                               /* overflow */
+    if (ax < 0x38800000u) {
+        /* subnormal half: value = ax_float / 2^-24 rounded to nearest even */
+        const float v = fp32_from_bits(ax);
+        const float s = v * 16777216.0f; /* exact scaling by 2^24 */
+        float r = rintf(s);              /* RNE */
+        return (uint16_t) (sign | (uint32_t) r);
+    }
+    /* normal: round mantissa 23 -> 10 bits, RNE */
+    uint32_t m = ax + 0xfffu + ((ax >> 13) & 1);
+    m -= 0x38000000u; /* rebias 127 -> 15 */
+    return (uint16_t) (sign | (m >> 13));
+}
+
+/* ---- x86-64-v4 (AVX-512) arithmetic of the CPU backend the reference selects on the
+ * MI355X host (refhost libggml-cpu-x64v4.so) ---------------------------------------------- */
+/* _mm512_reduce_add_ps (GCC avx512fintrin.h): 8 / 4 / 2 / 1 tree */
+static float reduce16(const float * w) {
+    float t3[8], t6[4];
+    for (int i = 0; i < 8; ++i) t3[i] = w[8 + i] + w[i];
+    for (int i = 0; i < 4; ++i) t6[i] = t3[4 + i] + t3[i];
+    return (t6[0] + t6[2]) + (t6[1] + t6[3]);
+}
+
+/* ggml_vec_dot_f16 / ggml_vec_dot_f32 with GGML_F16_STEP 64, EPR 16 (vec.cpp:191-231,
+ * simd-mappings.h AVX512F): 4 accumulators x 16 lanes of f32 FMAs, REDUCE, double leftovers */
+static float dot_avx512(const float * x, const float * y, int64_t n) {
+    float acc[64];
+    const int64_t np = n & ~(int64_t) 63;
+    for (int s = 0; s < 64; ++s) acc[s] = 0.0f;
+    for (int64_t i = 0; i < np; i += 64)
+        for (int s = 0; s < 64; ++s) acc[s] = fmaf(x[i + s], y[i + s], acc[s]);
+    float w[16];
+    for (int l = 0; l < 16; ++l) w[l] = (acc[l] + acc[32 + l]) + (acc[16 + l] + acc[48 + l]);
+    double sumf = reduce16(w);
+    for (int64_t i = np; i < n; ++i) sumf += (double) (x[i] * y[i]);
+    return (float) sumf;
+}
+
+/* K·Q of the CPU flash-attention for an f16 cache: Q rounded to f16, ggml_vec_dot_f16 */
+void orc_fa_scores(const float * q, const uint16_t * k, int64_t n, int64_t D, float * s);
+
+/* ggml_v_expf, AVX-512 variant (ggml-cpu/vec.h:731-756) */
+float orc_v_expf(float x) {
+    const float r = 0x1.8p23f;
+    const float z = fmaf(x, 0x1.715476p+0f, r);
+    const float n = z - r;
+    const float b = fmaf(-n, 0x1.7f7d1cp-20f, fmaf(-n, 0x1.62e4p-1f, x));
+    const float u = b * b;
+    const float j = fmaf(fmaf(fmaf(0x1.0e4020p-7f, b, 0x1.573e2ep-5f), u, fmaf(0x1.555e66p-3f, b, 0x1.fffdb6p-2f)), u,
+                         fmaf(0x1.ffffecp-1f, b, 1.0f));
+    if (fabsf(n) > 192.0f) return n <= 0.0f ? 0.0f : INFINITY;
+    return ldexpf(j, (int) n);
+}
+
+/* ggml_vec_silu_f32 (vec.cpp:233-255): AVX-512 body x / (1 + v_expf(-x)) in 16-wide
+ * chunks, libm expf for the tail (ggml_silu_f32, vec.h) */
+void orc_silu(const float * x, int64_t n, float * y) {
+    const int64_t nv = n & ~(int64_t) 15;
+    for (int64_t i = 0; i < n; ++i) {
+        const float e = i < nv ? orc_v_expf(0.0f - x[i]) : expf(-x[i]);
+        y[i] = x[i] / (1.0f + e);
+    }
+}
+
+/* ---- block layouts, ggml/src/ggml-common.h:167-334 -------------------------------------------- */
+typedef struct { uint16_t d; uint8_t qs[16]; } b_q4_0;
+typedef struct { uint16_t d; int8_t qs[32]; } b_q8_0;
+typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qs[128]; } b_q4_K;
+typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; } b_q5_K;
+typedef struct { uint8_t ql[128]; uint8_t qh[64]; int8_t scales[16]; uint16_t d; } b_q6_K;
+typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } b_q8_K;
+
+int orc_block_size(int type) {
+    switch (type) {
+        case T_Q4_0: return 32; case T_Q8_0: return 32;
+        case T_Q4_K: case T_Q5_K: case T_Q6_K: case T_Q8_K: return 256;
+        default: return 1;
+    }
+}
+int orc_type_size(int type) {
+    switch (type) {
+        case T_F32: return 4; case T_F16: return 2;
+        case T_Q4_0: return 18; case T_Q8_0: return 34; case T_Q4_K: return 144; case T_Q5_K: return 176;
+        case T_Q6_K: return 210; case T_Q8_K: return 292;
+        default: return 0;
+    }
+}
+
+/* nearest_int, ggml-quants.c:366-371 (round half to even via the 1.5*2^23 trick) */
+static inline int nearest_int(float fval) {
+    float val = fval + 12582912.f;
+    int i; memcpy(&i, &val, sizeof(int));
+    return (i & 0x007fffff) - 0x00400000;
+}
+
+/* quantize_row_q8_K_ref, ggml-quants.c:2471-2508 (the x86 CPU backend uses it verbatim,
+ * ggml-cpu/arch/x86/quants.c:481-484) */
+void orc_quantize_row_q8_K(const float * x, void * vy, int64_t k) {
+    b_q8_K * y = (b_q8_K *) vy;
+    const int64_t nb = k / QK_K;
+    for (int64_t i = 0; i < nb; i++) {
+        float max = 0, amax = 0;
+        for (int j = 0; j < QK_K; ++j) {
+            const float ax = fabsf(x[j]);
+            if (ax > amax) { amax = ax; max = x[j]; }
+        }
+        if (!amax) {
+            y[i].d = 0;
+            memset(y[i].qs, 0, QK_K);
+            memset(y[i].bsums, 0, sizeof(y[i].bsums));
+            x += QK_K;
+            continue;
+        }
+        const float iscale = -127.f / max;
+        for (int j = 0; j < QK_K; ++j) {
+            const volatile float prod = iscale * x[j];  /* no contraction into the rounding add */
+            const int v = nearest_int(prod);
+            y[i].qs[j] = (int8_t) MINF(127, v);
+        }
+        for (int j = 0; j < QK_K / 16; ++j) {
+            int sum = 0;
+            for (int ii = 0; ii < 16; ++ii) sum += y[i].qs[j * 16 + ii];
+            y[i].bsums[j] = (int16_t) sum;
+        }
+        y[i].d = 1 / iscale;
+        x += QK_K;
+    }
+}
+
+/* x86 quantize_row_q8_0, ggml-cpu/arch/x86/quants.c:278-372: d = max/127, id = 127/max,
+ * round-half-even of x*id (_mm256_round_ps(_MM_ROUND_NEAREST)), d stored as fp16 (F16C RNE). */
+void orc_quantize_row_q8_0(const float * x, void * vy, int64_t k) {
+    b_q8_0 * y = (b_q8_0 *) vy;
+    const int64_t nb = k / 32;
+    for (int64_t i = 0; i < nb; i++) {
+        float amax = 0.0f;
+        for (int j = 0; j < 32; ++j) amax = MAXF(amax, fabsf(x[i * 32 + j]));
+        const float d = amax / 127.f;
+        y[i].d = orc_fp32_to_fp16(d);
+        const float id = amax != 0.0f ? 127.f / amax : 0.0f;
+        for (int j = 0; j < 32; ++j) {
+            const volatile float v = x[i * 32 + j] * id;
+            float r = rintf(v);
+            if (r > 127.f) r = 127.f;
+            if (r < -128.f) r = -128.f;
+            y[i].qs[j] = (int8_t) r;
+        }
+    }
+}
+
+/* get_scale_min_k4, ggml-quants.c:625-633 */
+static inline void get_scale_min_k4(int j, const uint8_t * q, uint8_t * d, uint8_t * m) {
+    if (j < 4) {
+        *d = q[j] & 63; *m = q[j + 4] & 63;
+    } else {
+        *d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        *m = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4);
+    }
+}
+
+/* dequantize_row_* , ggml-quants.c:249 (q4_0), 343 (q8_0), 1274 (q4_K), 1476 (q5_K), 1684 (q6_K) */
+void orc_dequantize_row(int type, const void * vx, float * y, int64_t k) {
+    if (type == T_Q4_0) {
+        const b_q4_0 * x = (const b_q4_0 *) vx;
+        for (int64_t i = 0; i < k / 32; i++) {
+            const float d = orc_fp16_to_fp32(x[i].d);
+            for (int j = 0; j < 16; ++j) {
+                y[i * 32 + j] = ((x[i].qs[j] & 0x0F) - 8) * d;
+                y[i * 32 + j + 16] = ((x[i].qs[j] >> 4) - 8) * d;
+            }
+        }
+    } else if (type == T_Q8_0) {
+        const b_q8_0 * x = (const b_q8_0 *) vx;
+        for (int64_t i = 0; i < k / 32; i++) {
+            const float d = orc_fp16_to_fp32(x[i].d);
+            for (int j = 0; j < 32; ++j) y[i * 32 + j] = x[i].qs[j] * d;
+        }
+    } else if (type == T_Q4_K) {
+        const b_q4_K * x = (const b_q4_K *) vx;
+        for (int64_t i = 0; i < k / QK_K; i++) {
+            const uint8_t * q = x[i].qs;
+            const float d = orc_fp16_to_fp32(x[i].d), min = orc_fp16_to_fp32(x[i].dmin);
+            int is = 0; uint8_t sc, m;
+            for (int j = 0; j < QK_K; j += 64) {
+                get_scale_min_k4(is + 0, x[i].scales, &sc, &m);
+                const float d1 = d * sc, m1 = min * m;
+                get_scale_min_k4(is + 1, x[i].scales, &sc, &m);
+                const float d2 = d * sc, m2 = min * m;
+                for (int l = 0; l < 32; ++l) *y++ = d1 * (q[l] & 0xF) - m1;
+                for (int l = 0; l < 32; ++l) *y++ = d2 * (q[l] >> 4) - m2;
+                q += 32; is += 2;
+            }
+        }
+    } else if (type == T_Q5_K) {
+        const b_q5_K * x = (const b_q5_K *) vx;
+        for (int64_t i = 0; i < k / QK_K; i++) {
+            const uint8_t * ql = x[i].qs; const uint8_t * qh = x[i].qh;
+            const float d = orc_fp16_to_fp32(x[i].d), min = orc_fp16_to_fp32(x[i].dmin);
+            int is = 0; uint8_t sc, m; uint8_t u1 = 1, u2 = 2;
+            for (int j = 0; j < QK_K; j += 64) {
+                get_scale_min_k4(is + 0, x[i].scales, &sc, &m);
+                const float d1 = d * sc, m1 = min * m;
+                get_scale_min_k4(is + 1, x[i].scales, &sc, &m);
+                const float d2 = d * sc, m2 = min * m;
+                for (int l = 0; l < 32; ++l) *y++ = d1 * ((ql[l] & 0xF) + (qh[l] & u1 ? 16 : 0)) - m1;
+                for (int l = 0; l < 32; ++l) *y++ = d2 * ((ql[l] >> 4) + (qh[l] & u2 ? 16 : 0)) - m2;
+                ql += 32; is += 2; u1 <<= 2; u2 <<= 2;
+            }
+        }
+    } else if (type == T_Q6_K) {
+        const b_q6_K * x = (const b_q6_K *) vx;
+        for (int64_t i = 0; i < k / QK_K; i++) {
+            const float d = orc_fp16_to_fp32(x[i].d);
+            const uint8_t * ql = x[i].ql; const uint8_t * qh = x[i].qh; const int8_t * sc = x[i].scales;
+            for (int n = 0; n < QK_K; n += 128) {
+                for (int l = 0; l < 32; ++l) {
+                    const int is = l / 16;
+                    const int8_t q1 = (int8_t) ((ql[l + 0] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+                    const int8_t q2 = (int8_t) ((ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+                    const int8_t q3 = (int8_t) ((ql[l + 0] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+                    const int8_t q4 = (int8_t) ((ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+                    y[l + 0] = d * sc[is + 0] * q1;
+                    y[l + 32] = d * sc[is + 2] * q2;
+                    y[l + 64] = d * sc[is + 4] * q3;
+                    y[l + 96] = d * sc[is + 6] * q4;
+                }
+                y += 128; ql += 64; qh += 32; sc += 8;
+            }
+        }
+    } else if (type == T_F16) {
+        const uint16_t * x = (const uint16_t *) vx;
+        for (int64_t i = 0; i < k; ++i) y[i] = orc_fp16_to_fp32(x[i]);
+    } else if (type == T_F32) {
+        memcpy(y, vx, sizeof(float) * k);
+    }
+}
+
+/* Integer parts of the vec_dot kernels (ggml-cpu/quants.c:110-144, 269-297, 514-722):
+ * per-block integer sums returned in isum[b] (and min-sums in msum[b] for q4_K/q5_K) so
+ * tests can check them bit-exactly; the float result follows the generic kernels'
+ * combination d_x*d_y*isum - dmin_x*d_y*msum. */
+float orc_vec_dot(int type, int64_t n, const void * vx, const void * vy, int32_t * isum, int32_t * msum) {
+    float sumf = 0.0f;
+    if (type == T_Q4_0 || type == T_Q8_0) {
+        const b_q8_0 * y = (const b_q8_0 *) vy;
+        for (int64_t ib = 0; ib < n / 32; ++ib) {
+            int s = 0;
+            float dx;
+            if (type == T_Q4_0) {
+                const b_q4_0 * x = (const b_q4_0 *) vx + ib;
+                for (int j = 0; j < 16; ++j) {
+                    s += ((x->qs[j] & 0x0F) - 8) * y[ib].qs[j];
+                    s += ((x->qs[j] >> 4) - 8) * y[ib].qs[j + 16];
+                }
+                dx = orc_fp16_to_fp32(x->d);
+            } else {
+                const b_q8_0 * x = (const b_q8_0 *) vx + ib;
+                for (int j = 0; j < 32; ++j) s += x->qs[j] * y[ib].qs[j];
+                dx = orc_fp16_to_fp32(x->d);
+            }
+            if (isum) isum[ib] = s;
+            sumf += s * (dx * orc_fp16_to_fp32(y[ib].d));
+        }
+        return sumf;
+    }
+    const b_q8_K * y = (const b_q8_K *) vy;
+    for (int64_t i = 0; i < n / QK_K; ++i) {
+        int8_t a[QK_K];
+        int sumi = 0, summ = 0;
+        float dx, dmx = 0.0f;
+        if (type == T_Q4_K || type == T_Q5_K) {
+            const uint8_t * sc12;
+            const uint8_t * q4;
+            const uint8_t * hm = NULL;
+            if (type == T_Q4_K) {
+                const b_q4_K * x = (const b_q4_K *) vx + i;
+                sc12 = x->scales; q4 = x->qs; dx = orc_fp16_to_fp32(x->d); dmx = orc_fp16_to_fp32(x->dmin);
+            } else {
+                const b_q5_K * x = (const b_q5_K *) vx + i;
+                sc12 = x->scales; q4 = x->qs; hm = x->qh; dx = orc_fp16_to_fp32(x->d); dmx = orc_fp16_to_fp32(x->dmin);
+            }
+            uint8_t m = 1;
+            for (int j = 0; j < QK_K / 64; ++j) {
+                for (int l = 0; l < 32; ++l) a[64 * j + l] = (int8_t) ((q4[32 * j + l] & 0xF) + (hm && (hm[l] & m) ? 16 : 0));
+                m <<= 1;
+                for (int l = 0; l < 32; ++l) a[64 * j + 32 + l] = (int8_t) ((q4[32 * j + l] >> 4) + (hm && (hm[l] & m) ? 16 : 0));
+                m <<= 1;
+            }
+            for (int j = 0; j < 8; ++j) {
+                uint8_t sc, mn;
+                get_scale_min_k4(j, sc12, &sc, &mn);
+                int dot = 0;
+                for (int l = 0; l < 32; ++l) dot += a[32 * j + l] * y[i].qs[32 * j + l];
+                sumi += sc * dot;
+                summ += mn * (y[i].bsums[2 * j] + y[i].bsums[2 * j + 1]);
+            }
+        } else { /* Q6_K */
+            const b_q6_K * x = (const b_q6_K *) vx + i;
+            dx = orc_fp16_to_fp32(x->d);
+            const uint8_t * ql = x->ql; const uint8_t * qh = x->qh;
+            for (int h = 0; h < 2; ++h) {
+                for (int l = 0; l < 32; ++l) {
+                    a[128 * h + l + 0] = (int8_t) ((ql[64 * h + l] & 0xF) | (((qh[32 * h + l] >> 0) & 3) << 4)) - 32;
+                    a[128 * h + l + 32] = (int8_t) ((ql[64 * h + l + 32] & 0xF) | (((qh[32 * h + l] >> 2) & 3) << 4)) - 32;
+                    a[128 * h + l + 64] = (int8_t) ((ql[64 * h + l] >> 4) | (((qh[32 * h + l] >> 4) & 3) << 4)) - 32;
+                    a[128 * h + l + 96] = (int8_t) ((ql[64 * h + l + 32] >> 4) | (((qh[32 * h + l] >> 6) & 3) << 4)) - 32;
+                }
+            }
+            for (int j = 0; j < 16; ++j) {
+                int dot = 0;
+                for (int l = 0; l < 16; ++l) dot += a[16 * j + l] * y[i].qs[16 * j + l];
+                sumi += x->scales[j] * dot;
+            }
+        }
+        if (isum) isum[i] = sumi;
+        if (msum) msum[i] = summ;
+        sumf += (dx * y[i].d) * (float) sumi - (dmx * y[i].d) * (float) summ;
+    }
+    return sumf;
+}
+
+/* ggml_compute_forward_mul_mat for quantized src0 (ggml-cpu/ggml-cpu.c:1192-1384): every
+ * src1 row is first converted with the weight type's from_float (vec_dot_type), then
+ * Y[t][m] = vec_dot(W[m], Xq[t]).  W: M rows of K; X: T rows of K; Y: T rows of M. */
+void orc_mul_mat(int type, const void * W, int64_t K, int64_t M, const float * X, int64_t T, float * Y) {
+    const size_t wrow = (size_t) (K / orc_block_size(type)) * orc_type_size(type);
+    if (type == T_F16 || type == T_F32) {
+        float * w = (float *) malloc(sizeof(float) * K);
+        for (int64_t m = 0; m < M; ++m) {
+            orc_dequantize_row(type, (const char *) W + m * wrow, w, K);
+            for (int64_t t = 0; t < T; ++t) {
+                double s = 0;
+                for (int64_t k = 0; k < K; ++k) s += (double) w[k] * X[t * K + k];
+                Y[t * M + m] = (float) s;
+            }
+        }
+        free(w);
+        return;
+    }
+    const int kq = type == T_Q4_K || type == T_Q5_K || type == T_Q6_K;
+    const size_t arow = kq ? (size_t) (K / 256) * sizeof(b_q8_K) : (size_t) (K / 32) * sizeof(b_q8_0);
+    char * xq = (char *) malloc(arow * T);
+    for (int64_t t = 0; t < T; ++t) {
+        if (kq) orc_quantize_row_q8_K(X + t * K, xq + t * arow, K);
+        else orc_quantize_row_q8_0(X + t * K, xq + t * arow, K);
+    }
+    for (int64_t t = 0; t < T; ++t)
+        for (int64_t m = 0; m < M; ++m)
+            Y[t * M + m] = orc_vec_dot(type, K, (const char *) W + m * wrow, xq + t * arow, NULL, NULL);
+    free(xq);
+}
+
+/* ggml_compute_forward_rms_norm_f32, ggml-cpu/ops.cpp:3270-3316 (sum in double) */
+void orc_rms_norm(const float * x, int64_t ne0, int64_t nrows, float eps, float * y) {
+    for (int64_t r = 0; r < nrows; ++r) {
+        double sum = 0.0;
+        for (int64_t i = 0; i < ne0; ++i) sum += (double) (x[r * ne0 + i] * x[r * ne0 + i]);
+        const float mean = (float) (sum / ne0);
+        const float scale = 1.0f / sqrtf(mean + eps);
+        for (int64_t i = 0; i < ne0; ++i) y[r * ne0 + i] = x[r * ne0 + i] * scale;
+    }
+}
+
+/* ggml_rope_yarn_corr_dims, ggml.c:3772-3784 */
+static float corr_dim(int n_dims, int n_ctx_orig, float n_rot, float base) {
+    return n_dims * logf(n_ctx_orig / (n_rot * 2 * (float) M_PI)) / (2 * logf(base));
+}
+
+/* ggml_compute_forward_rope_f32 + ggml_rope_cache_init + rope_yarn, ops.cpp:5080-5362.
+ * x: [n_tok][n_head][ne0] (contiguous ggml [ne0, n_head, n_tok]); mode 0 = NORM, 2 = NEOX */
+void orc_rope(const float * x, int64_t ne0, int64_t n_head, int64_t n_tok, const int32_t * pos, int n_dims, int mode,
+              int n_ctx_orig, float freq_base, float freq_scale, float ext_factor, float attn_factor, float beta_fast,
+              float beta_slow, const float * ff, float * y) {
+    const float theta_scale = powf(freq_base, -2.0f / n_dims);
+    float corr[2];
+    corr[0] = MAXF(0, floorf(corr_dim(n_dims, n_ctx_orig, beta_fast, freq_base)));
+    corr[1] = MINF(n_dims - 1, ceilf(corr_dim(n_dims, n_ctx_orig, beta_slow, freq_base)));
+    float * cache = (float *) malloc(sizeof(float) * ne0);
+    for (int64_t t = 0; t < n_tok; ++t) {
+        float theta = (float) pos[t];
+        for (int64_t i0 = 0; i0 < ne0; i0 += 2) {
+            const float f = ff ? ff[i0 / 2] : 1.0f;
+            const float theta_extrap = theta / f;
+            const float theta_interp = freq_scale * theta_extrap;
+            float th = theta_interp, mscale = attn_factor;
+            if (ext_factor != 0.0f) {
+                const float yy = (i0 / 2 - corr[0]) / MAXF(0.001f, corr[1] - corr[0]);
+                const float ramp_mix = (1 - MINF(1, MAXF(0, yy))) * ext_factor;
+                th = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
+                mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
+            }
+            cache[i0] = cosf(th) * mscale;
+            cache[i0 + 1] = sinf(th) * mscale;
+            theta *= theta_scale;
+        }
+        for (int64_t h = 0; h < n_head; ++h) {
+            const float * src = x + (t * n_head + h) * ne0;
+            float * dst = y + (t * n_head + h) * ne0;
+            for (int64_t i0 = 0; i0 < ne0; ++i0) dst[i0] = src[i0];
+            for (int64_t i0 = 0; i0 < n_dims; i0 += 2) {
+                const float c = cache[i0], s = cache[i0 + 1];
+                int64_t a0, a1;
+                if (mode & 2) { a0 = i0 / 2; a1 = i0 / 2 + n_dims / 2; }
+                else { a0 = i0; a1 = i0 + 1; }
+                const float x0 = src[a0], x1 = src[a1];
+                /* the x86-64-v4 build contracts ops.cpp:5245-5246 as fma(x0, c, -(x1*s)) and
+                 * fma(x0, s, x1*c) (bit-exact against tests/golden/rope.npz) */
+                dst[a0] = fmaf(x0, c, -(x1 * s));
+                dst[a1] = fmaf(x0, s, x1 * c);
+            }
+        }
+    }
+    free(cache);
+}
+
+/* ggml_compute_forward_soft_max_f32, ops.cpp:4731-4827 (no ALiBi); mask rows broadcast
+ * with row index r % mask_rows; sum in double */
+void orc_soft_max(const float * x, int64_t nc, int64_t nr, const float * mask, int64_t mask_rows, float scale, float * y) {
+    for (int64_t r = 0; r < nr; ++r) {
+        float mx = -INFINITY;
+        for (int64_t i = 0; i < nc; ++i) {
+            float w = x[r * nc + i] * scale;
+            if (mask) w += mask[(r % mask_rows) * nc + i];
+            y[r * nc + i] = w;
+            mx = MAXF(mx, w);
+        }
+        /* ggml_vec_soft_max_f32 (vec.cpp:257-300): 16-wide ggml_v_expf chunks reduced by
+         * _mm512_reduce_add_ps and summed in double; libm expf for the tail */
+        double sum = 0.0;
+        int64_t i = 0;
+        for (; i + 15 < nc; i += 16) {
+            float w[16];
+            for (int k = 0; k < 16; ++k) { w[k] = orc_v_expf(y[r * nc + i + k] - mx); y[r * nc + i + k] = w[k]; }
+            sum += (double) reduce16(w);
+        }
+        for (; i < nc; ++i) {
+            const float e = expf(y[r * nc + i] - mx);
+            y[r * nc + i] = e;
+            sum += (double) e;
+        }
+        const float inv = (float) (1.0 / sum);
+        for (int64_t i = 0; i < nc; ++i) y[r * nc + i] *= inv;
+    }
+}
+
+#ifndef FA_S_UPDATE
+/* S = S*ms + vs is NOT contracted in the reference build (measured: the unfused form is
+ * 99.97% bit-exact on tests/golden/flash_attn.npz, the fused one 98%) */
+#define FA_S_UPDATE(S, ms, vs) ((S) * (ms) + (vs))
+#endif
+/* ggml_compute_forward_flash_attn_ext_f16, ops.cpp:7015-7232, for K/V f16 or q8_0.
+ * q: [n_q][H][D] f32, k/v: [n_kv][Hkv][D] in kv_type, mask: [n_q][n_kv] f16 (may be NULL),
+ * out: [n_q][H][D].  f16 V accumulates VKQ in f16 exactly like the CPU (ops.cpp:7147-7171). */
+void orc_flash_attn(const float * q, const void * k, const void * v, const uint16_t * mask, int kv_type, int64_t D,
+                    int64_t n_q, int64_t H, int64_t n_kv, int64_t Hkv, float scale, float softcap, float * out) {
+    const int64_t gqa = H / Hkv;
+    const size_t row = kv_type == T_F16 ? D * 2 : (D / 32) * sizeof(b_q8_0);
+    if (softcap != 0) scale /= softcap;
+    float * vkq32 = (float *) malloc(sizeof(float) * D);
+    uint16_t * vkq16 = (uint16_t *) malloc(sizeof(uint16_t) * D);
+    float * v32 = (float *) malloc(sizeof(float) * D);
+    uint16_t * q16 = (uint16_t *) malloc(sizeof(uint16_t) * D);
+    b_q8_0 * q8 = (b_q8_0 *) malloc(sizeof(b_q8_0) * (D / 32 + 1));
+    float * qf = (float *) malloc(sizeof(float) * D);
+    float * kf = (float *) malloc(sizeof(float) * D);
+    for (int64_t iq = 0; iq < n_q; ++iq) {
+        for (int64_t h = 0; h < H; ++h) {
+            const float * pq = q + (iq * H + h) * D;
+            if (kv_type == T_F16) {
+                for (int64_t d = 0; d < D; ++d) { q16[d] = orc_fp32_to_fp16(pq[d]); qf[d] = orc_fp16_to_fp32(q16[d]); }
+            } else {
+                orc_quantize_row_q8_0(pq, q8, D);
+            }
+            float S = 0.0f, M = -INFINITY;
+            if (kv_type == T_F16) memset(vkq16, 0, sizeof(uint16_t) * D);
+            else memset(vkq32, 0, sizeof(float) * D);
+            const int64_t hk = h / gqa;
+            for (int64_t ic = 0; ic < n_kv; ++ic) {
+                const float mv = mask ? orc_fp16_to_fp32(mask[iq * n_kv + ic]) : 0.0f;
+                if (mv == -INFINITY) continue;
+                const char * kd = (const char *) k + (ic * Hkv + hk) * row;
+                const char * vd = (const char *) v + (ic * Hkv + hk) * row;
+                float s;
+                if (kv_type == T_F16) {
+                    for (int64_t d = 0; d < D; ++d) kf[d] = orc_fp16_to_fp32(((const uint16_t *) kd)[d]);
+                    s = dot_avx512(kf, qf, D);
+                } else {
+                    s = orc_vec_dot(T_Q8_0, D, kd, q8, NULL, NULL);
+                }
+                s = s * scale;
+                if (softcap != 0.0f) s = softcap * tanhf(s);
+                s += mv;
+                const float Mold = M;
+                float ms = 1.0f, vs = 1.0f;
+                if (kv_type == T_F16) {
+                    if (s > M) {
+                        M = s;
+                        ms = expf(Mold - M);
+                        for (int64_t d = 0; d < D; ++d) vkq16[d] = orc_fp32_to_fp16(orc_fp16_to_fp32(vkq16[d]) * ms);
+                    } else {
+                        vs = expf(s - M);
+                    }
+                    for (int64_t d = 0; d < D; ++d)
+                        vkq16[d] = orc_fp32_to_fp16(orc_fp16_to_fp32(vkq16[d]) + orc_fp16_to_fp32(((const uint16_t *) vd)[d]) * vs);
+                } else {
+                    if (s > M) {
+                        M = s;
+                        ms = expf(Mold - M);
+                        for (int64_t d = 0; d < D; ++d) vkq32[d] *= ms;
+                    } else {
+                        vs = expf(s - M);
+                    }
+                    orc_dequantize_row(kv_type, vd, v32, D);
+                    for (int64_t d = 0; d < D; ++d) vkq32[d] += v32[d] * vs;
+                }
+                S = FA_S_UPDATE(S, ms, vs);
+            }
+            if (kv_type == T_F16) for (int64_t d = 0; d < D; ++d) vkq32[d] = orc_fp16_to_fp32(vkq16[d]);
+            const float S_inv = 1.0f / S;
+            for (int64_t d = 0; d < D; ++d) out[(iq * H + h) * D + d] = vkq32[d] * S_inv;
+        }
+    }
+    free(vkq32); free(vkq16); free(v32); free(q16); free(q8); free(qf); free(kf);
+}
+
+void orc_fa_scores(const float * q, const uint16_t * k, int64_t n, int64_t D, float * s) {
+    float * qf = (float *) malloc(sizeof(float) * D);
+    float * kf = (float *) malloc(sizeof(float) * D);
+    for (int64_t d = 0; d < D; ++d) qf[d] = orc_fp16_to_fp32(orc_fp32_to_fp16(q[d]));
+    for (int64_t j = 0; j < n; ++j) {
+        for (int64_t d = 0; d < D; ++d) kf[d] = orc_fp16_to_fp32(k[j * D + d]);
+        s[j] = dot_avx512(kf, qf, D);
+    }
+    free(qf); free(kf);
+}

@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""make_golden.py — write tests/golden/*.npz from the REFERENCE's own ggml.
+
+TEST INFRASTRUCTURE.  Calls oracle/_ref/libgolden.so (oracle/gen_golden.c linked against
+libggml-base + the x86-64-v4 ggml-cpu built from /root/reference sources by refhost/) to
+produce golden input/output vectors for the hot path:
+  * activation quantizers (the CPU backend's from_float for Q8_K and Q8_0),
+  * model-file quantized weights (ggml_quantize_chunk) + their dequantization,
+  * per-row vec_dot results and CPU mul_mat outputs for Q4_0/Q8_0/Q4_K/Q5_K/Q6_K,
+  * rms_norm, rope (NORM/NEOX, Llama-3 base 500000), soft_max, flash_attn_ext (f16 and q8_0 KV).
+Inputs follow tests/test-quantize-fns.cpp:31-35 (0.1 + 2*cos(i + offset)) plus seeded
+random data and hand-made edge cases.  Run here (where /root/reference exists):
+    python oracle/make_golden.py
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, "tests", "golden")
+
+F32, F16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 8, 12, 13, 14, 15
+BLK = {Q4_0: (32, 18), Q8_0: (32, 34), Q4_K: (256, 144), Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292),
+       F16: (1, 2), F32: (1, 4)}
+NAMES = {Q4_0: "q4_0", Q8_0: "q8_0", Q4_K: "q4_K", Q5_K: "q5_K", Q6_K: "q6_K"}
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+
+
+def fptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def load():
+    lib = ctypes.CDLL(os.path.join(HERE, "_ref", "libgolden.so"))
+    lib.gg_quantize.argtypes = [ctypes.c_int, P, P, I64, I64]
+    lib.gg_quantize.restype = ctypes.c_size_t
+    lib.gg_from_float.argtypes = [ctypes.c_int, P, P, I64]
+    lib.gg_to_float.argtypes = [ctypes.c_int, P, P, I64]
+    lib.gg_vec_dot.argtypes = [ctypes.c_int, I64, P, P]
+    lib.gg_vec_dot.restype = ctypes.c_float
+    lib.gg_mul_mat.argtypes = [ctypes.c_int, P, I64, I64, P, I64, P, ctypes.c_int]
+    lib.gg_rms_norm.argtypes = [P, I64, I64, ctypes.c_float, P]
+    lib.gg_rope.argtypes = [P, I64, I64, I64, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                            ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, P, P]
+    lib.gg_soft_max.argtypes = [P, I64, I64, P, I64, ctypes.c_float, P]
+    lib.gg_flash_attn.argtypes = [P, P, P, P, ctypes.c_int, I64, I64, I64, I64, I64, ctypes.c_float, ctypes.c_float, P,
+                                  ctypes.c_int]
+    lib.gg_init()
+    return lib
+
+
+def nbytes(t, n):
+    b, s = BLK[t]
+    return n // b * s
+
+
+def quantize(lib, t, w):
+    rows, k = w.shape
+    out = np.zeros(rows * nbytes(t, k), dtype=np.uint8)
+    lib.gg_quantize(t, fptr(w), fptr(out), rows, k)
+    return out.reshape(rows, -1)
+
+
+def from_float(lib, t, x):
+    rows, k = x.shape
+    out = np.zeros((rows, nbytes(t, k)), dtype=np.uint8)
+    for r in range(rows):
+        lib.gg_from_float(t, fptr(x[r]), fptr(out[r]), k)
+    return out
+
+
+def to_float(lib, t, q, k):
+    rows = q.shape[0]
+    out = np.zeros((rows, k), dtype=np.float32)
+    for r in range(rows):
+        lib.gg_to_float(t, fptr(q[r]), fptr(out[r]), k)
+    return out
+
+
+def act_cases(k, rng):
+    i = np.arange(k, dtype=np.float32)
+    rows = [
+        (0.1 + 2 * np.cos(i + 0.0)).astype(np.float32),           # test-quantize-fns data
+        (0.1 + 2 * np.cos(i + 1.0)).astype(np.float32),
+        rng.standard_normal(k).astype(np.float32),
+        (rng.standard_normal(k) * 1e-3).astype(np.float32),
+        (rng.standard_normal(k) * 300).astype(np.float32),
+        np.zeros(k, dtype=np.float32),                               # all-zero blocks (d = 0)
+    ]
+    tie = rng.standard_normal(k).astype(np.float32) * 0.5
+    tie[::256] = -3.0                                                # equal |max| of both signs:
+    tie[5::256] = 3.0                                                # first index must win
+    rows.append(tie)
+    half = np.round(rng.standard_normal(k) * 40).astype(np.float32) / 127.0 * 0.5
+    rows.append(half.astype(np.float32))                             # many x*iscale near .5
+    return np.stack(rows)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    lib = load()
+    rng = np.random.default_rng(1234)
+
+    # ---- activation quantizers ------------------------------------------------------------
+    K = 1024
+    x = act_cases(K, rng)
+    np.savez_compressed(os.path.join(OUT, "quant_act.npz"), x=x, q8_K=from_float(lib, Q8_K, x), q8_0=from_float(lib, Q8_0, x))
+
+    # ---- weights, dequant, vec_dot, mul_mat ------------------------------------------------
+    M, K, T = 64, 512, 8
+    for t, name in NAMES.items():
+        i = np.arange(M * K, dtype=np.float32).reshape(M, K)
+        w = (0.1 + 2 * np.cos(i + 0.5)).astype(np.float32) * 0.05
+        w[M // 2:] = (rng.standard_normal((M - M // 2, K)) * 0.02).astype(np.float32)
+        wq = quantize(lib, t, w)
+        wd = to_float(lib, t, wq, K)
+        xs = np.concatenate([act_cases(K, rng)[:T - 2], rng.standard_normal((2, K)).astype(np.float32)])
+        vdt = Q8_K if t in (Q4_K, Q5_K, Q6_K) else Q8_0
+        xq = from_float(lib, vdt, xs)
+        vd = np.zeros((T, M), dtype=np.float32)
+        for a in range(T):
+            for m in range(M):
+                vd[a, m] = lib.gg_vec_dot(t, K, fptr(wq[m]), fptr(xq[a]))
+        y = np.zeros((T, M), dtype=np.float32)
+        lib.gg_mul_mat(t, fptr(wq), K, M, fptr(xs), T, fptr(y), 1)
+        y1 = np.zeros((1, M), dtype=np.float32)
+        lib.gg_mul_mat(t, fptr(wq), K, M, fptr(xs[:1]), 1, fptr(y1), 1)
+        np.savez_compressed(os.path.join(OUT, f"mul_mat_{name}.npz"), type=t, w=w, wq=wq, wd=wd, x=xs, xq=xq, vec_dot=vd,
+                            y=y, y1=y1)
+
+    # ---- rms_norm ----------------------------------------------------------------------------
+    x = np.concatenate([act_cases(4096, rng)[:5], rng.standard_normal((3, 4096)).astype(np.float32)])
+    y = np.zeros_like(x)
+    lib.gg_rms_norm(fptr(x), 4096, x.shape[0], 1e-5, fptr(y))
+    np.savez_compressed(os.path.join(OUT, "rms_norm.npz"), x=x, y=y, eps=np.float32(1e-5))
+
+    # ---- rope: Llama-3 (NORM, base 500000) and NEOX, with/without freq factors --------------
+    ne0, nh, ntok = 128, 4, 6
+    pos = np.array([0, 1, 7, 255, 511, 4095], dtype=np.int32)
+    xr = rng.standard_normal((ntok, nh, ne0)).astype(np.float32)
+    ff = (1.0 + np.arange(ne0 // 2, dtype=np.float32) / 32).astype(np.float32)
+    cases = []
+    for mode in (0, 2):
+        for base, use_ff in ((500000.0, False), (10000.0, True)):
+            y = np.zeros_like(xr)
+            lib.gg_rope(fptr(xr), ne0, nh, ntok, fptr(pos), ne0, mode, 8192, base, 1.0, 0.0, 1.0, 32.0, 1.0,
+                        fptr(ff) if use_ff else None, fptr(y))
+            cases.append((mode, base, use_ff, y))
+    np.savez_compressed(os.path.join(OUT, "rope.npz"), x=xr, pos=pos, ff=ff,
+                        modes=np.array([c[0] for c in cases]), bases=np.array([c[1] for c in cases], dtype=np.float32),
+                        use_ff=np.array([c[2] for c in cases]), y=np.stack([c[3] for c in cases]))
+
+    # ---- soft_max with a causal-style mask ---------------------------------------------------
+    nc, nr = 200, 12
+    xs = (rng.standard_normal((nr, nc)) * 3).astype(np.float32)
+    mask = np.zeros((4, nc), dtype=np.float32)
+    for r in range(4):
+        mask[r, 150 + 10 * r:] = -np.inf
+    y = np.zeros_like(xs)
+    lib.gg_soft_max(fptr(xs), nc, nr, fptr(mask), 4, 0.125, fptr(y))
+    np.savez_compressed(os.path.join(OUT, "soft_max.npz"), x=xs, mask=mask, scale=np.float32(0.125), y=y)
+
+    # ---- flash attention: D 128, GQA 4, f16 and q8_0 KV ------------------------------------
+    D, H, Hkv, n_kv = 128, 8, 2, 256
+    fa = {}
+    for n_q in (1, 7):
+        q = rng.standard_normal((n_q, H, D)).astype(np.float32)
+        kf = rng.standard_normal((n_kv, Hkv, D)).astype(np.float32)
+        vf = rng.standard_normal((n_kv, Hkv, D)).astype(np.float32)
+        m = np.zeros((n_q, n_kv), dtype=np.float16)
+        valid = 200
+        for r in range(n_q):
+            m[r, valid + r:] = -np.inf
+        m[:, 3] = -np.inf
+        for kvt, kvname in ((F16, "f16"), (Q8_0, "q8_0")):
+            if kvt == F16:
+                kb, vb = kf.astype(np.float16).view(np.uint8), vf.astype(np.float16).view(np.uint8)
+            else:
+                kb = quantize(lib, Q8_0, kf.reshape(-1, D)).reshape(-1)
+                vb = quantize(lib, Q8_0, vf.reshape(-1, D)).reshape(-1)
+            out = np.zeros((n_q, H, D), dtype=np.float32)
+            lib.gg_flash_attn(fptr(q), fptr(np.ascontiguousarray(kb)), fptr(np.ascontiguousarray(vb)),
+                              fptr(m.view(np.uint16)), kvt, D, n_q, H, n_kv, Hkv, 1.0 / np.sqrt(D), 0.0, fptr(out), 1)
+            fa[f"q_{n_q}"] = q
+            fa[f"k_{kvname}_{n_q}"] = np.ascontiguousarray(kb)
+            fa[f"v_{kvname}_{n_q}"] = np.ascontiguousarray(vb)
+            fa[f"mask_{n_q}"] = m.view(np.uint16)
+            fa[f"out_{kvname}_{n_q}"] = out
+    np.savez_compressed(os.path.join(OUT, "flash_attn.npz"), D=D, H=H, Hkv=Hkv, n_kv=n_kv, **fa)
+    for f in sorted(os.listdir(OUT)):
+        print(f"{f:28s} {os.path.getsize(os.path.join(OUT, f)):9d} B")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

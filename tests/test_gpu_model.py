@@ -1,0 +1,85 @@
+"""End-to-end parity through the reference's unchanged host stack on MI355X:
+
+* test-backend-ops (the reference's per-op harness, tests/test-backend-ops.cpp) run against
+  the MI355X device for every op family the plugin supports (NMSE bounds of the reference);
+* greedy decoding of synthetic GGUF models through libllama on MI355X vs the reference CPU
+  backend in the same process: identical token ids (unless the CPU's own top-2 logits are a
+  near tie), logits compared with the bound stated below;
+* every node of the llama graph (except the embedding GET_ROWS) runs on the MI355X device.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import llamacog_amd as la
+from llamacog_amd import gguf_synth as gs
+
+OPS = ["MUL_MAT", "FLASH_ATTN_EXT", "RMS_NORM", "ROPE", "SOFT_MAX", "CPY", "GET_ROWS", "ADD", "MUL", "SCALE", "SILU",
+       "CONT", "DUP", "SUB", "DIV", "NORM", "GELU"]
+
+
+@pytest.mark.parametrize("op", OPS)
+def test_backend_ops(op):
+    exe = os.path.join(la.REFHOST, "test-backend-ops")
+    env = dict(os.environ, GGML_BACKEND_PATH=la.PLUGIN)
+    r = subprocess.run([exe, "-b", "MI355X0", "-o", op], env=env, capture_output=True, text=True, timeout=600)
+    out = r.stdout + r.stderr
+    assert "MI355X0" in out, out[-2000:]
+    assert r.returncode == 0, "\n".join(l for l in out.splitlines() if "FAIL" in l)[:4000]
+
+
+def _greedy(cfg, n_prompt, n_gen, fa, kv="f16", layers=None):
+    path = gs.ensure(cfg, n_layer=layers)
+    rng = np.random.default_rng(99)
+    prompt = [1] + rng.integers(300, gs.CONFIGS[cfg].n_vocab, n_prompt - 1).tolist()
+    res = {}
+    for gpu in (True, False):
+        m = la.Model(path, gpu=gpu, n_ctx=512, flash_attn=fa, kv_type=kv, n_threads=16)
+        res[gpu] = m.greedy(prompt, n_gen)
+        m.close()
+    return res
+
+
+def _check(res, max_rel):
+    (ids_g, lg_g), (ids_c, lg_c) = res[True], res[False]
+    rel = [float(np.abs(lg_g[i] - lg_c[i]).max() / np.abs(lg_c[i]).max()) for i in range(len(ids_c))]
+    for i in range(len(ids_c)):
+        if ids_g[i] != ids_c[i]:
+            top2 = np.sort(lg_c[i])[-2:]
+            gap = (top2[1] - top2[0]) / np.abs(lg_c[i]).max()
+            assert gap < 4 * max_rel, f"step {i}: ids {ids_g[i]} vs {ids_c[i]}, cpu top-2 gap {gap:.2e}, rel {rel}"
+            break  # sequences legitimately diverge after a near tie
+    first = next((i for i in range(len(ids_c)) if ids_g[i] != ids_c[i]), len(ids_c))
+    assert max(rel[: max(first, 1)]) < max_rel, rel
+    return rel
+
+
+@pytest.mark.parametrize("fa", [True, False])
+def test_greedy_tiny_q4km(fa):
+    rel = _check(_greedy("tiny-q4km", 16, 16, fa), 2e-2)
+    print("tiny-q4km fa", fa, "max rel logit err", max(rel))
+
+
+def test_greedy_tiny_q8_0():
+    _check(_greedy("tiny-q8_0", 16, 16, True), 2e-2)
+
+
+def test_greedy_llama3_8b_2layer_q4km():
+    rel = _check(_greedy("llama3-8b-2l-q4km", 32, 16, True), 2e-2)
+    print("llama3-8b-2l max rel logit err", max(rel))
+
+
+def test_graph_runs_on_mi355x():
+    path = gs.ensure("tiny-q4km")
+    lib = la.llb()
+    m = la.Model(path, gpu=True, n_ctx=256)
+    m.greedy([1, 2, 3], 2)
+    log = la.log_tail(lib, 1 << 20)
+    m.close()
+    # decode graph: one CPU split (token embedding GET_ROWS, src/llama-model.cpp:1572) + one MI355X split
+    splits = [int(l.split("=")[-1]) for l in log.splitlines() if "graph splits" in l]
+    assert splits and splits[-1] <= 2, splits

@@ -1,0 +1,125 @@
+"""Pin the CPU restatement (oracle/ggml_oracle.c) against golden vectors produced by the
+reference's own ggml CPU backend (oracle/make_golden.py -> tests/golden/*.npz).
+
+Integer/byte work must be bit-exact: the Q8_K / Q8_0 activation quantizers, weight
+dequantization and the integer block sums.  Float outputs must match to the tolerance
+stated per test (the restatement follows the scalar operation order; SIMD summation order
+in the reference only moves the last bits).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def test_fp16_roundtrip_matches_numpy():
+    rng = np.random.default_rng(0)
+    vals = np.concatenate([rng.standard_normal(20000) * s for s in (1e-8, 1e-5, 1e-2, 1, 100, 6e4)]).astype(np.float32)
+    vals = np.concatenate([vals, np.array([0.0, -0.0, 65504.0, 65520.0, 1e9, -1e9, 5.96e-8, 2.98e-8], dtype=np.float32)])
+    L = O.lib()
+    got = np.array([L.orc_fp32_to_fp16(float(v)) for v in vals], dtype=np.uint16)
+    ref = vals.astype(np.float16).view(np.uint16)
+    assert (got == ref).all()
+    back = np.array([L.orc_fp16_to_fp32(int(h)) for h in ref[:2000]], dtype=np.float32)
+    assert (back == ref[:2000].view(np.float16).astype(np.float32)).all()
+
+
+def test_q8_K_activation_quantizer_bit_exact(golden_dir):
+    g = load(golden_dir, "quant_act.npz")
+    got = O.quantize_rows(O.Q8_K, g["x"])
+    assert got.shape == g["q8_K"].shape
+    assert (got == g["q8_K"]).all(), "Q8_K blocks differ from quantize_row_q8_K_ref"
+
+
+def test_q8_0_activation_quantizer_bit_exact(golden_dir):
+    g = load(golden_dir, "quant_act.npz")
+    got = O.quantize_rows(O.Q8_0, g["x"])
+    assert (got == g["q8_0"]).all(), "Q8_0 blocks differ from the x86 quantize_row_q8_0"
+
+
+@pytest.mark.parametrize("name", ["q4_0", "q8_0", "q4_K", "q5_K", "q6_K"])
+def test_dequantize_bit_exact(golden_dir, name):
+    g = load(golden_dir, f"mul_mat_{name}.npz")
+    t = int(g["type"])
+    got = O.dequantize_rows(t, g["wq"], g["w"].shape[1])
+    assert (got.view(np.uint32) == g["wd"].view(np.uint32)).all()
+
+
+@pytest.mark.parametrize("name", ["q4_0", "q8_0", "q4_K", "q5_K", "q6_K"])
+def test_activation_quantization_of_mul_mat_inputs(golden_dir, name):
+    g = load(golden_dir, f"mul_mat_{name}.npz")
+    t = int(g["type"])
+    vdt = O.Q8_K if t in (O.Q4_K, O.Q5_K, O.Q6_K) else O.Q8_0
+    assert (O.quantize_rows(vdt, g["x"]) == g["xq"]).all()
+
+
+@pytest.mark.parametrize("name", ["q4_0", "q8_0", "q4_K", "q5_K", "q6_K"])
+def test_vec_dot_matches_reference(golden_dir, name):
+    """Integer block sums are exact; the float combination order of the reference's SIMD
+    vec_dot differs from the generic one, so the result agrees to a few ulps."""
+    g = load(golden_dir, f"mul_mat_{name}.npz")
+    t = int(g["type"])
+    K = g["w"].shape[1]
+    vd = g["vec_dot"]
+    got = np.zeros_like(vd)
+    for a in range(vd.shape[0]):
+        for m in range(vd.shape[1]):
+            got[a, m], isum, _ = O.vec_dot(t, K, g["wq"][m], g["xq"][a])
+    scale = np.abs(vd).max() + 1e-30
+    assert np.abs(got - vd).max() / scale < 2e-6
+
+
+@pytest.mark.parametrize("name", ["q4_0", "q8_0", "q4_K", "q5_K", "q6_K"])
+def test_mul_mat_matches_reference(golden_dir, name):
+    g = load(golden_dir, f"mul_mat_{name}.npz")
+    t = int(g["type"])
+    M, K = g["w"].shape
+    y = O.mul_mat(t, g["wq"], K, M, g["x"])
+    ref = g["y"]
+    assert np.abs(y - ref).max() / (np.abs(ref).max() + 1e-30) < 2e-6
+    # against the float weights the quantized product is only approximate
+    assert np.abs(y - g["x"] @ g["wd"].T).max() / np.abs(ref).max() < 0.05
+
+
+def test_rms_norm(golden_dir):
+    g = load(golden_dir, "rms_norm.npz")
+    y = O.rms_norm(g["x"], float(g["eps"]))
+    assert (y.view(np.uint32) == g["y"].view(np.uint32)).mean() > 0.999
+    assert np.abs(y - g["y"]).max() <= 1e-6 * np.abs(g["y"]).max()
+
+
+def test_rope(golden_dir):
+    g = load(golden_dir, "rope.npz")
+    for i in range(len(g["modes"])):
+        y = O.rope(g["x"], g["pos"], 128, int(g["modes"][i]), float(g["bases"][i]),
+                   ff=g["ff"] if g["use_ff"][i] else None)
+        ref = g["y"][i]
+        err = np.abs(y - ref).max() / np.abs(ref).max()
+        assert err < 2e-6, (i, err)
+
+
+def test_soft_max(golden_dir):
+    g = load(golden_dir, "soft_max.npz")
+    y = O.soft_max(g["x"], g["mask"], float(g["scale"]))
+    assert np.abs(y - g["y"]).max() < 2e-6
+    assert np.allclose(y.sum(axis=1), 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("n_q", [1, 7])
+@pytest.mark.parametrize("kv", ["f16", "q8_0"])
+def test_flash_attn(golden_dir, n_q, kv):
+    g = load(golden_dir, "flash_attn.npz")
+    D, H, Hkv, n_kv = int(g["D"]), int(g["H"]), int(g["Hkv"]), int(g["n_kv"])
+    kvt = O.F16 if kv == "f16" else O.Q8_0
+    out = O.flash_attn(g[f"q_{n_q}"], g[f"k_{kv}_{n_q}"], g[f"v_{kv}_{n_q}"], g[f"mask_{n_q}"], kvt, D, H, Hkv, n_kv,
+                       1.0 / np.sqrt(D))
+    ref = g[f"out_{kv}_{n_q}"]
+    err = np.abs(out - ref).max() / np.abs(ref).max()
+    # f16 VKQ accumulation is restated rounding-for-rounding; only exp/dot-order ulps remain
+    assert err < (2e-3 if kv == "f16" else 2e-6), err

@@ -32,7 +32,16 @@ void log_cb(enum ggml_log_level level, const char * text, void *) {
     if (g_log_echo || level == GGML_LOG_LEVEL_ERROR) fputs(text, stderr);
 }
 
+struct dump_rec {
+    std::string name;
+    int op;
+    int64_t ne[4];
+    std::vector<float> data;
+};
+
 struct llb {
+    bool dump = false;
+    std::vector<dump_rec> recs;
     llama_model * model = nullptr;
     llama_context * ctx = nullptr;
     const llama_vocab * vocab = nullptr;
@@ -40,6 +49,25 @@ struct llb {
     int n_batch = 0;
     std::vector<ggml_backend_dev_t> devs;
 };
+
+// scheduler eval callback (cf. examples/eval-callback): keep a copy of every f32 node
+bool dump_cb(struct ggml_tensor * t, bool ask, void * ud) {
+    auto * h = (llb *) ud;
+    if (ask) return h->dump;
+    if (t->type != GGML_TYPE_F32 || ggml_nelements(t) > (1 << 22)) return true;
+    dump_rec r;
+    r.name = t->name;
+    r.op = (int) t->op;
+    for (int i = 0; i < 4; ++i) r.ne[i] = t->ne[i];
+    r.data.resize(ggml_nelements(t));
+    if (ggml_is_contiguous(t)) {
+        ggml_backend_tensor_get(t, r.data.data(), 0, ggml_nbytes(t));
+    } else {
+        return true;
+    }
+    h->recs.push_back(std::move(r));
+    return true;
+}
 
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -54,7 +82,14 @@ int llb_load_backends(const char * cpu_dir, const char * plugin_path, int echo_l
     g_log_echo = echo_log != 0;
     llama_log_set(log_cb, nullptr);
     ggml_log_set(log_cb, nullptr);
-    ggml_backend_load_all_from_path(cpu_dir);
+    // LLB_CPU_LIB pins one CPU variant (e.g. libggml-cpu-x64v3.so) instead of the
+    // score-selected best one — used to measure the reference's own cross-ISA spread
+    const char * cpu_lib = getenv("LLB_CPU_LIB");
+    if (cpu_lib && cpu_lib[0]) {
+        ggml_backend_load(cpu_lib);
+    } else {
+        ggml_backend_load_all_from_path(cpu_dir);
+    }
     if (plugin_path && plugin_path[0]) {
         if (!ggml_backend_load(plugin_path)) return -1;
     }
@@ -70,8 +105,9 @@ int llb_dev_type(int i) { return (int) ggml_backend_dev_type(ggml_backend_dev_ge
 
 // gpu_mask: bit i selects registry device i as a model device; 0 = CPU only.
 void * llb_open(const char * path, unsigned long long gpu_mask, int n_gpu_layers, int flash_attn, int n_ctx,
-                int n_batch, int n_ubatch, int type_k, int type_v, int n_threads, int split_mode) {
+                int n_batch, int n_ubatch, int type_k, int type_v, int n_threads, int split_mode, int dump) {
     auto * h = new llb;
+    h->dump = dump != 0;
     for (size_t i = 0; i < ggml_backend_dev_count(); ++i) {
         if (gpu_mask & (1ull << i)) h->devs.push_back(ggml_backend_dev_get(i));
     }
@@ -94,6 +130,10 @@ void * llb_open(const char * path, unsigned long long gpu_mask, int n_gpu_layers
     cp.n_threads_batch = n_threads;
     cp.no_perf = true;
     cp.op_offload = gpu_mask != 0;
+    if (h->dump) {
+        cp.cb_eval = dump_cb;
+        cp.cb_eval_user_data = h;
+    }
     h->ctx = llama_init_from_model(h->model, cp);
     if (!h->ctx) { llama_model_free(h->model); delete h; return nullptr; }
     h->vocab = llama_model_get_vocab(h->model);
@@ -181,6 +221,16 @@ int llb_log(char * buf, int cap) {
     }
     return n;
 }
+
+int llb_dump_n(void * hp) { return (int) ((llb *) hp)->recs.size(); }
+const char * llb_dump_name(void * hp, int i) { return ((llb *) hp)->recs[i].name.c_str(); }
+int llb_dump_op(void * hp, int i) { return ((llb *) hp)->recs[i].op; }
+long long llb_dump_size(void * hp, int i) { return (long long) ((llb *) hp)->recs[i].data.size(); }
+void llb_dump_data(void * hp, int i, float * out) {
+    auto & r = ((llb *) hp)->recs[i];
+    memcpy(out, r.data.data(), r.data.size() * sizeof(float));
+}
+void llb_dump_clear(void * hp) { ((llb *) hp)->recs.clear(); }
 
 void llb_log_clear(void) {
     std::lock_guard<std::mutex> lk(g_log_mtx);
