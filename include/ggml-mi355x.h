@@ -39,6 +39,15 @@ bool               ggml_backend_is_mi355x(ggml_backend_t backend);
 void ggml_backend_mi355x_set_timing(int enable);
 void ggml_backend_mi355x_reset_timing(void);
 int  ggml_backend_mi355x_get_timing(int kind, double * ms, double * bytes, long * count);
+// whole-graph timing: kind 5 = device time of each graph_compute (events around it, works
+// with hipGraph replay), kind 6 = host time spent inside graph_compute
+void ggml_backend_mi355x_set_graph_timing(int enable);
+
+// run-time switches (default from GGML_MI355X_NO_FUSE / GGML_MI355X_NO_GRAPH): no_fuse = one
+// kernel per ggml node, no_graph = no hipGraph replay of repeated graphs
+void ggml_backend_mi355x_set_flags(int no_fuse, int no_graph);
+// hipGraph statistics since load: graphs captured, replays launched
+void ggml_backend_mi355x_graph_stats(long * captures, long * replays);
 
 // ---- flat kernel ABI (llamacog_amd/csrc/capi.cpp) ---------------------------------------------
 // Plain device pointers + sizes + a HIP stream (NULL = private stream, synchronised on
@@ -76,6 +85,13 @@ int mi355x_fa_scores_d128(const float * q, const uint16_t * k, int64_t n, float 
 int mi355x_flash_attn(const float * q, const void * k, const void * v, const uint16_t * mask, int kv_type, int64_t D,
                       int64_t n_q, int64_t H, int64_t n_kv, int64_t Hkv, float scale, float softcap, float * out,
                       void * stream);
+
+// microbenchmark hook: average device time (us) of one decode GEMV launch over nmat M x K
+// matrices of type wtype sharing one activation row, weights rotating over `copies` copies
+double mi355x_bench_gemv(int wtype, int64_t K, int64_t M, int nmat, int copies, int iters);
+// microbenchmark hook: which = 0 decode flash attention (D 128, H 32, Hkv 8, a cache
+// positions, b unmasked), 1 fused ADD+RMS_NORM+MUL+Q8_K of a floats; device us per launch
+double mi355x_bench_op(int which, int64_t a, int64_t b, int iters);
 
 #ifdef __cplusplus
 }

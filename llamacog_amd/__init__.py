@@ -43,6 +43,19 @@ def plugin_lib() -> ctypes.CDLL:
     return lib
 
 
+def set_flags(no_fuse: bool = False, no_graph: bool = False) -> None:
+    """Run-time switches of the plugin (ggml_backend_mi355x_set_flags): one kernel per ggml
+    node (no_fuse) and / or no hipGraph replay (no_graph)."""
+    plugin_lib().ggml_backend_mi355x_set_flags(1 if no_fuse else 0, 1 if no_graph else 0)
+
+
+def graph_stats() -> tuple[int, int]:
+    """(hipGraphs captured, hipGraph replays) since the plugin was loaded."""
+    c, r = ctypes.c_long(), ctypes.c_long()
+    plugin_lib().ggml_backend_mi355x_graph_stats(ctypes.byref(c), ctypes.byref(r))
+    return c.value, r.value
+
+
 def kernel_timing(lib: ctypes.CDLL, kind: int) -> tuple[float, float, int]:
     ms, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_long()
     lib.ggml_backend_mi355x_get_timing(kind, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(n))

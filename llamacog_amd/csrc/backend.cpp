@@ -16,7 +16,9 @@
 #include "ops.h"
 #include "../../include/ggml-mi355x.h"
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <mutex>
 #include <string>
@@ -30,6 +32,7 @@ using namespace mi355x;
 // timing accumulators (global so bench.py can read them through the C ABI)
 // ------------------------------------------------------------------------------------------
 static std::atomic<int> g_timing{0};
+static std::atomic<int> g_graph_timing{0};
 static std::mutex g_timing_mtx;
 static double g_acc_ms[8], g_acc_bytes[8];
 static long   g_acc_count[8];
@@ -52,12 +55,43 @@ void * exec_ctx::scratch(int slot, size_t bytes) {
     return slot_ptr[slot];
 }
 
+bool exec_ctx::prepare_dyn(ggml_cgraph * g) {
+    dyn_nodes.clear();
+    dyn_host.clear();
+    const int n = ggml_graph_n_nodes(g);
+    for (int i = 0; i < n; ++i) {
+        ggml_tensor * t = ggml_graph_node(g, i);
+        if (t->op == GGML_OP_CPY) {
+            dyn_nodes.push_back(t);
+            dyn_host.push_back(t->src[1]->data);
+        }
+    }
+    if (dyn_host.empty()) return true;
+    // fixed-size table: captured graphs keep its address, so it is never reallocated
+    constexpr size_t DYN_CAP = 16384;
+    if (dyn_host.size() > DYN_CAP) {   // direct pointers; this graph is not replayable
+        dyn_nodes.clear();
+        dyn_host.clear();
+        return false;
+    }
+    if (!dyn_dev) {
+        MI_CHECK(hipMalloc((void **) &dyn_dev, DYN_CAP * sizeof(void *)));
+        dyn_cap = DYN_CAP;
+    }
+    // pageable source: the runtime stages it before returning, so dyn_host can be reused
+    MI_CHECK(hipMemcpyAsync(dyn_dev, dyn_host.data(), dyn_host.size() * sizeof(void *), hipMemcpyHostToDevice, stream));
+    return true;
+}
+
 void exec_ctx::free_scratch() {
     for (int i = 0; i < N_SLOTS; ++i) {
         if (slot_ptr[i]) (void) hipFree(slot_ptr[i]);
         slot_ptr[i] = nullptr;
         slot_size[i] = 0;
     }
+    if (dyn_dev) (void) hipFree(dyn_dev);
+    dyn_dev = nullptr;
+    dyn_cap = 0;
 }
 
 hipEvent_t exec_ctx::get_event() {
@@ -262,11 +296,81 @@ static bool mi_buft_is_ours(ggml_backend_buffer_type_t buft) {
 // ------------------------------------------------------------------------------------------
 // backend (stream)
 // ------------------------------------------------------------------------------------------
+// hipGraph replay of repeated graphs (decode re-submits an identical graph every token).
+// A graph is captured the second time its signature is seen and replayed while it stays
+// unchanged; the signature covers everything a launch reads from the host: op, type,
+// shapes, strides, data pointers and op_params of every node and its sources (the role of
+// ggml-cuda.cu's ggml_graph_node_has_matching_properties, re-stated for this backend).
+struct graph_entry {
+    std::vector<int64_t> sig;
+    int             seen = 0;
+    hipGraphExec_t  exec = nullptr;
+    uint64_t        last_use = 0;
+};
+
 struct mi_backend_ctx {
     int device;
     std::string name;
     exec_ctx ex;
+    std::vector<graph_entry> graphs;   // small LRU of recently seen graphs
+    uint64_t use_clock = 0;
+    bool graphs_broken = false;        // capture failed once: stay eager
 };
+
+static int env_flag(const char * name) {
+    const char * v = getenv(name);
+    return v && atoi(v) != 0 ? 1 : 0;
+}
+static std::atomic<long> g_graph_captures{0}, g_graph_replays{0};
+static std::atomic<int> g_no_fuse{env_flag("GGML_MI355X_NO_FUSE")};
+// rocprofv3 --kernel-trace (ROCm 7.2) segfaults the profiled process when it traces the
+// kernels of a replayed hipGraph; under kernel tracing the same kernels are launched
+// eagerly instead (profiles/README.md)
+static std::atomic<int> g_no_graph{env_flag("GGML_MI355X_NO_GRAPH") | env_flag("ROCPROF_KERNEL_TRACE")};
+
+namespace mi355x {
+bool fusion_enabled() { return g_no_fuse.load(std::memory_order_relaxed) == 0; }
+bool graphs_enabled() { return g_no_graph.load(std::memory_order_relaxed) == 0; }
+}
+
+static void graph_signature(ggml_cgraph * cgraph, std::vector<int64_t> & sig) {
+    sig.clear();
+    const int n = ggml_graph_n_nodes(cgraph);
+    sig.reserve((size_t) n * 48);
+    // CPY destinations (and the CPY nodes, which alias them) are read through the dynamic
+    // pointer table, so their addresses / view offsets are not part of the signature
+    static thread_local std::vector<const ggml_tensor *> dyn;
+    dyn.clear();
+    for (int i = 0; i < n; ++i) {
+        const ggml_tensor * t = ggml_graph_node(cgraph, i);
+        if (t->op == GGML_OP_CPY) { dyn.push_back(t); dyn.push_back(t->src[1]); }
+    }
+    auto is_dyn = [&](const ggml_tensor * t) { return std::find(dyn.begin(), dyn.end(), t) != dyn.end(); };
+    auto put_tensor = [&](const ggml_tensor * t) {
+        sig.push_back(is_dyn(t) ? 0 : (int64_t) (intptr_t) t->data);
+        sig.push_back((int64_t) t->type);
+        for (int k = 0; k < 4; ++k) sig.push_back(t->ne[k]);
+        for (int k = 0; k < 4; ++k) sig.push_back((int64_t) t->nb[k]);
+    };
+    sig.push_back(n);
+    for (int i = 0; i < n; ++i) {
+        const ggml_tensor * t = ggml_graph_node(cgraph, i);
+        sig.push_back((int64_t) (intptr_t) t);
+        sig.push_back((int64_t) t->op);
+        put_tensor(t);
+        const int32_t * pp = t->op_params;
+        const bool skip_params = t->op == GGML_OP_VIEW && is_dyn(t);   // view offset = n_past
+        for (int k = 0; k < GGML_MAX_OP_PARAMS / 8; ++k) {
+            int64_t v = 0;
+            if (!skip_params) memcpy(&v, pp + 2 * k, 8);
+            sig.push_back(v);
+        }
+        for (int j = 0; j < GGML_MAX_SRC; ++j) {
+            if (t->src[j]) put_tensor(t->src[j]);
+            else sig.push_back(-1);
+        }
+    }
+}
 
 static const char * mi_backend_get_name(ggml_backend_t backend) {
     return ((mi_backend_ctx *) backend->context)->name.c_str();
@@ -278,6 +382,9 @@ static void mi_backend_free(ggml_backend_t backend) {
     MI_CHECK(hipStreamSynchronize(ctx->ex.stream));
     ctx->ex.collect_timing();
     for (auto e : ctx->ex.event_pool) (void) hipEventDestroy(e);
+    for (auto & g : ctx->graphs) {
+        if (g.exec) (void) hipGraphExecDestroy(g.exec);
+    }
     ctx->ex.free_scratch();
     MI_CHECK(hipStreamDestroy(ctx->ex.stream));
     delete ctx;
@@ -331,13 +438,92 @@ static void mi_backend_synchronize(ggml_backend_t backend) {
     ctx->ex.collect_timing();
 }
 
+static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
+    ex.qcache_clear();
+    ex.done.clear();
+    const int n = ggml_graph_n_nodes(cgraph);
+    for (int i = 0; i < n;) {
+        i += op_compute(ex, cgraph, i);
+    }
+}
+
+// returns true when the graph was launched as (or captured into) a hipGraph
+static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
+    static thread_local std::vector<int64_t> sig;
+    graph_signature(cgraph, sig);
+    graph_entry * e = nullptr;
+    for (auto & g : ctx->graphs) {
+        if (g.sig == sig) { e = &g; break; }
+    }
+    if (!e) {
+        constexpr size_t MAX_GRAPHS = 4;
+        if (ctx->graphs.size() >= MAX_GRAPHS) {
+            auto lru = ctx->graphs.begin();
+            for (auto it = ctx->graphs.begin(); it != ctx->graphs.end(); ++it) {
+                if (it->last_use < lru->last_use) lru = it;
+            }
+            if (lru->exec) MI_CHECK(hipGraphExecDestroy(lru->exec));
+            ctx->graphs.erase(lru);
+        }
+        ctx->graphs.emplace_back();
+        e = &ctx->graphs.back();
+        e->sig = sig;
+    }
+    e->last_use = ++ctx->use_clock;
+    if (e->exec) {
+        MI_CHECK(hipGraphLaunch(e->exec, ctx->ex.stream));
+        g_graph_replays.fetch_add(1);
+        return true;
+    }
+    if (++e->seen < 2) return false;   // first sighting runs eagerly (sizes the scratch arena)
+
+    hipGraph_t g = nullptr;
+    ctx->ex.capturing = true;
+    MI_CHECK(hipStreamBeginCapture(ctx->ex.stream, hipStreamCaptureModeRelaxed));
+    run_nodes(ctx->ex, cgraph);
+    const hipError_t cerr = hipStreamEndCapture(ctx->ex.stream, &g);
+    ctx->ex.capturing = false;
+    if (cerr != hipSuccess || g == nullptr ||
+        hipGraphInstantiate(&e->exec, g, nullptr, nullptr, 0) != hipSuccess) {
+        MI_LOG_WARN("mi355x: hipGraph capture failed (%s); running graphs eagerly\n", hipGetErrorString(cerr));
+        (void) hipGetLastError();
+        if (g) (void) hipGraphDestroy(g);
+        e->exec = nullptr;
+        ctx->graphs_broken = true;
+        return false;
+    }
+    MI_CHECK(hipGraphDestroy(g));
+    MI_CHECK(hipGraphLaunch(e->exec, ctx->ex.stream));
+    g_graph_captures.fetch_add(1);
+    return true;
+}
+
 static enum ggml_status mi_backend_graph_compute(ggml_backend_t backend, ggml_cgraph * cgraph) {
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
     ctx->ex.timing = g_timing.load(std::memory_order_relaxed) != 0;
-    const int n = ggml_graph_n_nodes(cgraph);
-    for (int i = 0; i < n;) {
-        i += op_compute(ctx->ex, cgraph, i);
+    // whole-graph timing (kind TK_GRAPH: device time between events around the graph;
+    // TK_GRAPH_HOST: host time spent in this call) — works with hipGraph replay
+    const bool gtime = g_graph_timing.load(std::memory_order_relaxed) != 0;
+    const auto h0 = std::chrono::steady_clock::now();
+    hipEvent_t gbeg = nullptr;
+    if (gtime) {
+        gbeg = ctx->ex.get_event();
+        MI_CHECK(hipEventRecord(gbeg, ctx->ex.stream));
+    }
+    const bool dyn_ok = ctx->ex.prepare_dyn(cgraph);
+    const bool use_graph = dyn_ok && graphs_enabled() && !ctx->graphs_broken && !ctx->ex.timing;
+    if (!use_graph || !graph_compute_hipgraph(ctx, cgraph)) {
+        run_nodes(ctx->ex, cgraph);
+    }
+    if (gtime) {
+        hipEvent_t gend = ctx->ex.get_event();
+        MI_CHECK(hipEventRecord(gend, ctx->ex.stream));
+        ctx->ex.pending.push_back({gbeg, gend, 0.0, TK_GRAPH});
+        const double hms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+        std::lock_guard<std::mutex> lk(g_timing_mtx);
+        g_acc_ms[TK_GRAPH_HOST] += hms;
+        g_acc_count[TK_GRAPH_HOST] += 1;
     }
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) {
@@ -585,6 +771,18 @@ GGML_BACKEND_API ggml_backend_t ggml_backend_mi355x_init(int device) {
 }
 
 GGML_BACKEND_API bool ggml_backend_is_mi355x(ggml_backend_t backend) { return mi_backend_is_ours(backend); }
+
+GGML_BACKEND_API void ggml_backend_mi355x_graph_stats(long * captures, long * replays) {
+    if (captures) *captures = g_graph_captures.load();
+    if (replays) *replays = g_graph_replays.load();
+}
+
+GGML_BACKEND_API void ggml_backend_mi355x_set_graph_timing(int enable) { g_graph_timing.store(enable ? 1 : 0); }
+
+GGML_BACKEND_API void ggml_backend_mi355x_set_flags(int no_fuse, int no_graph) {
+    g_no_fuse.store(no_fuse ? 1 : 0);
+    g_no_graph.store(no_graph ? 1 : 0);
+}
 
 GGML_BACKEND_API void ggml_backend_mi355x_set_timing(int enable) { g_timing.store(enable ? 1 : 0); }
 

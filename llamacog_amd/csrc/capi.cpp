@@ -8,6 +8,8 @@
 #include "../../include/ggml-mi355x.h"
 
 #include <cstring>
+#include <functional>
+#include <vector>
 
 using namespace mi355x;
 
@@ -219,3 +221,147 @@ GGML_BACKEND_API int mi355x_fa_scores_d128(const float * q, const uint16_t * k, 
 }
 
 }  // extern "C"
+
+// ---- microbenchmark hook: decode GEMV (k_gemv.hip) in isolation ---------------------------------
+// nmat matrices of M x K (wtype) share one activation row; `copies` rotating weight copies
+// (> MALL size in total) make every launch stream from HBM like a real layer walk.  Returns
+// the average device time per grouped launch in microseconds (activation quantized once).
+namespace mi355x {
+}
+
+extern "C" GGML_BACKEND_API double mi355x_bench_gemv(int wtype, int64_t K, int64_t M, int nmat, int copies, int iters) {
+    const ggml_type t = (ggml_type) wtype;
+    const size_t row = ggml_row_size(t, K);
+    const size_t mat = row * (size_t) M;
+    std::vector<char *> pool((size_t) copies * nmat);
+    for (auto & p : pool) {
+        MI_CHECK(hipMalloc(&p, mat));
+        // small positive f16 scales everywhere keep values finite; content is irrelevant
+        MI_CHECK(hipMemset(p, 0x11, mat));
+    }
+    float * x; float * y;
+    MI_CHECK(hipMalloc(&x, K * 4));
+    MI_CHECK(hipMalloc(&y, M * 4 * nmat));
+    MI_CHECK(hipMemset(x, 0x3c, K * 4));
+    scoped_ctx sc(nullptr);
+    std::vector<ggml_tensor> W(nmat), Y(nmat);
+    ggml_tensor X;
+    const int64_t nex[4] = {K, 1, 1, 1};
+    init_tensor(X, GGML_TYPE_F32, nex, x);
+    std::vector<ggml_tensor *> mms(nmat);
+    for (int m = 0; m < nmat; ++m) {
+        const int64_t new_[4] = {K, M, 1, 1}, ney[4] = {M, 1, 1, 1};
+        init_tensor(W[m], t, new_, pool[m]);
+        init_tensor(Y[m], GGML_TYPE_F32, ney, y + m * M);
+        Y[m].op = GGML_OP_MUL_MAT;
+        Y[m].src[0] = &W[m];
+        Y[m].src[1] = &X;
+        mms[m] = &Y[m];
+    }
+    if (!gemv_supported(mms[0])) return -1.0;
+    hipEvent_t e0, e1;
+    MI_CHECK(hipEventCreate(&e0));
+    MI_CHECK(hipEventCreate(&e1));
+    auto run = [&](int it) {
+        for (int m = 0; m < nmat; ++m) W[m].data = pool[(size_t) (it % copies) * nmat + m];
+        gemv_group(sc.ex, mms.data(), nmat, nullptr);
+    };
+    run(0);   // quantizes X into the cache; later launches reuse it
+    for (int i = 1; i < 4; ++i) run(i);
+    MI_CHECK(hipEventRecord(e0, sc.ex.stream));
+    for (int i = 0; i < iters; ++i) run(i);
+    MI_CHECK(hipEventRecord(e1, sc.ex.stream));
+    MI_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    MI_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    MI_CHECK(hipEventDestroy(e0));
+    MI_CHECK(hipEventDestroy(e1));
+    for (auto p : pool) MI_CHECK(hipFree(p));
+    MI_CHECK(hipFree(x));
+    MI_CHECK(hipFree(y));
+    return ms * 1000.0 / iters;
+}
+
+// ---- microbenchmark hook: the per-layer small ops in isolation -----------------------------------
+// which = 0: decode FLASH_ATTN_EXT (exact f16 path) with D = 128, H = 32, Hkv = 8, a cache
+//            positions of which the first b are unmasked (Llama-3-8B layout);
+//         1: fused residual ADD + RMS_NORM + MUL + Q8_K quantization of one row of a floats.
+// Returns the average device time per launch in microseconds.
+extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t b, int iters) {
+    scoped_ctx sc(nullptr);
+    hipEvent_t e0, e1;
+    MI_CHECK(hipEventCreate(&e0));
+    MI_CHECK(hipEventCreate(&e1));
+    std::vector<void *> bufs;
+    auto dalloc = [&](size_t n, int pattern) {
+        void * p;
+        MI_CHECK(hipMalloc(&p, n));
+        MI_CHECK(hipMemset(p, pattern, n));
+        bufs.push_back(p);
+        return p;
+    };
+    std::function<void()> run;
+    ggml_tensor Q, K, V, Mk, O, X, R, A, N, Wt, Mu;
+    if (which == 0) {
+        const int64_t D = 128, H = 32, Hkv = 8, n_kv = a;
+        float * q = (float *) dalloc(D * H * 4, 0x3c);
+        void * k = dalloc(D * Hkv * n_kv * 2, 0x3c);
+        void * v = dalloc(D * Hkv * n_kv * 2, 0x3c);
+        std::vector<uint16_t> hm(n_kv);
+        for (int64_t i = 0; i < n_kv; ++i) hm[i] = i < b ? 0 : 0xFC00;
+        uint16_t * m = (uint16_t *) dalloc(n_kv * 2, 0);
+        MI_CHECK(hipMemcpy(m, hm.data(), n_kv * 2, hipMemcpyHostToDevice));
+        float * out = (float *) dalloc(D * H * 4, 0);
+        const int64_t neq[4] = {D, H, 1, 1};
+        init_tensor(Q, GGML_TYPE_F32, neq, q);
+        std::swap(Q.ne[1], Q.ne[2]); std::swap(Q.nb[1], Q.nb[2]);
+        const int64_t nek[4] = {D, Hkv, n_kv, 1};
+        init_tensor(K, GGML_TYPE_F16, nek, k);
+        std::swap(K.ne[1], K.ne[2]); std::swap(K.nb[1], K.nb[2]);
+        init_tensor(V, GGML_TYPE_F16, nek, v);
+        std::swap(V.ne[1], V.ne[2]); std::swap(V.nb[1], V.nb[2]);
+        const int64_t nem[4] = {n_kv, 1, 1, 1}, neo[4] = {D, H, 1, 1};
+        init_tensor(Mk, GGML_TYPE_F16, nem, m);
+        init_tensor(O, GGML_TYPE_F32, neo, out);
+        O.op = GGML_OP_FLASH_ATTN_EXT;
+        O.src[0] = &Q; O.src[1] = &K; O.src[2] = &V; O.src[3] = &Mk;
+        const float scale = 0.088f, zero = 0.0f;
+        memcpy(O.op_params, &scale, 4);
+        memcpy(O.op_params + 1, &zero, 4);
+        memcpy(O.op_params + 2, &zero, 4);
+        run = [&] { op_flash_attn(sc.ex, &O); };
+    } else {
+        const int64_t n = a;
+        const int64_t ne[4] = {n, 1, 1, 1};
+        init_tensor(X, GGML_TYPE_F32, ne, dalloc(n * 4, 0x3c));
+        init_tensor(R, GGML_TYPE_F32, ne, dalloc(n * 4, 0x3c));
+        init_tensor(A, GGML_TYPE_F32, ne, dalloc(n * 4, 0));
+        init_tensor(N, GGML_TYPE_F32, ne, dalloc(n * 4, 0));
+        init_tensor(Wt, GGML_TYPE_F32, ne, dalloc(n * 4, 0x3c));
+        init_tensor(Mu, GGML_TYPE_F32, ne, dalloc(n * 4, 0));
+        A.op = GGML_OP_ADD; A.src[0] = &X; A.src[1] = &R;
+        N.op = GGML_OP_RMS_NORM; N.src[0] = &A;
+        const float eps = 1e-5f;
+        memcpy(N.op_params, &eps, 4);
+        Mu.op = GGML_OP_MUL; Mu.src[0] = &N; Mu.src[1] = &Wt;
+        // a Q4_K consumer so the norm quantizes to Q8_K
+        static ggml_tensor W, MM;
+        const int64_t new_[4] = {n, 16, 1, 1}, nem_[4] = {16, 1, 1, 1};
+        init_tensor(W, GGML_TYPE_Q4_K, new_, dalloc(ggml_row_size(GGML_TYPE_Q4_K, n) * 16, 0x11));
+        init_tensor(MM, GGML_TYPE_F32, nem_, dalloc(64, 0));
+        MM.op = GGML_OP_MUL_MAT; MM.src[0] = &W; MM.src[1] = &Mu;
+        run = [&] { fused_norm(sc.ex, &A, &N, &Mu, &MM); };
+    }
+    for (int i = 0; i < 3; ++i) run();
+    MI_CHECK(hipEventRecord(e0, sc.ex.stream));
+    for (int i = 0; i < iters; ++i) run();
+    MI_CHECK(hipEventRecord(e1, sc.ex.stream));
+    MI_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    MI_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    MI_CHECK(hipEventDestroy(e0));
+    MI_CHECK(hipEventDestroy(e1));
+    MI_CHECK(hipStreamSynchronize(sc.ex.stream));
+    for (void * p : bufs) MI_CHECK(hipFree(p));
+    return ms * 1000.0 / iters;
+}

@@ -7,12 +7,15 @@
 // DESIGN.md (RMS_NORM + MUL).
 #include "ops.h"
 
+#include <algorithm>
+
 namespace mi355x {
 
 bool mmv_q_supported_type(ggml_type t);
 void mul_mat_vec(exec_ctx & ctx, ggml_tensor * dst, const q8_act * pre);
 bool mmq_supported(const ggml_tensor * dst);
 void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst);
+
 bool fattn_supported(const ggml_tensor * op);
 
 static bool is_f32(const ggml_tensor * t) { return t && t->type == GGML_TYPE_F32; }
@@ -122,16 +125,261 @@ bool op_supported(const ggml_tensor * op) {
 }
 
 void op_mul_mat(exec_ctx & ctx, ggml_tensor * dst) {
-    if (mmq_supported(dst)) {
+    if (gemv_supported(dst)) {
+        ggml_tensor * one[1] = {dst};
+        gemv_group(ctx, one, 1, nullptr);
+    } else if (mmq_supported(dst)) {
         mul_mat_q(ctx, dst);
     } else {
         mul_mat_vec(ctx, dst, nullptr);
     }
 }
 
+
+static ggml_tensor * at(ggml_cgraph * g, int i, int n) { return i < n ? ggml_graph_node(g, i) : nullptr; }
+
+// the MUL by a norm weight row that directly follows RMS_NORM node i, or nullptr
+static ggml_tensor * norm_weight_mul(ggml_cgraph * g, int i, int n) {
+    ggml_tensor * node = ggml_graph_node(g, i);
+    ggml_tensor * nx = at(g, i + 1, n);
+    if (nx && nx->op == GGML_OP_MUL && nx->src[0] == node && is_f32(nx->src[1]) &&
+        nx->src[1]->ne[0] == node->ne[0] && nx->src[1]->ne[1] == 1 && nx->src[1]->ne[2] == 1 &&
+        nx->src[1]->ne[3] == 1 && ggml_are_same_shape(nx, node) && node->nb[1] == nx->nb[1]) {
+        return nx;
+    }
+    return nullptr;
+}
+
+static bool overlaps(const ggml_tensor * a, const ggml_tensor * b) {
+    if (!a || !b || !a->data || !b->data) return false;
+    const char * a0 = (const char *) a->data, * a1 = a0 + ggml_nbytes(a);
+    const char * b0 = (const char *) b->data, * b1 = b0 + ggml_nbytes(b);
+    return a0 < b1 && b0 < a1;
+}
+
+// may node j run before the nodes i+1 .. j-1 (except those in `skip`)?  Its output must
+// not touch anything those nodes read or write (ggml-alloc re-uses memory of tensors
+// whose last consumer ran, so a later node's output can alias an earlier temporary).
+static bool can_hoist(ggml_cgraph * g, int i, int j, const ggml_tensor * const * outs, int nout,
+                      const std::vector<const ggml_tensor *> & skip) {
+    for (int k = i + 1; k < j; ++k) {
+        const ggml_tensor * t = ggml_graph_node(g, k);
+        if (std::find(skip.begin(), skip.end(), t) != skip.end()) continue;
+        // views / reshapes / permutes neither read nor write memory
+        if (t->op == GGML_OP_NONE || t->op == GGML_OP_VIEW || t->op == GGML_OP_RESHAPE ||
+            t->op == GGML_OP_PERMUTE || t->op == GGML_OP_TRANSPOSE) continue;
+        for (int o = 0; o < nout; ++o) {
+            if (overlaps(outs[o], t)) return false;
+            for (int s = 0; s < GGML_MAX_SRC; ++s) {
+                if (overlaps(outs[o], t->src[s])) return false;
+            }
+        }
+    }
+    return true;
+}
+
+// SiLU node that directly follows MUL_MAT node i and reads exactly its output, or nullptr
+static ggml_tensor * silu_after(ggml_cgraph * g, int i, int n) {
+    ggml_tensor * mm = ggml_graph_node(g, i);
+    ggml_tensor * nx = at(g, i + 1, n);
+    if (nx && nx->op == GGML_OP_UNARY && ggml_get_unary_op(nx) == GGML_UNARY_OP_SILU && nx->src[0] == mm &&
+        nx->type == GGML_TYPE_F32 && ggml_is_contiguous(nx) && ggml_are_same_shape(nx, mm)) {
+        return nx;
+    }
+    return nullptr;
+}
+
+// base node of a (chain of) view/reshape nodes
+static const ggml_tensor * base_of(const ggml_tensor * t) {
+    while (t && t->view_src) t = t->view_src;
+    return t;
+}
+
+// index of `t` among the graph nodes, -1 for leaves (weights, inputs)
+static int node_index(ggml_cgraph * g, const ggml_tensor * t) {
+    const int n = ggml_graph_n_nodes(g);
+    for (int k = 0; k < n; ++k) {
+        if (ggml_graph_node(g, k) == t) return k;
+    }
+    return -1;
+}
+
+// has the data of `t` been produced when node i runs (earlier node, leaf, or hoisted)?
+static bool computed_before(exec_ctx & ctx, ggml_cgraph * g, const ggml_tensor * t, int i) {
+    const ggml_tensor * b = base_of(t);
+    if (std::find(ctx.done.begin(), ctx.done.end(), b) != ctx.done.end()) return true;
+    const int k = node_index(g, b);
+    return k < i;
+}
+
+// the f32 -> f16 CPY (KV-cache store) of `out` within the next few nodes after position p:
+// src is `out` itself or a contiguous reshape of it, destination contiguous f16 of the same
+// size.  Returns the CPY node or nullptr.
+static ggml_tensor * f16_store_of(ggml_cgraph * g, const ggml_tensor * out, int p, int n) {
+    if (!ggml_is_contiguous(out) || out->type != GGML_TYPE_F32) return nullptr;
+    for (int k = p + 1; k < n && k <= p + 12; ++k) {
+        ggml_tensor * c = ggml_graph_node(g, k);
+        if (c->op != GGML_OP_CPY) continue;
+        const ggml_tensor * s = c->src[0];
+        const bool same = s == out || (base_of(s) == out && s->data == out->data && ggml_is_contiguous(s));
+        if (!same) continue;
+        const ggml_tensor * d = c->src[1];
+        if (d->type == GGML_TYPE_F16 && ggml_is_contiguous(d) && ggml_nelements(d) == ggml_nelements(out)) return c;
+    }
+    return nullptr;
+}
+
+// NORM-mode ROPE (one token) applied to the output of MUL_MAT `mm` within the next few
+// nodes (through a contiguous reshape), or nullptr
+static ggml_tensor * rope_of(ggml_cgraph * g, const ggml_tensor * mm, int p, int n) {
+    for (int k = p + 1; k < n && k <= p + 4; ++k) {
+        ggml_tensor * r = ggml_graph_node(g, k);
+        if (r->op != GGML_OP_ROPE) continue;
+        const ggml_tensor * x = r->src[0];
+        if (base_of(x) != mm || x->data != mm->data || !ggml_is_contiguous(x) || !ggml_is_contiguous(r)) return nullptr;
+        if (r->op_params[2] != 0 || r->type != GGML_TYPE_F32) return nullptr;   // NORM mode only
+        const int n_dims = r->op_params[1];
+        if (x->ne[2] != 1 || x->ne[3] != 1 || x->ne[0] % 2 != 0 || n_dims > x->ne[0] || n_dims % 2 != 0) return nullptr;
+        if (r->src[1]->type != GGML_TYPE_I32) return nullptr;
+        return r;
+    }
+    return nullptr;
+}
+
+// does t overlap any of outs?  An exact alias of `self` (an in-place SiLU / ROPE that
+// ggml-alloc placed in the projection's own buffer) is allowed: the epilogue writes the
+// projection value and then the derived value to the same address from the same lane.
+static bool overlaps_any(const ggml_tensor * t, const std::vector<const ggml_tensor *> & outs,
+                         const ggml_tensor * self = nullptr) {
+    for (const ggml_tensor * o : outs) {
+        if (o == t) continue;
+        if (o == self && t->data == self->data && ggml_nbytes(t) == ggml_nbytes(self)) continue;
+        if (overlaps(t, o)) return true;
+    }
+    return false;
+}
+
+// decode mat-vec: launch node i together with up to two later MUL_MATs on the same src1
+// (Q/K/V, gate/up) in one grouped kernel, with fused epilogues: the SiLU that follows a
+// projection, the NORM-mode ROPE of a projection, and f16 KV-cache stores (CPY) of a
+// projection or of its rope.  Every hoisted node's outputs are checked against what the
+// skipped-over nodes read and write, and against the other outputs of the launch.
+int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * mm0 = ggml_graph_node(g, i);
+    ggml_tensor * mms[3] = {mm0, nullptr, nullptr};
+    gemv_epi epi;
+    int nm = 1;
+    std::vector<const ggml_tensor *> absorbed;   // nodes this launch computes (besides node i)
+    std::vector<const ggml_tensor *> outs = {mm0};
+
+    // epilogues of matrix m (node position pm): silu, or rope (+ its cache store), or a cache store
+    auto add_epilogues = [&](int m, int pm) {
+        ggml_tensor * mm = mms[m];
+        if (ggml_tensor * sl = silu_after(g, pm, n)) {
+            const ggml_tensor * o[1] = {sl};
+            if (!overlaps_any(sl, outs, mm) && (pm == i || can_hoist(g, i, pm + 1, o, 1, absorbed))) {
+                epi.silu[m] = sl;
+                absorbed.push_back(sl);
+                outs.push_back(sl);
+            }
+            return;
+        }
+        if (ggml_tensor * r = rope_of(g, mm, pm, n)) {
+            const ggml_tensor * o[1] = {r};
+            const int pr = node_index(g, r);
+            if (!overlaps_any(r, outs, mm) && can_hoist(g, i, pr, o, 1, absorbed)) {
+                epi.rope[m] = r;
+                absorbed.push_back(r);
+                outs.push_back(r);
+                if (ggml_tensor * c = f16_store_of(g, r, pr, n)) {
+                    void * const * slot = ctx.dyn_slot(c);
+                    const ggml_tensor * oc[1] = {c->src[1]};
+                    if (slot && !overlaps_any(c->src[1], outs) && can_hoist(g, i, node_index(g, c), oc, 1, absorbed)) {
+                        epi.rope_f16[m] = slot;
+                        absorbed.push_back(c);
+                        outs.push_back(c->src[1]);
+                    }
+                }
+            }
+            return;
+        }
+        if (ggml_tensor * c = f16_store_of(g, mm, pm, n)) {
+            void * const * slot = ctx.dyn_slot(c);
+            const ggml_tensor * oc[1] = {c->src[1]};
+            if (slot && !overlaps_any(c->src[1], outs) && can_hoist(g, i, node_index(g, c), oc, 1, absorbed)) {
+                epi.f16out[m] = slot;
+                absorbed.push_back(c);
+                outs.push_back(c->src[1]);
+            }
+        }
+    };
+    add_epilogues(0, i);
+
+    for (int j = i + 1; j < n && j <= i + 12 && nm < 3; ++j) {
+        ggml_tensor * c = ggml_graph_node(g, j);
+        if (c->op != GGML_OP_MUL_MAT || c->src[1] != mm0->src[1] || !gemv_supported(c)) continue;
+        if (std::find(ctx.done.begin(), ctx.done.end(), c) != ctx.done.end()) continue;
+        if (c->src[0]->type != mm0->src[0]->type || c->src[0]->ne[0] != mm0->src[0]->ne[0]) continue;
+        const ggml_tensor * o[1] = {c};
+        if (overlaps_any(c, outs) || !can_hoist(g, i, j, o, 1, absorbed)) continue;
+        mms[nm] = c;
+        absorbed.push_back(c);
+        outs.push_back(c);
+        add_epilogues(nm, j);
+        ++nm;
+    }
+    gemv_group(ctx, mms, nm, &epi);
+    // node i+1 when it is node i's SiLU is consumed here; everything else is skipped later
+    const bool next_absorbed = epi.silu[0] && epi.silu[0] == at(g, i + 1, n);
+    for (const ggml_tensor * t : absorbed) {
+        if (!(next_absorbed && t == epi.silu[0])) ctx.done.push_back(t);
+    }
+    return next_absorbed ? 2 : 1;
+}
+
+// ROPE of Q at node i + ROPE of K (same parameters and positions, input already computed)
+// in one launch, each with its f16 KV-cache store fused when present
+static int op_rope_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * r0 = ggml_graph_node(g, i);
+    ggml_tensor * nodes[2] = {r0, nullptr};
+    void * const * cache[2] = {nullptr, nullptr};
+    std::vector<const ggml_tensor *> absorbed;
+    int nr = 1;
+    for (int j = i + 1; j < n && j <= i + 6; ++j) {
+        ggml_tensor * c = ggml_graph_node(g, j);
+        if (c->op != GGML_OP_ROPE) continue;
+        if (c->src[1] != r0->src[1] || c->src[2] != r0->src[2] || memcmp(c->op_params, r0->op_params, 15 * sizeof(int32_t)) != 0) break;
+        if (c->src[0]->ne[0] != r0->src[0]->ne[0] || !computed_before(ctx, g, c->src[0], i)) break;
+        const ggml_tensor * outs[1] = {c};
+        if (!can_hoist(g, i, j, outs, 1, absorbed)) break;
+        nodes[nr++] = c;
+        absorbed.push_back(c);
+        break;
+    }
+    for (int k = 0; k < nr; ++k) {
+        ggml_tensor * c = f16_store_of(g, nodes[k], node_index(g, nodes[k]), n);
+        if (!c) continue;
+        void * const * slot = ctx.dyn_slot(c);
+        const ggml_tensor * outs[1] = {c->src[1]};
+        if (!slot || !can_hoist(g, i, node_index(g, c), outs, 1, absorbed)) continue;
+        cache[k] = slot;
+        absorbed.push_back(c);
+    }
+    op_rope_multi(ctx, nodes, nr, cache);
+    for (const ggml_tensor * t : absorbed) ctx.done.push_back(t);
+    return 1;
+}
+
 int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
     ggml_tensor * node = ggml_graph_node(cgraph, i);
     if (ggml_is_empty(node)) return 1;
+    if (!ctx.done.empty()) {
+        auto it = std::find(ctx.done.begin(), ctx.done.end(), node);
+        if (it != ctx.done.end()) {   // already computed by a grouped launch
+            ctx.done.erase(it);
+            return 1;
+        }
+    }
     const int n = ggml_graph_n_nodes(cgraph);
     switch (node->op) {
         case GGML_OP_NONE:
@@ -141,6 +389,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
         case GGML_OP_TRANSPOSE:
             return 1;
         case GGML_OP_MUL_MAT:
+            if (fusion_enabled() && gemv_supported(node)) return op_gemv_grouped(ctx, cgraph, i, n);
             op_mul_mat(ctx, node);
             return 1;
         case GGML_OP_GET_ROWS:
@@ -150,24 +399,33 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             // fuse y = rms_norm(x) * w when the next node is that MUL (build_norm,
             // src/llama-graph.cpp:464-497); the norm output is still written, so other
             // readers of it stay correct.
-            if (i + 1 < n) {
-                ggml_tensor * nx = ggml_graph_node(cgraph, i + 1);
-                if (nx->op == GGML_OP_MUL && nx->src[0] == node && is_f32(nx->src[1]) &&
-                    nx->src[1]->ne[0] == node->ne[0] && nx->src[1]->ne[1] == 1 && nx->src[1]->ne[2] == 1 &&
-                    nx->src[1]->ne[3] == 1 && ggml_are_same_shape(nx, node) && node->nb[1] == nx->nb[1]) {
-                    op_rms_norm(ctx, node, nx->src[1], nx);
-                    return 2;
-                }
+            ggml_tensor * mul = norm_weight_mul(cgraph, i, n);
+            if (fusion_enabled() && fused_norm(ctx, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
+                return mul ? 2 : 1;
             }
-            op_rms_norm(ctx, node, nullptr, nullptr);
-            return 1;
+            op_rms_norm(ctx, node, mul ? mul->src[1] : nullptr, mul);
+            return mul ? 2 : 1;
         }
         case GGML_OP_NORM:
             op_norm(ctx, node);
             return 1;
         case GGML_OP_ADD:
-        case GGML_OP_SUB:
+            // residual ADD feeding the next RMS_NORM (+ norm-weight MUL, + MUL_MAT input)
+            if (fusion_enabled()) {
+                ggml_tensor * nx = at(cgraph, i + 1, n);
+                if (nx && nx->op == GGML_OP_RMS_NORM && nx->src[0] == node) {
+                    ggml_tensor * mul = norm_weight_mul(cgraph, i + 1, n);
+                    if (fused_norm(ctx, node, nx, mul, at(cgraph, i + (mul ? 3 : 2), n))) return mul ? 3 : 2;
+                }
+            }
+            op_binary(ctx, node);
+            return 1;
         case GGML_OP_MUL:
+            // gated-FFN product feeding the down projection: multiply + quantize in one pass
+            if (fusion_enabled() && fused_mul_quant(ctx, node, at(cgraph, i + 1, n))) return 1;
+            op_binary(ctx, node);
+            return 1;
+        case GGML_OP_SUB:
         case GGML_OP_DIV:
             op_binary(ctx, node);
             return 1;
@@ -178,21 +436,34 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             op_unary(ctx, node);
             return 1;
         case GGML_OP_CPY:
-            op_cpy(ctx, node->src[0], node->src[1]);
+            op_cpy(ctx, node->src[0], node->src[1], node);
             return 1;
         case GGML_OP_DUP:
         case GGML_OP_CONT:
-            op_cpy(ctx, node->src[0], node);
+            op_cpy(ctx, node->src[0], node, nullptr);
             return 1;
         case GGML_OP_ROPE:
+            if (fusion_enabled()) return op_rope_grouped(ctx, cgraph, i, n);
             op_rope(ctx, node);
             return 1;
         case GGML_OP_SOFT_MAX:
             op_soft_max(ctx, node);
             return 1;
-        case GGML_OP_FLASH_ATTN_EXT:
-            op_flash_attn(ctx, node);
+        case GGML_OP_FLASH_ATTN_EXT: {
+            // attention output -> reshape -> output projection: quantize in the FA epilogue
+            const ggml_tensor * mm = nullptr;
+            if (fusion_enabled()) {
+                ggml_tensor * r = at(cgraph, i + 1, n);
+                ggml_tensor * c = at(cgraph, i + 2, n);
+                if (r && c && (r->op == GGML_OP_RESHAPE || r->op == GGML_OP_VIEW) && r->view_src == node &&
+                    r->data == node->data && ggml_is_contiguous(r) && c->op == GGML_OP_MUL_MAT && c->src[1] == r &&
+                    gemv_supported(c)) {
+                    mm = c;
+                }
+            }
+            op_flash_attn(ctx, node, mm);
             return 1;
+        }
         default:
             GGML_ABORT("mi355x: op %s reached graph_compute but is not supported", ggml_op_desc(node));
     }

@@ -1,0 +1,33 @@
+// fattn.h — shared argument block of the flash-attention kernels (k_fattn.hip: split-K
+// f32 kernel; k_fattn_exact.hip: the CPU-exact f16 kernel).
+#pragma once
+
+#include "ops.h"
+
+namespace mi355x {
+
+struct fa_args {
+    const char * q; int64_t nbq1, nbq2, nbq3;
+    const char * k; int64_t nbk1, nbk2, nbk3;
+    const char * v; int64_t nbv1, nbv2, nbv3;
+    const char * mask; int64_t nbm1; int64_t mask_ne1;
+    int k_type, v_type;
+    int64_t D, n_kv, n_q, H, Hkv, chunk;
+    float scale, softcap, max_bias, m0, m1; uint32_t n_head_log2;
+    float * part;      // [nchunks][n_q][H][D+2]  (M, S, O[D])
+    float * dst;       // final output when nchunks == 1
+    int64_t nb1_dst, nb2_dst;
+    int nchunks;
+    // fused quantization of the output for the following MUL_MAT (exact kernel only):
+    // qmode 0 none, 1 Q8_K, 2 Q8_0 over the flat [n_q][H*D] output rows
+    int qmode;
+    int8_t * qs; float * qd; int16_t * qsum;
+};
+
+constexpr int FAX_GMAX = 8;     // max query heads per KV head in the exact kernel
+
+// launch the CPU-exact f16 kernel (k_fattn_exact.hip); D in {64, 128, 256}
+void launch_fattn_exact(hipStream_t stream, const fa_args & a, int64_t nq3);
+void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int64_t n, float * s);
+
+}  // namespace mi355x

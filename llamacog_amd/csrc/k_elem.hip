@@ -5,18 +5,28 @@
 // Each op follows the CPU backend's arithmetic (ggml/src/ggml-cpu/ops.cpp,
 // binary-ops.cpp, unary-ops.cpp, vec.h) — operation order per element is kept, reductions
 // use wider accumulators where the CPU does (rms_norm sums in ggml_float = double).
-// They are HBM/latency-bound; all use 256-thread blocks with one row per block.
+// They are HBM/latency-bound; rows are split over several 256-thread workgroups when
+// there are few of them (decode).
 #include "ops.h"
+#include "rope.h"
 
 #include <cmath>
 
 namespace mi355x {
 
 struct t4 { int64_t ne[4]; int64_t nb[4]; };
+__device__ __forceinline__ int64_t nrows_all(const t4 & t) { return t.ne[1] * t.ne[2] * t.ne[3]; }
 static t4 mk(const ggml_tensor * t) {
     t4 r;
     for (int i = 0; i < 4; ++i) { r.ne[i] = t->ne[i]; r.nb[i] = (int64_t) t->nb[i]; }
     return r;
+}
+
+// column slices per row: few rows (decode) spread one row over many workgroups, many rows
+// (prefill) keep one workgroup per row
+static unsigned col_blocks(int64_t ne0, int64_t nrows, unsigned thr) {
+    const int64_t want = std::max<int64_t>(1, 1024 / std::max<int64_t>(nrows, 1));
+    return (unsigned) std::min<int64_t>(ceil_div(ne0, thr), want);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -35,13 +45,14 @@ __device__ __forceinline__ float bin_apply(float a, float b) {
 template <int OP>
 __global__ __launch_bounds__(256) void k_binary(const char * __restrict__ a, t4 ta, const char * __restrict__ b, t4 tb,
                                                 char * __restrict__ d, t4 td) {
-    const int64_t r = blockIdx.x;  // row over (i1, i2, i3) of dst
+    const int64_t cb = gridDim.x / nrows_all(td);   // column slices per row
+    const int64_t r = blockIdx.x / cb;              // row over (i1, i2, i3) of dst
     const int64_t i1 = r % td.ne[1], i2 = (r / td.ne[1]) % td.ne[2], i3 = r / (td.ne[1] * td.ne[2]);
     const char * ar = a + i1 * ta.nb[1] + i2 * ta.nb[2] + i3 * ta.nb[3];
     const char * br = b + (i1 % tb.ne[1]) * tb.nb[1] + (i2 % tb.ne[2]) * tb.nb[2] + (i3 % tb.ne[3]) * tb.nb[3];
     char * dr = d + i1 * td.nb[1] + i2 * td.nb[2] + i3 * td.nb[3];
     const int64_t ne0 = td.ne[0], ne10 = tb.ne[0];
-    for (int64_t i0 = threadIdx.x; i0 < ne0; i0 += blockDim.x) {
+    for (int64_t i0 = (blockIdx.x % cb) * blockDim.x + threadIdx.x; i0 < ne0; i0 += cb * blockDim.x) {
         const float x = *(const float *) (ar + i0 * ta.nb[0]);
         const float y = *(const float *) (br + (i0 % ne10) * tb.nb[0]);
         *(float *) (dr + i0 * td.nb[0]) = bin_apply<OP>(x, y);
@@ -54,12 +65,13 @@ void op_binary(exec_ctx & ctx, ggml_tensor * dst) {
     const int64_t nrows = dst->ne[1] * dst->ne[2] * dst->ne[3];
     if (nrows == 0 || dst->ne[0] == 0) return;
     const unsigned thr = dst->ne[0] >= 256 ? 256 : 64;
+    const dim3 grid((unsigned) (col_blocks(dst->ne[0], nrows, thr) * nrows));
     auto A = mk(s0), B = mk(s1), D = mk(dst);
     switch (dst->op) {
-        case GGML_OP_ADD: hipLaunchKernelGGL(k_binary<BIN_ADD>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
-        case GGML_OP_SUB: hipLaunchKernelGGL(k_binary<BIN_SUB>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
-        case GGML_OP_MUL: hipLaunchKernelGGL(k_binary<BIN_MUL>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
-        case GGML_OP_DIV: hipLaunchKernelGGL(k_binary<BIN_DIV>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
+        case GGML_OP_ADD: hipLaunchKernelGGL(k_binary<BIN_ADD>, grid, dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
+        case GGML_OP_SUB: hipLaunchKernelGGL(k_binary<BIN_SUB>, grid, dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
+        case GGML_OP_MUL: hipLaunchKernelGGL(k_binary<BIN_MUL>, grid, dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
+        case GGML_OP_DIV: hipLaunchKernelGGL(k_binary<BIN_DIV>, grid, dim3(thr), 0, ctx.stream, (const char *) s0->data, A, (const char *) s1->data, B, (char *) dst->data, D); break;
         default: GGML_ABORT("mi355x: bad binary op");
     }
 }
@@ -91,12 +103,13 @@ __device__ __forceinline__ float un_apply(float x, float s) {
 
 template <int OP>
 __global__ __launch_bounds__(256) void k_unary(const char * __restrict__ a, t4 ta, char * __restrict__ d, t4 td, float s) {
-    const int64_t r = blockIdx.x;
+    const int64_t cb = gridDim.x / nrows_all(td);
+    const int64_t r = blockIdx.x / cb;
     const int64_t i1 = r % td.ne[1], i2 = (r / td.ne[1]) % td.ne[2], i3 = r / (td.ne[1] * td.ne[2]);
     const char * ar = a + i1 * ta.nb[1] + i2 * ta.nb[2] + i3 * ta.nb[3];
     char * dr = d + i1 * td.nb[1] + i2 * td.nb[2] + i3 * td.nb[3];
     const int64_t nvec = (td.ne[0] / 16) * 16;  // ggml_vec_silu_f32: 16-wide SIMD body, scalar tail
-    for (int64_t i0 = threadIdx.x; i0 < td.ne[0]; i0 += blockDim.x) {
+    for (int64_t i0 = (blockIdx.x % cb) * blockDim.x + threadIdx.x; i0 < td.ne[0]; i0 += cb * blockDim.x) {
         const float x = *(const float *) (ar + i0 * ta.nb[0]);
         float yv;
         if constexpr (OP == UN_SILU) yv = i0 < nvec ? un_apply<OP>(x, s) : x / (1.0f + expf_cr(-x));
@@ -110,7 +123,7 @@ static void launch_unary(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * 
     const int64_t nrows = dst->ne[1] * dst->ne[2] * dst->ne[3];
     if (nrows == 0 || dst->ne[0] == 0) return;
     const unsigned thr = dst->ne[0] >= 256 ? 256 : 64;
-    hipLaunchKernelGGL(k_unary<OP>, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) src->data, mk(src),
+    hipLaunchKernelGGL(k_unary<OP>, dim3((unsigned) (col_blocks(dst->ne[0], nrows, thr) * nrows)), dim3(thr), 0, ctx.stream, (const char *) src->data, mk(src),
                        (char *) dst->data, mk(dst), s);
 }
 
@@ -152,7 +165,9 @@ template <> __device__ __forceinline__ uint16_t cvt<uint16_t, uint16_t>(uint16_t
 template <> __device__ __forceinline__ int32_t  cvt<int32_t, int32_t>(int32_t v) { return v; }
 
 template <typename TS, typename TD>
-__global__ __launch_bounds__(256) void k_cpy(const char * __restrict__ s, t4 ts, char * __restrict__ d, t4 td, int64_t n) {
+__global__ __launch_bounds__(256) void k_cpy(const char * __restrict__ s, t4 ts, char * __restrict__ d, t4 td, int64_t n,
+                                             char * const * dslot) {
+    if (dslot) d = *dslot;
     for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
         int64_t r = i;
         const int64_t s0 = r % ts.ne[0]; r /= ts.ne[0];
@@ -168,14 +183,18 @@ __global__ __launch_bounds__(256) void k_cpy(const char * __restrict__ s, t4 ts,
 }
 
 // contiguous f32 -> f16 fast path (KV store of K/V rows, mask cast)
-__global__ __launch_bounds__(256) void k_cpy_f32_f16_contig(const float * __restrict__ s, uint16_t * __restrict__ d, int64_t n) {
+__global__ __launch_bounds__(256) void k_cpy_f32_f16_contig(const float * __restrict__ s, uint16_t * __restrict__ d, int64_t n,
+                                                            uint16_t * const * dslot) {
+    if (dslot) d = *dslot;
     for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
         d[i] = f2h(s[i]);
     }
 }
 
 // f32 rows -> q8_0 blocks (x86 quantize_row_q8_0 semantics, see k_mmv.hip); one wave per 8 blocks
-__global__ __launch_bounds__(64) void k_cpy_f32_q8_0(const char * __restrict__ s, t4 ts, char * __restrict__ d, t4 td) {
+__global__ __launch_bounds__(64) void k_cpy_f32_q8_0(const char * __restrict__ s, t4 ts, char * __restrict__ d, t4 td,
+                                                     char * const * dslot) {
+    if (dslot) d = *dslot;
     const int lane = threadIdx.x;
     const int64_t r = blockIdx.y;  // source row
     const int64_t i1 = r % ts.ne[1], i2 = (r / ts.ne[1]) % ts.ne[2], i3 = r / (ts.ne[1] * ts.ne[2]);
@@ -207,23 +226,25 @@ __global__ __launch_bounds__(64) void k_cpy_f32_q8_0(const char * __restrict__ s
     if ((lane & 7) == 0) blk->d = f2h(dd);
 }
 
-void op_cpy(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst) {
+void op_cpy(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst, const ggml_tensor * node) {
     const int64_t n = ggml_nelements(src);
     if (n == 0) return;
+    char * const * dslot = node ? (char * const *) ctx.dyn_slot(node) : nullptr;
     const t4 S = mk(src), D = mk(dst);
     const unsigned grid = (unsigned) std::min<int64_t>(ceil_div(n, 256), 8192);
     if (src->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_F16 && ggml_is_contiguous(src) && ggml_is_contiguous(dst)) {
-        hipLaunchKernelGGL(k_cpy_f32_f16_contig, dim3(grid), dim3(256), 0, ctx.stream, (const float *) src->data, (uint16_t *) dst->data, n);
+        hipLaunchKernelGGL(k_cpy_f32_f16_contig, dim3(grid), dim3(256), 0, ctx.stream, (const float *) src->data, (uint16_t *) dst->data, n,
+                           (uint16_t * const *) dslot);
         return;
     }
     if (src->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_Q8_0) {
         const int64_t nrows = src->ne[1] * src->ne[2] * src->ne[3];
         dim3 g((unsigned) ceil_div(src->ne[0], 256), (unsigned) nrows);
-        hipLaunchKernelGGL(k_cpy_f32_q8_0, g, dim3(64), 0, ctx.stream, (const char *) src->data, S, (char *) dst->data, D);
+        hipLaunchKernelGGL(k_cpy_f32_q8_0, g, dim3(64), 0, ctx.stream, (const char *) src->data, S, (char *) dst->data, D, dslot);
         return;
     }
 #define CPY_CASE(TS_, TD_, ts, td) \
-    if (src->type == TS_ && dst->type == TD_) { hipLaunchKernelGGL((k_cpy<ts, td>), dim3(grid), dim3(256), 0, ctx.stream, (const char *) src->data, S, (char *) dst->data, D, n); return; }
+    if (src->type == TS_ && dst->type == TD_) { hipLaunchKernelGGL((k_cpy<ts, td>), dim3(grid), dim3(256), 0, ctx.stream, (const char *) src->data, S, (char *) dst->data, D, n, dslot); return; }
     CPY_CASE(GGML_TYPE_F32, GGML_TYPE_F32, float, float)
     CPY_CASE(GGML_TYPE_F32, GGML_TYPE_F16, float, uint16_t)
     CPY_CASE(GGML_TYPE_F16, GGML_TYPE_F32, uint16_t, float)
@@ -406,65 +427,56 @@ void op_norm(exec_ctx & ctx, ggml_tensor * dst) {
 // RoPE (ops.cpp:5080-5362).  theta for pair i is built exactly like ggml_rope_cache_init:
 // theta_0 = p, theta_{i+1} = theta_i * theta_scale (fp32, sequential), then rope_yarn.
 // ------------------------------------------------------------------------------------------
-struct rope_params {
-    int n_dims; int mode; float freq_scale, ext_factor, attn_factor; float corr0, corr1; float theta_scale;
-    int has_ff;
+// one ROPE node: x -> y, optionally also stored as f16 into a KV-cache view (the CPY that
+// follows K's rope, fused; its destination comes from the dynamic-pointer table)
+struct rope_job {
+    const char * x; t4 tx; char * y; t4 ty;
+    uint16_t * const * cache;   // nullable: f16 copy of y (y contiguous, flat element order)
+    int64_t nrows;
 };
 
-__device__ __forceinline__ void rope_yarn_dev(float theta_extrap, float freq_scale, float corr0, float corr1, int64_t i0,
-                                              float ext_factor, float mscale, float & c, float & s) {
-    const float theta_interp = freq_scale * theta_extrap;
-    float theta = theta_interp;
-    if (ext_factor != 0.0f) {
-        const float y = (i0 / 2 - corr0) / fmaxf(0.001f, corr1 - corr0);
-        const float ramp_mix = (1.0f - fminf(1.0f, fmaxf(0.0f, y))) * ext_factor;
-        theta = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
-        mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
-    }
-    // libm cosf/sinf of the CPU backend: take them in double and round once
-    c = __fmul_rn((float) cos((double) theta), mscale);
-    s = __fmul_rn((float) sin((double) theta), mscale);
-}
+struct rope_jobs { rope_job j[2]; int njobs; };
 
-__global__ __launch_bounds__(256) void k_rope(const char * __restrict__ x, t4 tx, char * __restrict__ y, t4 ty,
-                                              const int32_t * __restrict__ pos, const float * __restrict__ ff, rope_params rp) {
-    const int64_t r = blockIdx.x;  // row over (i1 head, i2 token, i3)
+__global__ __launch_bounds__(256) void k_rope(const rope_jobs J, const int32_t * __restrict__ pos,
+                                              const float * __restrict__ ff, rope_params rp) {
+    int64_t r = blockIdx.x;  // row over (i1 head, i2 token, i3) of job 0, then job 1
+    const int jb = (J.njobs > 1 && r >= J.j[0].nrows) ? 1 : 0;
+    if (jb) r -= J.j[0].nrows;
+    const rope_job & jo = J.j[jb];
+    const t4 & tx = jo.tx;
+    const t4 & ty = jo.ty;
     const int64_t i1 = r % tx.ne[1], i2 = (r / tx.ne[1]) % tx.ne[2], i3 = r / (tx.ne[1] * tx.ne[2]);
-    const char * xr = x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3];
-    char * yr = y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3];
+    const char * xr = jo.x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3];
+    char * yr = jo.y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3];
+    uint16_t * cr = jo.cache ? *jo.cache + (yr - jo.y) / 4 : nullptr;
     const int64_t ne0 = tx.ne[0];
     const float p = (float) pos[i2];
     const bool neox = rp.mode & 2;
     for (int64_t ip = threadIdx.x; ip < ne0 / 2; ip += blockDim.x) {
         const int64_t i0 = 2 * ip;
+        int64_t a0, a1;
+        float o0, o1;
         if (i0 < rp.n_dims) {
-            float theta = p;
-            for (int64_t k = 0; k < ip; ++k) theta *= rp.theta_scale;
-            const float f = rp.has_ff ? ff[ip] : 1.0f;
             float c, s;
-            rope_yarn_dev(theta / f, rp.freq_scale, rp.corr0, rp.corr1, i0, rp.ext_factor, rp.attn_factor, c, s);
-            int64_t a0, a1;
+            rope_cs(rp, p, ip, ff, c, s);
             if (neox) { a0 = ip; a1 = ip + rp.n_dims / 2; }
             else      { a0 = i0; a1 = i0 + 1; }
             const float x0 = *(const float *) (xr + a0 * tx.nb[0]);
             const float x1 = *(const float *) (xr + a1 * tx.nb[0]);
-            // the reference's x86-64-v4 build contracts these as below (bit-exact vs
-            // tests/golden/rope.npz)
-            *(float *) (yr + a0 * ty.nb[0]) = fmaf(x0, c, -__fmul_rn(x1, s));
-            *(float *) (yr + a1 * ty.nb[0]) = fmaf(x0, s, __fmul_rn(x1, c));
+            rope_rotate(x0, x1, c, s, o0, o1);
         } else {
-            *(float *) (yr + i0 * ty.nb[0])       = *(const float *) (xr + i0 * tx.nb[0]);
-            *(float *) (yr + (i0 + 1) * ty.nb[0]) = *(const float *) (xr + (i0 + 1) * tx.nb[0]);
+            a0 = i0; a1 = i0 + 1;
+            o0 = *(const float *) (xr + i0 * tx.nb[0]);
+            o1 = *(const float *) (xr + (i0 + 1) * tx.nb[0]);
         }
+        *(float *) (yr + a0 * ty.nb[0]) = o0;
+        *(float *) (yr + a1 * ty.nb[0]) = o1;
+        if (cr) { cr[a0] = f2h(o0); cr[a1] = f2h(o1); }
     }
 }
 
-void op_rope(exec_ctx & ctx, ggml_tensor * dst) {
-    const ggml_tensor * src = dst->src[0];
-    const ggml_tensor * pos = dst->src[1];
-    const ggml_tensor * ff  = dst->src[2];
+bool rope_params_of(const ggml_tensor * dst, rope_params & rp) {
     const int32_t * op = dst->op_params;
-    rope_params rp;
     rp.n_dims = op[1];
     rp.mode = op[2];
     const int n_ctx_orig = op[4];
@@ -479,12 +491,43 @@ void op_rope(exec_ctx & ctx, ggml_tensor * dst) {
     float corr[2];
     ggml_rope_yarn_corr_dims(rp.n_dims, n_ctx_orig, freq_base, beta_fast, beta_slow, corr);
     rp.corr0 = corr[0]; rp.corr1 = corr[1];
-    rp.has_ff = ff != nullptr;
-    const int64_t nrows = src->ne[1] * src->ne[2] * src->ne[3];
-    if (nrows == 0) return;
-    const unsigned thr = src->ne[0] / 2 >= 256 ? 256 : 64;
-    hipLaunchKernelGGL(k_rope, dim3((unsigned) nrows), dim3(thr), 0, ctx.stream, (const char *) src->data, mk(src),
-                       (char *) dst->data, mk(dst), (const int32_t *) pos->data, ff ? (const float *) ff->data : nullptr, rp);
+    rp.has_ff = dst->src[2] != nullptr;
+    return true;
+}
+
+static rope_job make_rope_job(const ggml_tensor * dst, uint16_t * const * cache) {
+    const ggml_tensor * src = dst->src[0];
+    rope_job j;
+    j.x = (const char *) src->data; j.tx = mk(src);
+    j.y = (char *) dst->data; j.ty = mk(dst);
+    j.cache = cache;
+    j.nrows = src->ne[1] * src->ne[2] * src->ne[3];
+    return j;
+}
+
+// one or two ROPE nodes with identical parameters / positions in one launch;
+// cache[i] = dynamic-table slot of a fused f16 KV-cache store for node i (nullable)
+void op_rope_multi(exec_ctx & ctx, ggml_tensor * const * nodes, int n, void * const * const * cache) {
+    rope_params rp;
+    rope_params_of(nodes[0], rp);
+    rope_jobs J;
+    J.njobs = n;
+    int64_t rows = 0;
+    for (int i = 0; i < n; ++i) {
+        J.j[i] = make_rope_job(nodes[i], cache ? (uint16_t * const *) cache[i] : nullptr);
+        rows += J.j[i].nrows;
+    }
+    if (rows == 0) return;
+    const ggml_tensor * pos = nodes[0]->src[1];
+    const ggml_tensor * ff  = nodes[0]->src[2];
+    const unsigned thr = nodes[0]->src[0]->ne[0] / 2 >= 256 ? 256 : 64;
+    hipLaunchKernelGGL(k_rope, dim3((unsigned) rows), dim3(thr), 0, ctx.stream, J, (const int32_t *) pos->data,
+                       ff ? (const float *) ff->data : nullptr, rp);
+}
+
+void op_rope(exec_ctx & ctx, ggml_tensor * dst) {
+    ggml_tensor * nodes[1] = {dst};
+    op_rope_multi(ctx, nodes, 1, nullptr);
 }
 
 // ------------------------------------------------------------------------------------------

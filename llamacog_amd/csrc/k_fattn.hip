@@ -13,25 +13,11 @@
 // broadcast from LDS), does the online-softmax update with wave reductions, then streams
 // the 64 V rows with lanes owning D/64 output dims each.  Long caches are split over
 // chunks (split-K) so decode fills the chip; a combine kernel merges the chunk partials.
-#include "ops.h"
+#include "fattn.h"
 
 #include <cmath>
 
 namespace mi355x {
-
-struct fa_args {
-    const char * q; int64_t nbq1, nbq2, nbq3;
-    const char * k; int64_t nbk1, nbk2, nbk3;
-    const char * v; int64_t nbv1, nbv2, nbv3;
-    const char * mask; int64_t nbm1; int64_t mask_ne1;
-    int k_type, v_type;
-    int64_t D, n_kv, n_q, H, Hkv, chunk;
-    float scale, softcap, max_bias, m0, m1; uint32_t n_head_log2;
-    float * part;      // [nchunks][n_q][H][D+2]  (M, S, O[D])
-    float * dst;       // final output when nchunks == 1
-    int64_t nb1_dst, nb2_dst;
-    int nchunks;
-};
 
 template <int EPL>  // elements of D per lane (D = 64*EPL)
 __global__ __launch_bounds__(256) void k_fattn_vec(const fa_args a) {
@@ -223,233 +209,6 @@ __global__ __launch_bounds__(64) void k_fattn_combine(const fa_args a) {
     for (int e = 0; e < EPL; ++e) drow[lane * EPL + e] = ot[e] * inv;
 }
 
-// ------------------------------------------------------------------------------------------
-// CPU-exact flash attention for an f16 KV cache (the default; GGML_MI355X_FA_FAST=1 selects
-// the split-K f32 kernel above).  Reproduces ops.cpp:7015-7232 on x86-64-v4 (the AVX-512
-// CPU backend the reference selects on the MI355X host):
-//   * Q rounded to f16; K·Q with ggml_vec_dot_f16's AVX-512 order (vec.cpp:191-231): 16
-//     lanes x 4 accumulators of f32 FMAs, REDUCE (x0+=x2, x1+=x3, x0+=x1) then the
-//     _mm512_reduce_add_ps tree (8/4/2/1);
-//   * the online softmax walks the cache in order and accumulates VKQ in f16 with the
-//     vec_mad_f16 / vec_scale_f16 roundings (vec.h:262-290, 410-440): y = f16(fma(v,vs,y)),
-//     y = f16(y*ms); S = S*ms + vs; expf taken in double and rounded (glibc's expf is
-//     correctly rounded in practice).
-// MI355X structure: one workgroup per (q row, KV head) covers the G = H/Hkv query heads of
-// that KV head (GQA) so each K/V row is read once for all of them.  Chunks of CH cache
-// positions run three phases: (1) all scores in parallel (one position per thread, the K
-// row held in VGPRs), (2) per-head prefix max + the (ms, vs) coefficients in parallel,
-// (3) the f16 recurrence, sequential over positions, parallel over G*D elements.
-// ------------------------------------------------------------------------------------------
-constexpr int FAX_CH = 512;     // cache positions per chunk
-constexpr int FAX_GMAX = 8;     // max query heads per KV head
-
-// round through f16 AFTER the f32 result exists: the empty asm keeps hipcc from fusing the
-// preceding fma/mul into v_fma_mixlo_f16, which rounds the exact product straight to f16
-// (one rounding) where the CPU rounds to f32 and then to f16 (two roundings)
-__device__ __forceinline__ float f16r(float x) {
-    asm volatile("" : "+v"(x));
-    return __half2float(__float2half_rn(x));
-}
-
-// ggml_vec_dot_f16 (AVX-512) of a K row (f16) with q (f16-rounded floats in LDS)
-template <int D>
-__device__ __forceinline__ float dot_f16_avx512(const uint32_t (&k)[D / 2], const float * q) {
-    float w[16];
-#pragma unroll
-    for (int l = 0; l < 16; ++l) {
-        float a[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int s = 16 * j + l;
-            float acc = 0.0f;
-#pragma unroll
-            for (int i = 0; i < D / 64; ++i) {
-                const int e = 64 * i + s;
-                const float kv = h2f((k[e >> 1] >> (16 * (e & 1))) & 0xffff);
-                acc = i == 0 ? __fmul_rn(kv, q[e]) : fmaf(kv, q[e], acc);
-            }
-            a[j] = acc;
-        }
-        w[l] = __fadd_rn(__fadd_rn(a[0], a[2]), __fadd_rn(a[1], a[3]));
-    }
-    return reduce16_avx512(w);
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
-    const int tid = threadIdx.x;
-    const int64_t iq1 = blockIdx.x;
-    const int64_t hk = blockIdx.y % a.Hkv;
-    const int64_t iq3 = blockIdx.y / a.Hkv;
-    const int G = (int) (a.H / a.Hkv);
-
-    __shared__ float qf[FAX_GMAX][D];
-    __shared__ float sc[FAX_GMAX][FAX_CH];   // scores -> vs coefficient
-    __shared__ float cm[FAX_GMAX][FAX_CH];   // ms coefficient (0 marks "skip", <0 unused)
-    __shared__ float red[FAX_GMAX][4];
-    __shared__ float mcarry[FAX_GMAX];
-
-    for (int i = tid; i < G * D; i += 256) {
-        const int g = i / D, d = i % D;
-        const float * qrow = (const float *) (a.q + iq1 * a.nbq1 + (hk * G + g) * a.nbq2 + iq3 * a.nbq3);
-        qf[g][d] = f16r(qrow[d]);
-    }
-    if (tid < FAX_GMAX) mcarry[tid] = -INFINITY;
-
-    // phase-3 state: each thread owns up to 4 (g, d) elements
-    constexpr int EMAX = FAX_GMAX * D / 256 > 0 ? FAX_GMAX * D / 256 : 1;
-    float y[EMAX], S[EMAX];
-#pragma unroll
-    for (int e = 0; e < EMAX; ++e) { y[e] = 0.0f; S[e] = 0.0f; }
-    const int nel = G * D;
-
-    const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
-    const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
-    const char * mrow = a.mask ? a.mask + (iq1 % a.mask_ne1) * a.nbm1 : nullptr;
-    __syncthreads();
-
-    for (int64_t c0 = 0; c0 < a.n_kv; c0 += FAX_CH) {
-        const int nch = (int) min((int64_t) FAX_CH, a.n_kv - c0);
-        // ---- phase 1: scores ---------------------------------------------------------------
-        for (int j = tid; j < nch; j += 256) {
-            const int64_t pos = c0 + j;
-            const float mv = mrow ? h2f(*(const uint16_t *) (mrow + 2 * pos)) : 0.0f;
-            if (mv == -INFINITY) {
-                for (int g = 0; g < G; ++g) sc[g][j] = -INFINITY;
-                continue;
-            }
-            uint32_t kr[D / 2];
-            const char * krow = kbase + pos * a.nbk1;
-#pragma unroll
-            for (int i = 0; i < D / 8; ++i) {
-                const uint4 v = ld16(krow + 16 * i);
-                kr[4 * i] = v.x; kr[4 * i + 1] = v.y; kr[4 * i + 2] = v.z; kr[4 * i + 3] = v.w;
-            }
-            for (int g = 0; g < G; ++g) {
-                float s = dot_f16_avx512<D>(kr, qf[g]);
-                s = __fmul_rn(s, a.scale);
-                if (a.softcap != 0.0f) s = __fmul_rn(a.softcap, tanhf(s));
-                // ALiBi slope of head h = hk*G + g (ops.cpp:7109)
-                const uint32_t hh = (uint32_t) (hk * G + g);
-                const float slope = a.max_bias > 0.0f
-                    ? (float) (hh < a.n_head_log2 ? pow((double) a.m0, (double) (hh + 1))
-                                                  : pow((double) a.m1, (double) (2 * (hh - a.n_head_log2) + 1))) : 1.0f;
-                s = __fadd_rn(s, __fmul_rn(slope, mv));
-                sc[g][j] = s;
-            }
-        }
-        __syncthreads();
-        // ---- phase 2: prefix max per head and the (ms, vs) coefficients --------------------
-        constexpr int PER = FAX_CH / 256;
-        for (int g = 0; g < G; ++g) {
-            float lm = -INFINITY;
-#pragma unroll
-            for (int p = 0; p < PER; ++p) {
-                const int j = tid * PER + p;
-                if (j < nch) lm = fmaxf(lm, sc[g][j]);
-            }
-            // inclusive scan of max across the 256 threads
-            const int lane = tid & 63, wave = tid >> 6;
-            float sm = lm;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const float t = __shfl_up(sm, o, WAVE);
-                if (lane >= o) sm = fmaxf(sm, t);
-            }
-            if (lane == 63) red[g][wave] = sm;
-            __syncthreads();
-            float prev = mcarry[g];
-            for (int w = 0; w < wave; ++w) prev = fmaxf(prev, red[g][w]);
-            const float ex = __shfl_up(sm, 1, WAVE);
-            if (lane > 0) prev = fmaxf(prev, ex);
-            // sequential within the thread's positions
-            float M = prev;
-#pragma unroll
-            for (int p = 0; p < PER; ++p) {
-                const int j = tid * PER + p;
-                if (j >= nch) break;
-                const float s = sc[g][j];
-                if (s == -INFINITY) { cm[g][j] = -1.0f; sc[g][j] = 0.0f; continue; }
-                if (s > M) {
-                    cm[g][j] = M == -INFINITY ? 0.0f : expf_cr(M - s);   // ms, applied before the add
-                    sc[g][j] = 1.0f;                                       // vs
-                    M = s;
-                } else {
-                    cm[g][j] = 1.0f;
-                    sc[g][j] = expf_cr(s - M);
-                }
-            }
-            __syncthreads();
-            if (tid == 255) mcarry[g] = fmaxf(mcarry[g], fmaxf(red[g][0], fmaxf(red[g][1], fmaxf(red[g][2], red[g][3]))));
-            __syncthreads();
-        }
-        // ---- phase 3: sequential f16 recurrence --------------------------------------------
-        // the element loop is innermost so a thread's EMAX independent chains interleave
-        if (tid < nel) {
-            int ge[EMAX];
-            const char * vp[EMAX];
-#pragma unroll
-            for (int e = 0; e < EMAX; ++e) {
-                const int idx = min(tid + 256 * e, nel - 1);
-                ge[e] = idx / D;
-                vp[e] = vbase + c0 * a.nbv1 + 2 * (idx % D);
-            }
-            constexpr int U = 8;
-            for (int j = 0; j < nch; j += U) {
-                uint16_t vv[U][EMAX];
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int e = 0; e < EMAX; ++e)
-                        vv[u][e] = (j + u < nch) ? *(const uint16_t *) (vp[e] + (j + u) * a.nbv1) : 0;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (j + u >= nch) break;
-#pragma unroll
-                    for (int e = 0; e < EMAX; ++e) {
-                        const float ms = cm[ge[e]][j + u];
-                        if (ms < 0.0f) continue;
-                        const float vs = sc[ge[e]][j + u];
-                        float yy = y[e];
-                        if (ms != 1.0f) yy = f16r(__fmul_rn(yy, ms));
-                        y[e] = f16r(fmaf(h2f(vv[u][e]), vs, yy));
-                        S[e] = __fadd_rn(__fmul_rn(S[e], ms), vs);   // not contracted on the CPU
-                    }
-                }
-            }
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int e = 0; e < EMAX; ++e) {
-        const int idx = tid + 256 * e;
-        if (idx >= nel) break;
-        const int g = idx / D, d = idx % D;
-        const int64_t h = hk * G + g;
-        float * drow = (float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H + h * a.nb1_dst + iq3 * a.nb2_dst);
-        drow[d] = __fmul_rn(y[e], 1.0f / S[e]);
-    }
-}
-
-// test hook: the K·Q scores exactly as phase 1 of k_fattn_exact computes them
-// (q [D] f32 is f16-rounded first), one thread per cache row; D = 128
-__global__ void k_fattn_scores_d128(const float * q, const uint16_t * k, int64_t n, float * s) {
-    __shared__ float qf[128];
-    for (int i = threadIdx.x; i < 128; i += blockDim.x) qf[i] = f16r(q[i]);
-    __syncthreads();
-    const int64_t j = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    uint32_t kr[64];
-    for (int i = 0; i < 16; ++i) {
-        const uint4 v = ld16(k + j * 128 + 8 * i);
-        kr[4 * i] = v.x; kr[4 * i + 1] = v.y; kr[4 * i + 2] = v.z; kr[4 * i + 3] = v.w;
-    }
-    s[j] = dot_f16_avx512<128>(kr, qf);
-}
-
-void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int64_t n, float * s) {
-    hipLaunchKernelGGL(k_fattn_scores_d128, dim3((unsigned) ceil_div(n, 64)), dim3(64), 0, st, q, k, n, s);
-}
 
 bool fattn_supported(const ggml_tensor * op) {
     const ggml_tensor * q = op->src[0];
@@ -472,7 +231,9 @@ bool fattn_supported(const ggml_tensor * op) {
     return true;
 }
 
-void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst) {
+bool mmv_q_supported_type(ggml_type t);
+
+void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     const ggml_tensor * q = dst->src[0];
     const ggml_tensor * k = dst->src[1];
     const ggml_tensor * v = dst->src[2];
@@ -507,6 +268,8 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst) {
     nchunks = ceil_div(a.n_kv, a.chunk);
     a.nchunks = (int) nchunks;
     a.part = nullptr;
+    a.qmode = 0;
+    a.qs = nullptr; a.qd = nullptr; a.qsum = nullptr;
     if (nchunks > 1) a.part = (float *) ctx.scratch(1, sizeof(float) * nchunks * rows * (a.D + 2));
 
     hipEvent_t ev = nullptr;
@@ -514,13 +277,21 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst) {
     if (ctx.timing) ctx.time_begin(TK_FATTN, bytes, ev);
     static const bool fast = getenv("GGML_MI355X_FA_FAST") != nullptr && atoi(getenv("GGML_MI355X_FA_FAST")) != 0;
     if (!fast && a.k_type == GGML_TYPE_F16 && a.H / a.Hkv <= FAX_GMAX) {
-        dim3 gx((unsigned) a.n_q, (unsigned) (a.Hkv * nq3));
-        switch (a.D) {
-            case 64:  hipLaunchKernelGGL(k_fattn_exact<64>,  gx, dim3(256), 0, ctx.stream, a); break;
-            case 128: hipLaunchKernelGGL(k_fattn_exact<128>, gx, dim3(256), 0, ctx.stream, a); break;
-            case 256: hipLaunchKernelGGL(k_fattn_exact<256>, gx, dim3(256), 0, ctx.stream, a); break;
-            default: GGML_ABORT("mi355x: FA head size");
+        // fused quantization of the output for the next MUL_MAT (decode: one row)
+        q8_act act;
+        if (mm && a.n_q == 1 && nq3 == 1 && mmv_q_supported_type(mm->src[0]->type) &&
+            mm->src[1]->ne[0] == a.H * a.D && ggml_nrows(mm->src[1]) == 1 && ggml_is_contiguous(dst)) {
+            const ggml_type wt = mm->src[0]->type;
+            const bool kq = wt == GGML_TYPE_Q4_K || wt == GGML_TYPE_Q5_K || wt == GGML_TYPE_Q6_K;
+            const int64_t G = a.H / a.Hkv;
+            if ((G * a.D) % (kq ? 256 : 32) == 0 && (a.H * a.D) % (kq ? 256 : 32) == 0) {
+                carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(a.H * a.D, 1, kq)), a.H * a.D, 1, kq);
+                a.qmode = kq ? 1 : 2;
+                a.qs = act.qs; a.qd = act.d; a.qsum = act.s;
+            }
         }
+        launch_fattn_exact(ctx.stream, a, nq3);
+        if (a.qmode) ctx.qcache_put(mm->src[1], a.qmode == 1, act);
         if (ctx.timing) ctx.time_end(TK_FATTN, bytes, ev);
         return;
     }

@@ -1,0 +1,200 @@
+// k_fused.hip — fused producers of the decode graph.  Each replaces a chain of ggml nodes
+// with ONE kernel that writes every node's output exactly as the unfused kernels would
+// (same per-element arithmetic, same reduction), plus the quantized activation of the
+// MUL_MAT that consumes the chain (into exec_ctx's quantization cache), so the MUL_MAT does
+// not launch its own quantizer:
+//
+//   [ADD] -> RMS_NORM -> [MUL w] -> (MUL_MAT)     k_norm_fused   (src/llama-graph.cpp:464-497
+//                                                 build_norm; residual ADDs :llama.cpp build)
+//   MUL (silu(gate) * up) -> (MUL_MAT down)       k_mul_quant    (build_ffn LLM_FFN_PAR)
+//
+// Arithmetic: ADD/MUL are single f32 ops; RMS_NORM sums float(x*x) in double
+// (ops.cpp:3270-3316), scale = 1/sqrtf(float(sum/ne0)+eps), y = x*scale; quantizers are
+// quant_act.h's (bit-exact with the CPU).  All run with rows in registers: one 256-thread
+// workgroup per row, each thread owning NV float4 slices (ne0 = 1024*NV).
+#include "ops.h"
+#include "quant_act.h"
+
+namespace mi355x {
+
+struct norm_fused_args {
+    const float * a; const float * b;   // x = a (+ b)
+    float * xsum;                       // ADD output (nullable)
+    float * y;                          // RMS_NORM output
+    const float * w; float * yw;        // MUL weight / output (nullable)
+    int64_t ne0;
+    float eps;
+    int qmode;                          // 0 none, 1 Q8_K, 2 Q8_0 (of yw if w else y)
+    int8_t * qs; float * qd; int16_t * qsum;
+};
+
+template <int NV>
+__global__ __launch_bounds__(256) void k_norm_fused(const norm_fused_args p) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t row = blockIdx.x;
+    const int64_t ro = row * p.ne0;
+    float4 v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int64_t e = 4 * (tid + 256 * k);
+        v[k] = *(const float4 *) (p.a + ro + e);
+        if (p.b) {
+            const float4 bb = *(const float4 *) (p.b + ro + e);
+            v[k].x = __fadd_rn(v[k].x, bb.x); v[k].y = __fadd_rn(v[k].y, bb.y);
+            v[k].z = __fadd_rn(v[k].z, bb.z); v[k].w = __fadd_rn(v[k].w, bb.w);
+        }
+    }
+    if (p.xsum) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) *(float4 *) (p.xsum + ro + 4 * (tid + 256 * k)) = v[k];
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        sum += (double) __fmul_rn(v[k].x, v[k].x);
+        sum += (double) __fmul_rn(v[k].y, v[k].y);
+        sum += (double) __fmul_rn(v[k].z, v[k].z);
+        sum += (double) __fmul_rn(v[k].w, v[k].w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
+    __shared__ double part[4];
+    if (lane == 0) part[wave] = sum;
+    __syncthreads();
+    sum = part[0] + part[1] + part[2] + part[3];
+    const float mean = (float) (sum / (double) p.ne0);
+    const float scale = 1.0f / sqrtf(mean + p.eps);
+
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int64_t e = 4 * (tid + 256 * k);
+        float4 y;
+        y.x = __fmul_rn(v[k].x, scale); y.y = __fmul_rn(v[k].y, scale);
+        y.z = __fmul_rn(v[k].z, scale); y.w = __fmul_rn(v[k].w, scale);
+        *(float4 *) (p.y + ro + e) = y;
+        if (p.w) {
+            const float4 ww = *(const float4 *) (p.w + e);
+            y.x = __fmul_rn(y.x, ww.x); y.y = __fmul_rn(y.y, ww.y);
+            y.z = __fmul_rn(y.z, ww.z); y.w = __fmul_rn(y.w, ww.w);
+            *(float4 *) (p.yw + ro + e) = y;
+        }
+        const float q[4] = {y.x, y.y, y.z, y.w};
+        // the wave's 256 elements of slice k are one Q8_K block / eight Q8_0 blocks
+        const int64_t c0 = 1024 * k + 256 * wave;
+        if (p.qmode == 1) {
+            q8K_wave(q, lane, p.qs + ro + c0, p.qsum + row * (p.ne0 / 16) + c0 / 16, p.qd + row * (p.ne0 / 256) + c0 / 256);
+        } else if (p.qmode == 2) {
+            q8_0_wave(q, lane, true, p.qs + ro + c0, p.qd + row * (p.ne0 / 32) + c0 / 32, p.qsum + row * (p.ne0 / 32) + c0 / 32);
+        }
+    }
+}
+
+// dst = a*b (same shape, contiguous) and its quantization; one wave per 256 elements
+template <int QMODE>
+__global__ __launch_bounds__(64) void k_mul_quant(const float * __restrict__ a, const float * __restrict__ b,
+                                                  float * __restrict__ dst, int64_t K,
+                                                  int8_t * __restrict__ qs, float * __restrict__ qd,
+                                                  int16_t * __restrict__ qsum) {
+    const int lane = threadIdx.x;
+    const int64_t row = blockIdx.y;
+    const int64_t c0 = (int64_t) blockIdx.x * 256;
+    const int64_t e0 = c0 + 4 * lane;
+    const bool valid = e0 < K;
+    float q[4] = {0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+        const float4 x = *(const float4 *) (a + row * K + e0);
+        const float4 y = *(const float4 *) (b + row * K + e0);
+        float4 r;
+        r.x = __fmul_rn(x.x, y.x); r.y = __fmul_rn(x.y, y.y); r.z = __fmul_rn(x.z, y.z); r.w = __fmul_rn(x.w, y.w);
+        *(float4 *) (dst + row * K + e0) = r;
+        q[0] = r.x; q[1] = r.y; q[2] = r.z; q[3] = r.w;
+    }
+    if constexpr (QMODE == 1) {
+        q8K_wave(q, lane, qs + row * K + c0, qsum + row * (K / 16) + c0 / 16, qd + row * (K / 256) + c0 / 256);
+    } else {
+        q8_0_wave(q, lane, valid, qs + row * K + c0, qd + row * (K / 32) + c0 / 32, qsum + row * (K / 32) + c0 / 32);
+    }
+}
+
+// ---- host side -------------------------------------------------------------------------------
+static bool f32_contig(const ggml_tensor * t) { return t && t->type == GGML_TYPE_F32 && ggml_is_contiguous(t); }
+
+bool mmv_q_supported_type(ggml_type t);
+
+// vec_dot_type quantization wanted by a MUL_MAT consumer of `x` (0 = none / not fusable)
+static int consumer_qmode(const ggml_tensor * mm, const ggml_tensor * x) {
+    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != x) return 0;
+    const ggml_type t = mm->src[0]->type;
+    if (!mmv_q_supported_type(t)) return 0;
+    if (mm->src[1]->ne[1] * mm->src[1]->ne[2] * mm->src[1]->ne[3] > 8) return 0;   // mat-vec path only
+    const bool kq = t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K;
+    if (x->ne[0] % (kq ? 256 : 32) != 0) return 0;
+    return kq ? 1 : 2;
+}
+
+bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm) {
+    const int64_t ne0 = norm->ne[0];
+    if (ne0 % 1024 != 0 || ne0 > 8192) return false;
+    if (!f32_contig(norm) || !f32_contig(norm->src[0])) return false;
+    if (add && (!f32_contig(add->src[0]) || !f32_contig(add->src[1]) || !ggml_are_same_shape(add->src[0], add->src[1]) ||
+                !ggml_are_same_shape(add, norm) || norm->src[0] != add)) return false;
+    if (mul && (!f32_contig(mul) || !f32_contig(mul->src[1]) || ggml_nelements(mul->src[1]) != ne0)) return false;
+    const ggml_tensor * out = mul ? mul : norm;
+    const int qmode = consumer_qmode(mm, out);
+    const int64_t nrows = ggml_nrows(norm);
+
+    norm_fused_args p;
+    p.a = add ? (const float *) add->src[0]->data : (const float *) norm->src[0]->data;
+    p.b = add ? (const float *) add->src[1]->data : nullptr;
+    p.xsum = add ? (float *) add->data : nullptr;
+    p.y = (float *) norm->data;
+    p.w = mul ? (const float *) mul->src[1]->data : nullptr;
+    p.yw = mul ? (float *) mul->data : nullptr;
+    p.ne0 = ne0;
+    memcpy(&p.eps, norm->op_params, sizeof(float));
+    p.qmode = qmode;
+    q8_act act;
+    if (qmode) {
+        const bool kq = qmode == 1;
+        void * base = ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(ne0, nrows, kq));
+        carve_act(act, base, ne0, nrows, kq);
+        p.qs = act.qs; p.qd = act.d; p.qsum = act.s;
+    } else {
+        p.qs = nullptr; p.qd = nullptr; p.qsum = nullptr;
+    }
+    switch (ne0 / 1024) {
+        case 1: hipLaunchKernelGGL(k_norm_fused<1>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+        case 2: hipLaunchKernelGGL(k_norm_fused<2>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+        case 3: hipLaunchKernelGGL(k_norm_fused<3>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+        case 4: hipLaunchKernelGGL(k_norm_fused<4>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+        case 5: hipLaunchKernelGGL(k_norm_fused<5>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+        case 6: hipLaunchKernelGGL(k_norm_fused<6>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+        case 7: hipLaunchKernelGGL(k_norm_fused<7>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+        default: hipLaunchKernelGGL(k_norm_fused<8>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+    }
+    if (qmode) ctx.qcache_put(out, qmode == 1, act);
+    return true;
+}
+
+bool fused_mul_quant(exec_ctx & ctx, ggml_tensor * mul, const ggml_tensor * mm) {
+    if (!f32_contig(mul) || !f32_contig(mul->src[0]) || !f32_contig(mul->src[1])) return false;
+    if (!ggml_are_same_shape(mul->src[0], mul->src[1]) || !ggml_are_same_shape(mul, mul->src[0])) return false;
+    const int qmode = consumer_qmode(mm, mul);
+    if (!qmode || mul->ne[0] % 4 != 0) return false;
+    const int64_t K = mul->ne[0], nrows = ggml_nrows(mul);
+    const bool kq = qmode == 1;
+    q8_act act;
+    carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(K, nrows, kq)), K, nrows, kq);
+    const dim3 grid((unsigned) ceil_div(K, 256), (unsigned) nrows);
+    if (kq) {
+        hipLaunchKernelGGL(k_mul_quant<1>, grid, dim3(64), 0, ctx.stream, (const float *) mul->src[0]->data,
+                           (const float *) mul->src[1]->data, (float *) mul->data, K, act.qs, act.d, act.s);
+    } else {
+        hipLaunchKernelGGL(k_mul_quant<2>, grid, dim3(64), 0, ctx.stream, (const float *) mul->src[0]->data,
+                           (const float *) mul->src[1]->data, (float *) mul->data, K, act.qs, act.d, act.s);
+    }
+    ctx.qcache_put(mul, kq, act);
+    return true;
+}
+
+}  // namespace mi355x

@@ -1,0 +1,614 @@
+// k_gemv.hip — decode mat-vec (one activation column) over quantized weights, with
+// grouped launches and fused epilogues.
+//
+// Arithmetic is the one of k_mmv.hip (integer sub-block sums against the CPU-exact Q8_K /
+// Q8_0 activation, fp32 combination per task), so results are those of the general
+// mat-vec kernel.  The layout is built for HBM latency on MI355X:
+//   * a wavefront owns R consecutive weight rows; every lane keeps the activation slice of
+//     its task in VGPRs and walks the R rows, so the activation is read once per R rows
+//     (not once per row) and each lane has R independent 48..64-byte weight loads in
+//     flight;
+//   * for short matrices WPR waves split a row's K range (LDS reduction) so that the grid
+//     keeps >= 2048 waves in flight;
+//   * one launch covers up to three matrices that share src1 (Q/K/V, gate/up): the grid
+//     walks the concatenated row space, each workgroup inside one matrix;
+//   * optional SiLU epilogue: the gate projection also writes silu(gate) — the UNARY node
+//     that follows it — with ggml_vec_silu_f32's arithmetic (vec.cpp:233: AVX-512 ggml_v_silu
+//     on 16-element chunks, x/(1+expf(-x)) on the tail);
+//   * optional f16 epilogue: the V projection also performs the CPY of its output into the
+//     f16 KV cache (destination read from the dynamic-pointer table, exec_ctx::dyn_slot).
+#include "ops.h"
+#include "rope.h"
+
+namespace mi355x {
+
+struct gemv_act { const int8_t * qs; const float * d; const int16_t * s; };
+
+// ---- per-type tasks: load(): activation slice of task t; dot(): that task's weight slice of
+// one row -> fp32 contribution (same formula as k_mmv.hip's tasks) ------------------------------
+__device__ __forceinline__ void k4_scales_g(uint32_t s0, uint32_t s1, uint32_t s2, int j,
+                                            int & sc_lo, int & sc_hi, int & m_lo, int & m_hi) {
+    const uint32_t km1 = 0x3f3f3f3f, km2 = 0x0f0f0f0f, km3 = 0x03030303;
+    const uint32_t u0 = s0 & km1;
+    const uint32_t u1 = (s2 & km2) | (((s0 >> 6) & km3) << 4);
+    const uint32_t u2 = s1 & km1;
+    const uint32_t u3 = ((s2 >> 4) & km2) | (((s1 >> 6) & km3) << 4);
+    const uint32_t sw = j < 2 ? u0 : u1;
+    const uint32_t mw = j < 2 ? u2 : u3;
+    const int sh = 16 * (j & 1);
+    sc_lo = (sw >> sh) & 0xff; sc_hi = (sw >> (sh + 8)) & 0xff;
+    m_lo  = (mw >> sh) & 0xff; m_hi  = (mw >> (sh + 8)) & 0xff;
+}
+
+struct g_q4_K {
+    static constexpr int per_block = 4, blk_bytes = 144;
+    struct act { int a[16]; int bs0, bs1; float dy; };
+    __device__ static void load(const gemv_act & A, int t, act & x) {
+        const int b = t >> 2, j = t & 3;
+        const int4 * v = (const int4 *) (A.qs + b * 256 + 64 * j);
+        const int4 v0 = v[0], v1 = v[1], v2 = v[2], v3 = v[3];
+        x.a[0] = v0.x; x.a[1] = v0.y; x.a[2] = v0.z; x.a[3] = v0.w;
+        x.a[4] = v1.x; x.a[5] = v1.y; x.a[6] = v1.z; x.a[7] = v1.w;
+        x.a[8] = v2.x; x.a[9] = v2.y; x.a[10] = v2.z; x.a[11] = v2.w;
+        x.a[12] = v3.x; x.a[13] = v3.y; x.a[14] = v3.z; x.a[15] = v3.w;
+        const int16_t * bs = A.s + b * 16 + 4 * j;
+        x.bs0 = bs[0] + bs[1];
+        x.bs1 = bs[2] + bs[3];
+        x.dy = A.d[b];
+    }
+    struct raw { uint4 hdr, qa, qb; };
+    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+        const int b = t >> 2, j = t & 3;
+        const uint8_t * blk = wrow + (int64_t) b * 144;
+        w.hdr = ld16(blk);
+        w.qa  = ld16(blk + 16 + 32 * j);
+        w.qb  = ld16(blk + 32 + 32 * j);
+    }
+    __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
+        raw w;
+        fetch(wrow, t, w);
+        return dotr(w, t, x);
+    }
+    __device__ static float dotr(const raw & w, int t, const act & x) {
+        const int j = t & 3;
+        const uint4 hdr = w.hdr, qa = w.qa, qb = w.qb;
+        const float d    = h2f(hdr.x & 0xffff);
+        const float dmin = h2f(hdr.x >> 16);
+        int sc_lo, sc_hi, m_lo, m_hi;
+        k4_scales_g(hdr.y, hdr.z, hdr.w, j, sc_lo, sc_hi, m_lo, m_hi);
+        const uint32_t q[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+        int dl = 0, dh = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            dl = dot4((int) (q[i] & 0x0f0f0f0f), x.a[i], dl);
+            dh = dot4((int) ((q[i] >> 4) & 0x0f0f0f0f), x.a[8 + i], dh);
+        }
+        const int sumi = sc_lo * dl + sc_hi * dh;
+        const int summ = m_lo * x.bs0 + m_hi * x.bs1;
+        return (d * x.dy) * (float) sumi - (dmin * x.dy) * (float) summ;
+    }
+};
+
+struct g_q5_K {
+    static constexpr int per_block = 4, blk_bytes = 176;
+    using act = g_q4_K::act;
+    __device__ static void load(const gemv_act & A, int t, act & x) { g_q4_K::load(A, t, x); }
+    struct raw { uint4 hdr, ha, hb, qa, qb; };
+    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+        const int b = t >> 2, j = t & 3;
+        const uint8_t * blk = wrow + (int64_t) b * 176;
+        w.hdr = ld16(blk);
+        w.ha  = ld16(blk + 16);
+        w.hb  = ld16(blk + 32);
+        w.qa  = ld16(blk + 48 + 32 * j);
+        w.qb  = ld16(blk + 64 + 32 * j);
+    }
+    __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
+        raw w;
+        fetch(wrow, t, w);
+        return dotr(w, t, x);
+    }
+    __device__ static float dotr(const raw & w, int t, const act & x) {
+        const int j = t & 3;
+        const uint4 hdr = w.hdr, ha = w.ha, hb = w.hb, qa = w.qa, qb = w.qb;
+        const float d    = h2f(hdr.x & 0xffff);
+        const float dmin = h2f(hdr.x >> 16);
+        int sc_lo, sc_hi, m_lo, m_hi;
+        k4_scales_g(hdr.y, hdr.z, hdr.w, j, sc_lo, sc_hi, m_lo, m_hi);
+        const uint32_t q[8]  = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+        const uint32_t qh[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+        int dl = 0, dh = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t lo = (q[i] & 0x0f0f0f0f) | (((qh[i] >> (2 * j)) & 0x01010101) << 4);
+            const uint32_t hi = ((q[i] >> 4) & 0x0f0f0f0f) | (((qh[i] >> (2 * j + 1)) & 0x01010101) << 4);
+            dl = dot4((int) lo, x.a[i], dl);
+            dh = dot4((int) hi, x.a[8 + i], dh);
+        }
+        const int sumi = sc_lo * dl + sc_hi * dh;
+        const int summ = m_lo * x.bs0 + m_hi * x.bs1;
+        return (d * x.dy) * (float) sumi - (dmin * x.dy) * (float) summ;
+    }
+};
+
+struct g_q6_K {
+    static constexpr int per_block = 4, blk_bytes = 210;
+    struct act { int4 a0, a1, a2, a3; int b0, b1, b2, b3; float dy; };
+    __device__ static void load(const gemv_act & A, int t, act & x) {
+        const int b = t >> 2, h = (t >> 1) & 1, lr = t & 1;
+        const int8_t * ap = A.qs + b * 256 + 128 * h + 16 * lr;
+        x.a0 = *(const int4 *) (ap);
+        x.a1 = *(const int4 *) (ap + 32);
+        x.a2 = *(const int4 *) (ap + 64);
+        x.a3 = *(const int4 *) (ap + 96);
+        const int16_t * bs = A.s + b * 16 + 8 * h + lr;
+        x.b0 = 32 * bs[0]; x.b1 = 32 * bs[2]; x.b2 = 32 * bs[4]; x.b3 = 32 * bs[6];
+        x.dy = A.d[b];
+    }
+    struct raw { uint4 la, lb, hh; uint2 sc8; uint32_t d16; };
+    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+        const int b = t >> 2, h = (t >> 1) & 1, lr = t & 1;
+        const uint8_t * blk = wrow + (int64_t) b * 210;
+        w.la = ld16(blk + 64 * h + 16 * lr);
+        w.lb = ld16(blk + 64 * h + 32 + 16 * lr);
+        w.hh = ld16(blk + 128 + 32 * h + 16 * lr);
+        w.sc8 = ld8(blk + 192 + 8 * h);
+        w.d16 = ld2(blk + 208);
+    }
+    __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
+        raw w;
+        fetch(wrow, t, w);
+        return dotr(w, t, x);
+    }
+    __device__ static float dotr(const raw & w, int t, const act & x) {
+        const int lr = t & 1;
+        const uint4 la = w.la, lb = w.lb, hh = w.hh;
+        const uint2 sc8 = w.sc8;
+        const float d = h2f((uint16_t) w.d16);
+        const int sc0 = (int8_t) ((sc8.x >> (8 * lr)) & 0xff);
+        const int sc1 = (int8_t) ((sc8.x >> (8 * lr + 16)) & 0xff);
+        const int sc2 = (int8_t) ((sc8.y >> (8 * lr)) & 0xff);
+        const int sc3 = (int8_t) ((sc8.y >> (8 * lr + 16)) & 0xff);
+        const uint32_t L[4] = {la.x, la.y, la.z, la.w};
+        const uint32_t M[4] = {lb.x, lb.y, lb.z, lb.w};
+        const uint32_t H[4] = {hh.x, hh.y, hh.z, hh.w};
+        const int A0[4] = {x.a0.x, x.a0.y, x.a0.z, x.a0.w};
+        const int A1[4] = {x.a1.x, x.a1.y, x.a1.z, x.a1.w};
+        const int A2[4] = {x.a2.x, x.a2.y, x.a2.z, x.a2.w};
+        const int A3[4] = {x.a3.x, x.a3.y, x.a3.z, x.a3.w};
+        int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s0 = dot4((int) ((L[i] & 0x0f0f0f0f)        | ((H[i] & 0x03030303) << 4)), A0[i], s0);
+            s1 = dot4((int) ((M[i] & 0x0f0f0f0f)        | (((H[i] >> 2) & 0x03030303) << 4)), A1[i], s1);
+            s2 = dot4((int) (((L[i] >> 4) & 0x0f0f0f0f) | (((H[i] >> 4) & 0x03030303) << 4)), A2[i], s2);
+            s3 = dot4((int) (((M[i] >> 4) & 0x0f0f0f0f) | (((H[i] >> 6) & 0x03030303) << 4)), A3[i], s3);
+        }
+        s0 -= x.b0; s1 -= x.b1; s2 -= x.b2; s3 -= x.b3;
+        const int sumi = sc0 * s0 + sc1 * s1 + sc2 * s2 + sc3 * s3;
+        return (d * x.dy) * (float) sumi;
+    }
+};
+
+struct g_q8_0 {
+    static constexpr int per_block = 1, blk_bytes = 34;
+    struct act { int4 a0, a1; float dy; };
+    __device__ static void load(const gemv_act & A, int t, act & x) {
+        const int4 * ap = (const int4 *) (A.qs + (int64_t) t * 32);
+        x.a0 = ap[0]; x.a1 = ap[1];
+        x.dy = A.d[t];
+    }
+    struct raw { uint4 qa, qb; uint32_t d16; };
+    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+        const uint8_t * blk = wrow + (int64_t) t * 34;
+        w.d16 = ld2(blk);
+        w.qa = ld16(blk + 2);
+        w.qb = ld16(blk + 18);
+    }
+    __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
+        raw w;
+        fetch(wrow, t, w);
+        return dotr(w, t, x);
+    }
+    __device__ static float dotr(const raw & w, int t, const act & x) {
+        const float d = h2f((uint16_t) w.d16);
+        const uint4 qa = w.qa, qb = w.qb;
+        int s = 0;
+        s = dot4(qa.x, x.a0.x, s); s = dot4(qa.y, x.a0.y, s); s = dot4(qa.z, x.a0.z, s); s = dot4(qa.w, x.a0.w, s);
+        s = dot4(qb.x, x.a1.x, s); s = dot4(qb.y, x.a1.y, s); s = dot4(qb.z, x.a1.z, s); s = dot4(qb.w, x.a1.w, s);
+        return (float) s * (d * x.dy);
+    }
+};
+
+struct g_q4_0 {
+    static constexpr int per_block = 1, blk_bytes = 18;
+    struct act { int4 a0, a1; int s8; float dy; };
+    __device__ static void load(const gemv_act & A, int t, act & x) {
+        const int4 * ap = (const int4 *) (A.qs + (int64_t) t * 32);
+        x.a0 = ap[0]; x.a1 = ap[1];
+        x.s8 = 8 * A.s[t];
+        x.dy = A.d[t];
+    }
+    struct raw { uint4 q; uint32_t d16; };
+    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+        const uint8_t * blk = wrow + (int64_t) t * 18;
+        w.d16 = ld2(blk);
+        w.q = ld16(blk + 2);
+    }
+    __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
+        raw r;
+        fetch(wrow, t, r);
+        return dotr(r, t, x);
+    }
+    __device__ static float dotr(const raw & r, int t, const act & x) {
+        const float d = h2f((uint16_t) r.d16);
+        const uint4 q = r.q;
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+        const int al[4] = {x.a0.x, x.a0.y, x.a0.z, x.a0.w};
+        const int ah[4] = {x.a1.x, x.a1.y, x.a1.z, x.a1.w};
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s = dot4((int) (w[i] & 0x0f0f0f0f), al[i], s);
+            s = dot4((int) ((w[i] >> 4) & 0x0f0f0f0f), ah[i], s);
+        }
+        s -= x.s8;
+        return (float) s * (d * x.dy);
+    }
+};
+
+// ---- kernel ------------------------------------------------------------------------------------
+constexpr int GEMV_MAXMAT = 3;
+
+struct gemv_args {
+    const uint8_t * W[GEMV_MAXMAT]; int64_t nb01[GEMV_MAXMAT]; int64_t M[GEMV_MAXMAT];
+    float * dst[GEMV_MAXMAT];
+    float * silu[GEMV_MAXMAT];            // SiLU epilogue output (nullable)
+    uint16_t * const * f16out[GEMV_MAXMAT];   // fused f32->f16 CPY (KV-cache store) slot (nullable)
+    int64_t blk0[GEMV_MAXMAT + 1];        // first workgroup of each matrix
+    gemv_act A;
+    int ntasks;
+    // fused ROPE (NORM mode, one token) of the projection output: adjacent rows (2i, 2i+1)
+    // of a head are rotated in the epilogue; optional f16 copy of the result (KV-cache store)
+    float * rope_out[GEMV_MAXMAT];
+    uint16_t * const * rope_f16[GEMV_MAXMAT];
+    rope_params rp;
+    const int32_t * rope_pos; const float * rope_ff; int64_t rope_d;
+    int need_pairs;
+};
+
+// epilogue of one output row; v = this row's sum, vp = the sum of its rope partner row^1
+__device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t M, int64_t row, float v, float vp) {
+    p.dst[mi][row] = v;
+    if (p.f16out[mi]) (*p.f16out[mi])[row] = f2h(v);
+    if (p.silu[mi]) {
+        const int64_t nvec = (M / 16) * 16;
+        p.silu[mi][row] = row < nvec ? v / (1.0f + v_expf_avx512(-v)) : v / (1.0f + expf_cr(-v));
+    }
+    if (p.rope_out[mi]) {
+        const int64_t i0 = row % p.rope_d;
+        float o = v;
+        if (i0 < p.rp.n_dims) {
+            float c, sn, o0, o1;
+            rope_cs(p.rp, (float) p.rope_pos[0], i0 / 2, p.rope_ff, c, sn);
+            const bool odd = row & 1;
+            rope_rotate(odd ? vp : v, odd ? v : vp, c, sn, o0, o1);
+            o = odd ? o1 : o0;
+        }
+        p.rope_out[mi][row] = o;
+        if (p.rope_f16[mi]) (*p.rope_f16[mi])[row] = f2h(o);
+    }
+}
+
+typedef __attribute__((address_space(3))) void * lds_vptr;
+
+template <class T, int R, int WPR, bool LDS>
+__global__ __launch_bounds__(256) void k_gemv(const gemv_args p) {
+    constexpr int RB = (4 / WPR) * R;   // rows per workgroup
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wsub = wave % WPR;
+    int mi = 0;
+#pragma unroll
+    for (int k = 1; k < GEMV_MAXMAT; ++k) mi += blockIdx.x >= p.blk0[k] ? 1 : 0;
+    const int64_t M = p.M[mi];
+    const int64_t rowg = (blockIdx.x - p.blk0[mi]) * RB;     // first row of the workgroup
+    const int64_t row0 = rowg + (wave / WPR) * R;            // first row of this wave
+    const uint8_t * W = p.W[mi];
+    const int64_t nb01 = p.nb01[mi];
+
+    float acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+    const uint8_t * wrow[R];
+    if constexpr (LDS) {
+        // stream the workgroup's RB contiguous rows HBM -> LDS (global_load_lds, 16 B per
+        // lane, 1 KiB per wave instruction, no VGPRs), then compute out of LDS
+        extern __shared__ __attribute__((aligned(16))) uint8_t slab[];
+        const int64_t nrow = min((int64_t) RB, M - rowg);
+        const int64_t nchunk = nrow * nb01 / 16;
+        const int64_t last = nchunk - 1;
+        const uint8_t * src = W + rowg * nb01;
+        for (int64_t c0 = (int64_t) wave * 64; c0 < nchunk; c0 += 256) {
+            const int64_t c = min(c0 + lane, last);
+            __builtin_amdgcn_global_load_lds((const void *) (src + 16 * c), (lds_vptr) (slab + 16 * c0), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r) wrow[r] = slab + min((int64_t) ((wave / WPR) * R + r), nrow - 1) * nb01;
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) wrow[r] = W + min(row0 + r, M - 1) * nb01;
+    }
+
+    if (row0 < M) {
+        for (int t = wsub * WAVE + lane; t < p.ntasks; t += WAVE * WPR) {
+            typename T::act x;
+            T::load(p.A, t, x);
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r] += T::dot(wrow[r], t, x);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+    if constexpr (WPR > 1) {
+        __shared__ float red[4][R];
+        if (lane == 0) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) red[wave][r] = acc[r];
+        }
+        __syncthreads();
+        if (wsub == 0) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                float s = red[wave][r];
+#pragma unroll
+                for (int w = 1; w < WPR; ++w) s += red[wave + w][r];
+                acc[r] = s;
+            }
+        }
+    }
+    if (wsub == 0 && lane < R) {
+        float v = acc[0], vp = acc[R > 1 ? 1 : 0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) v = lane == r ? acc[r] : v;
+#pragma unroll
+        for (int r = 0; r < R; ++r) vp = (lane ^ 1) == r ? acc[r] : vp;
+        const int64_t row = row0 + lane;
+        if (row < M) gemv_store(p, mi, M, row, v, vp);
+    }
+}
+
+// ---- persistent, software-pipelined variant ------------------------------------------------------
+// A grid of ~2 workgroups per CU walks the row groups; each wave fetches the next group's
+// weight slices into registers before computing the current one, so dequantization and the
+// dot products overlap the HBM stream instead of following it (a one-shot grid computes
+// only after its last load lands).  Needs ntasks <= 64*WPR (one pass over K per wave).
+template <class T, int R, int WPR>
+__global__ __launch_bounds__(256) void k_gemv_pipe(const gemv_args p, const int64_t ngroups) {
+    constexpr int RPG = (4 / WPR) * R;   // rows per group
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wsub = wave % WPR;
+    const int t = wsub * WAVE + lane;
+    const bool active = t < p.ntasks;
+    const int tt = active ? t : 0;
+    typename T::act x;
+    T::load(p.A, tt, x);
+
+    auto locate = [&](int64_t g, int & mi, int64_t & row0) {
+        mi = 0;
+#pragma unroll
+        for (int k = 1; k < GEMV_MAXMAT; ++k) mi += g >= p.blk0[k] ? 1 : 0;
+        row0 = (g - p.blk0[mi]) * RPG + (wave / WPR) * R;
+    };
+    auto fetch = [&](int64_t g, typename T::raw (&w)[R]) {
+        int mi;
+        int64_t row0;
+        locate(g, mi, row0);
+        const int64_t M = p.M[mi];
+#pragma unroll
+        for (int r = 0; r < R; ++r) T::fetch(p.W[mi] + min(row0 + r, M - 1) * p.nb01[mi], tt, w[r]);
+    };
+
+    typename T::raw cur[R], nxt[R];
+    int64_t g = blockIdx.x;
+    if (g < ngroups) fetch(g, cur);
+    __shared__ float red[2][4][R];
+    int par = 0;
+    for (; g < ngroups; g += gridDim.x, par ^= 1) {
+        const int64_t gn = g + gridDim.x;
+        if (gn < ngroups) fetch(gn, nxt);
+        float acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = active ? T::dotr(cur[r], tt, x) : 0.0f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
+        if constexpr (WPR > 1) {
+            if (lane == 0) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) red[par][wave][r] = acc[r];
+            }
+            __syncthreads();
+            if (wsub == 0) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    float s = red[par][wave][r];
+#pragma unroll
+                    for (int w = 1; w < WPR; ++w) s += red[par][wave + w][r];
+                    acc[r] = s;
+                }
+            }
+        }
+        if (wsub == 0 && lane < R) {
+            int mi;
+            int64_t row0;
+            locate(g, mi, row0);
+            const int64_t M = p.M[mi];
+            float v = acc[0], vp = acc[R > 1 ? 1 : 0];
+#pragma unroll
+            for (int r = 1; r < R; ++r) v = lane == r ? acc[r] : v;
+#pragma unroll
+            for (int r = 0; r < R; ++r) vp = (lane ^ 1) == r ? acc[r] : vp;
+            const int64_t row = row0 + lane;
+            if (row < M) gemv_store(p, mi, M, row, v, vp);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) cur[r] = nxt[r];
+    }
+}
+
+// ---- host ----------------------------------------------------------------------------------------
+static int g_gemv_lds = -1;   // GGML_MI355X_GEMV_LDS: 1 = stage weights through LDS
+
+template <class T, int R, int WPR>
+static void launch_g(hipStream_t st, gemv_args & a, int nmat) {
+    constexpr int RB = (4 / WPR) * R;
+    a.blk0[0] = 0;
+    for (int i = 0; i < GEMV_MAXMAT; ++i) {
+        a.blk0[i + 1] = a.blk0[i] + (i < nmat ? ceil_div(a.M[i], RB) : 0);
+    }
+    for (int i = nmat; i < GEMV_MAXMAT; ++i) a.blk0[i] = a.blk0[nmat];   // never selected
+    if (g_gemv_lds < 0) g_gemv_lds = getenv("GGML_MI355X_GEMV_LDS") ? atoi(getenv("GGML_MI355X_GEMV_LDS")) : 0;
+    int64_t maxrow = 0;
+    bool rows16 = true;
+    for (int i = 0; i < nmat; ++i) {
+        maxrow = std::max<int64_t>(maxrow, a.nb01[i]);
+        rows16 = rows16 && a.nb01[i] % 16 == 0 && ((uintptr_t) a.W[i]) % 16 == 0;
+    }
+    const size_t slab = (size_t) RB * maxrow;
+    if (g_gemv_lds && rows16 && slab <= 64 * 1024) {
+        hipLaunchKernelGGL((k_gemv<T, R, WPR, true>), dim3((unsigned) a.blk0[nmat]), dim3(256), slab, st, a);
+    } else {
+        hipLaunchKernelGGL((k_gemv<T, R, WPR, false>), dim3((unsigned) a.blk0[nmat]), dim3(256), 0, st, a);
+    }
+}
+
+static int g_gemv_pipe = -1;   // GGML_MI355X_GEMV_PIPE: 0 disables the pipelined kernel
+static int g_gemv_wgs = -1;    // GGML_MI355X_GEMV_WGS: persistent grid size
+
+template <class T, int R, int WPR>
+static void launch_pipe(hipStream_t st, gemv_args & a, int nmat) {
+    constexpr int RPG = (4 / WPR) * R;
+    a.blk0[0] = 0;
+    for (int i = 0; i < GEMV_MAXMAT; ++i) a.blk0[i + 1] = a.blk0[i] + (i < nmat ? ceil_div(a.M[i], RPG) : 0);
+    for (int i = nmat; i < GEMV_MAXMAT; ++i) a.blk0[i] = a.blk0[nmat];
+    const int64_t ng = a.blk0[nmat];
+    const int64_t grid = std::min<int64_t>(ng, g_gemv_wgs);
+    hipLaunchKernelGGL((k_gemv_pipe<T, R, WPR>), dim3((unsigned) grid), dim3(256), 0, st, a, ng);
+}
+
+template <class T>
+static bool launch_pipe_t(hipStream_t st, gemv_args & a, int nmat, int64_t Mt) {
+    if (g_gemv_pipe < 0) g_gemv_pipe = getenv("GGML_MI355X_GEMV_PIPE") ? atoi(getenv("GGML_MI355X_GEMV_PIPE")) : 1;
+    if (g_gemv_wgs < 0) g_gemv_wgs = getenv("GGML_MI355X_GEMV_WGS") ? atoi(getenv("GGML_MI355X_GEMV_WGS")) : 512;
+    if (!g_gemv_pipe || a.ntasks > 4 * WAVE) return false;
+    const int wpr = a.ntasks <= WAVE ? 1 : (a.ntasks <= 2 * WAVE ? 2 : 4);
+    const int64_t g4 = ceil_div(Mt * wpr, 16);   // groups with R = 4
+    int R = g4 >= 512 ? 4 : (2 * g4 >= 512 ? 2 : 1);
+    if (R == 1 && a.need_pairs) R = 2;   // the rope epilogue needs rows 2i, 2i+1 in one wave
+    switch (R * 8 + wpr) {
+        case 4 * 8 + 1: launch_pipe<T, 4, 1>(st, a, nmat); break;
+        case 4 * 8 + 2: launch_pipe<T, 4, 2>(st, a, nmat); break;
+        case 4 * 8 + 4: launch_pipe<T, 4, 4>(st, a, nmat); break;
+        case 2 * 8 + 1: launch_pipe<T, 2, 1>(st, a, nmat); break;
+        case 2 * 8 + 2: launch_pipe<T, 2, 2>(st, a, nmat); break;
+        case 2 * 8 + 4: launch_pipe<T, 2, 4>(st, a, nmat); break;
+        case 1 * 8 + 1: launch_pipe<T, 1, 1>(st, a, nmat); break;
+        case 1 * 8 + 2: launch_pipe<T, 1, 2>(st, a, nmat); break;
+        default:        launch_pipe<T, 1, 4>(st, a, nmat); break;
+    }
+    return true;
+}
+
+template <class T>
+static void launch_t(hipStream_t st, gemv_args & a, int nmat) {
+    int64_t Mt = 0;
+    for (int i = 0; i < nmat; ++i) Mt += a.M[i];
+    if (launch_pipe_t<T>(st, a, nmat, Mt)) return;
+    // WPR depends on K only, so a row's summation order (and its bits) is the same whether
+    // the matrix is launched alone or grouped; R (rows per wave: activation reuse, loads in
+    // flight) is then the largest that keeps >= 2048 waves on the chip
+    const int wpr = a.ntasks >= 8 * WAVE ? 4 : (a.ntasks >= 3 * WAVE ? 2 : 1);
+    int R = ceil_div(Mt, 4) * wpr >= 2048 ? 4 : (ceil_div(Mt, 2) * wpr >= 2048 ? 2 : 1);
+    if (R == 1 && a.need_pairs) R = 2;
+    switch (R * 8 + wpr) {
+        case 4 * 8 + 1: launch_g<T, 4, 1>(st, a, nmat); break;
+        case 4 * 8 + 2: launch_g<T, 4, 2>(st, a, nmat); break;
+        case 4 * 8 + 4: launch_g<T, 4, 4>(st, a, nmat); break;
+        case 2 * 8 + 1: launch_g<T, 2, 1>(st, a, nmat); break;
+        case 2 * 8 + 2: launch_g<T, 2, 2>(st, a, nmat); break;
+        case 2 * 8 + 4: launch_g<T, 2, 4>(st, a, nmat); break;
+        case 1 * 8 + 2: launch_g<T, 1, 2>(st, a, nmat); break;
+        case 1 * 8 + 4: launch_g<T, 1, 4>(st, a, nmat); break;
+        default:        launch_g<T, 1, 1>(st, a, nmat); break;
+    }
+}
+
+static bool is_kq(ggml_type t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
+
+bool gemv_supported(const ggml_tensor * mm) {
+    const ggml_tensor * w = mm->src[0];
+    const ggml_tensor * x = mm->src[1];
+    switch (w->type) {
+        case GGML_TYPE_Q4_0: case GGML_TYPE_Q8_0: case GGML_TYPE_Q4_K: case GGML_TYPE_Q5_K: case GGML_TYPE_Q6_K: break;
+        default: return false;
+    }
+    return x->type == GGML_TYPE_F32 && x->ne[1] == 1 && x->ne[2] == 1 && x->ne[3] == 1 && w->ne[2] == 1 && w->ne[3] == 1 &&
+           mm->type == GGML_TYPE_F32 && ggml_is_contiguous(mm) && x->nb[0] == 4 &&
+           w->ne[0] % ggml_blck_size(w->type) == 0;
+}
+
+bool gemv_epilogue_ok(const ggml_tensor * mm) { return gemv_supported(mm); }
+
+// one launch for up to three MUL_MATs sharing src1 (all gemv_supported, same weight type
+// and K); silu[i] = optional SiLU output for matrix i
+void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi) {
+    GGML_ASSERT(nmat >= 1 && nmat <= GEMV_MAXMAT);
+    const ggml_tensor * src1 = mms[0]->src[1];
+    const ggml_type wt = mms[0]->src[0]->type;
+    const bool kq = is_kq(wt);
+    hipEvent_t ev_beg = nullptr;
+    double bytes = 0;
+    for (int i = 0; i < nmat; ++i) bytes += (double) ggml_nbytes(mms[i]->src[0]) + (double) ggml_nbytes(mms[i]);
+    bytes += (double) src1->ne[0] * (kq ? 1.14 : 1.0);
+    if (ctx.timing) ctx.time_begin(TK_MMV, bytes, ev_beg);
+
+    q8_act act;
+    if (!ctx.qcache_get(src1, kq, act)) {
+        quantize_act(ctx, src1, kq, act, exec_ctx::QSLOT);
+        ctx.qcache_put(src1, kq, act);
+    }
+    gemv_args a = {};
+    for (int i = 0; i < nmat; ++i) {
+        const ggml_tensor * w = mms[i]->src[0];
+        a.W[i] = (const uint8_t *) w->data;
+        a.nb01[i] = w->nb[1];
+        a.M[i] = w->ne[1];
+        a.dst[i] = (float *) mms[i]->data;
+        a.silu[i] = epi && epi->silu[i] ? (float *) epi->silu[i]->data : nullptr;
+        a.f16out[i] = epi ? (uint16_t * const *) epi->f16out[i] : nullptr;
+        a.rope_out[i] = epi && epi->rope[i] ? (float *) epi->rope[i]->data : nullptr;
+        a.rope_f16[i] = epi ? (uint16_t * const *) epi->rope_f16[i] : nullptr;
+        if (a.rope_out[i]) {
+            const ggml_tensor * r = epi->rope[i];
+            rope_params_of(r, a.rp);
+            a.rope_pos = (const int32_t *) r->src[1]->data;
+            a.rope_ff = r->src[2] ? (const float *) r->src[2]->data : nullptr;
+            a.rope_d = r->src[0]->ne[0];
+            a.need_pairs = 1;
+        }
+    }
+    a.A = {act.qs, act.d, act.s};
+    const int64_t nblk = src1->ne[0] / ggml_blck_size(wt);
+    switch (wt) {
+        case GGML_TYPE_Q4_K: a.ntasks = (int) (nblk * 4); launch_t<g_q4_K>(ctx.stream, a, nmat); break;
+        case GGML_TYPE_Q5_K: a.ntasks = (int) (nblk * 4); launch_t<g_q5_K>(ctx.stream, a, nmat); break;
+        case GGML_TYPE_Q6_K: a.ntasks = (int) (nblk * 4); launch_t<g_q6_K>(ctx.stream, a, nmat); break;
+        case GGML_TYPE_Q8_0: a.ntasks = (int) nblk;       launch_t<g_q8_0>(ctx.stream, a, nmat); break;
+        case GGML_TYPE_Q4_0: a.ntasks = (int) nblk;       launch_t<g_q4_0>(ctx.stream, a, nmat); break;
+        default: GGML_ABORT("mi355x: gemv type");
+    }
+    if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
+}
+
+}  // namespace mi355x

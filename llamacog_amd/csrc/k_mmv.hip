@@ -17,6 +17,7 @@
 // (M small) WPR waves split one row's K range and reduce through LDS so the grid still
 // fills 256 CUs.
 #include "ops.h"
+#include "quant_act.h"
 
 namespace mi355x {
 
@@ -24,9 +25,7 @@ namespace mi355x {
 // activation quantizers
 // ------------------------------------------------------------------------------------------
 
-// Q8_K, one wave per 256-element block; lane l holds x[4l..4l+3].
-// Bit-exact restatement of quantize_row_q8_K_ref: first index of max |x| wins,
-// iscale = -127/max, q = min(127, nearest_int(iscale*x)), d = 1/iscale, bsums over 16.
+// Q8_K, one wave per 256-element block; lane l holds x[4l..4l+3] (quant_act.h).
 __global__ __launch_bounds__(64) void k_quantize_q8_K(const char * __restrict__ x, int64_t K,
                                                       int64_t ne1, int64_t ne2,
                                                       int64_t nb1, int64_t nb2, int64_t nb3,
@@ -37,55 +36,12 @@ __global__ __launch_bounds__(64) void k_quantize_q8_K(const char * __restrict__ 
     const int64_t col = blockIdx.y;
     const int64_t i1 = col % ne1, i2 = (col / ne1) % ne2, i3 = col / (ne1 * ne2);
     const float * row = (const float *) (x + i1 * nb1 + i2 * nb2 + i3 * nb3);
-
     const uint4 v = ld16(row + b * 256 + 4 * lane);
-    float vv[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
-
-    // local first-max
-    float amax = 0.0f, vmax = 0.0f;
-    int   imax = 0x7fffffff;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float ax = fabsf(vv[k]);
-        if (ax > amax) { amax = ax; vmax = vv[k]; imax = 4 * lane + k; }
-    }
-    // wave argmax with lowest-index tie break (== sequential strict '>' scan)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float oa = __shfl_xor(amax, o, WAVE);
-        const float ov = __shfl_xor(vmax, o, WAVE);
-        const int   oi = __shfl_xor(imax, o, WAVE);
-        if (oa > amax || (oa == amax && oi < imax)) { amax = oa; vmax = ov; imax = oi; }
-    }
-
-    int8_t * q = qs + col * K + b * 256;
-    int16_t * bsum = bs + col * (K / 16) + b * 16;
-    if (amax == 0.0f) {
-        *(uint32_t *) (q + 4 * lane) = 0;
-        if (lane < 16) bsum[lane] = 0;
-        if (lane == 0) dd[col * (K / 256) + b] = 0.0f;
-        return;
-    }
-    const float iscale = -127.0f / vmax;
-    int s = 0;
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        int iv = (int) rintf(__fmul_rn(iscale, vv[k]));   // nearest_int: round-half-even
-        iv = iv < 127 ? iv : 127;
-        s += iv;
-        packed |= (uint32_t) (iv & 0xff) << (8 * k);
-    }
-    *(uint32_t *) (q + 4 * lane) = packed;
-    s += __shfl_xor(s, 1, WAVE);
-    s += __shfl_xor(s, 2, WAVE);
-    if ((lane & 3) == 0) bsum[lane >> 2] = (int16_t) s;
-    if (lane == 0) dd[col * (K / 256) + b] = 1.0f / iscale;
+    const float vv[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+    q8K_wave(vv, lane, qs + col * K + b * 256, bs + col * (K / 16) + b * 16, dd + col * (K / 256) + b);
 }
 
-// Q8_0 with the x86 AVX rounding (ggml-cpu/arch/x86/quants.c:278-372):
-// d = amax/127, id = 127/amax, q = round-half-even(x*id); d is stored as fp16 by the
-// CPU, so we keep the fp16-rounded value.  Eight lanes per 32-block, lane holds 4 values.
+// Q8_0 (x86 rounding), eight 32-blocks per wave (quant_act.h).
 __global__ __launch_bounds__(64) void k_quantize_q8_0(const char * __restrict__ x, int64_t K,
                                                       int64_t ne1, int64_t ne2,
                                                       int64_t nb1, int64_t nb2, int64_t nb3,
@@ -93,43 +49,17 @@ __global__ __launch_bounds__(64) void k_quantize_q8_0(const char * __restrict__ 
                                                       int16_t * __restrict__ bs) {
     const int lane = threadIdx.x;
     const int64_t col = blockIdx.y;
-    const int64_t e0 = (int64_t) blockIdx.x * 256 + 4 * lane;
+    const int64_t c0 = (int64_t) blockIdx.x * 256;
+    const int64_t e0 = c0 + 4 * lane;
     const int64_t i1 = col % ne1, i2 = (col / ne1) % ne2, i3 = col / (ne1 * ne2);
     const float * row = (const float *) (x + i1 * nb1 + i2 * nb2 + i3 * nb3);
     const bool valid = e0 < K;
-
     float vv[4] = {0.f, 0.f, 0.f, 0.f};
     if (valid) {
         const uint4 v = ld16(row + e0);
         vv[0] = __uint_as_float(v.x); vv[1] = __uint_as_float(v.y); vv[2] = __uint_as_float(v.z); vv[3] = __uint_as_float(v.w);
     }
-    float amax = fmaxf(fmaxf(fabsf(vv[0]), fabsf(vv[1])), fmaxf(fabsf(vv[2]), fabsf(vv[3])));
-    amax = fmaxf(amax, __shfl_xor(amax, 1, WAVE));
-    amax = fmaxf(amax, __shfl_xor(amax, 2, WAVE));
-    amax = fmaxf(amax, __shfl_xor(amax, 4, WAVE));
-
-    const float d  = amax / 127.0f;
-    const float id = amax != 0.0f ? 127.0f / amax : 0.0f;
-    int s = 0;
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        int iv = (int) rintf(__fmul_rn(vv[k], id));
-        iv = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
-        s += iv;
-        packed |= (uint32_t) (iv & 0xff) << (8 * k);
-    }
-    s += __shfl_xor(s, 1, WAVE);
-    s += __shfl_xor(s, 2, WAVE);
-    s += __shfl_xor(s, 4, WAVE);
-    if (valid) {
-        *(uint32_t *) (qs + col * K + e0) = packed;
-        if ((lane & 7) == 0) {
-            const int64_t blk = e0 / 32;
-            dd[col * (K / 32) + blk] = h2f(f2h(d));
-            bs[col * (K / 32) + blk] = (int16_t) s;
-        }
-    }
+    q8_0_wave(vv, lane, valid, qs + col * K + c0, dd + col * (K / 32) + c0 / 32, bs + col * (K / 32) + c0 / 32);
 }
 
 size_t q8_act::bytes(int64_t K, int64_t ncols, bool k_quant) {
@@ -139,7 +69,7 @@ size_t q8_act::bytes(int64_t K, int64_t ncols, bool k_quant) {
     return al(K * ncols) + al(nd * ncols * 4) + al(ns * ncols * 2);
 }
 
-static void carve(q8_act & act, void * base, int64_t K, int64_t ncols, bool k_quant) {
+void carve_act(q8_act & act, void * base, int64_t K, int64_t ncols, bool k_quant) {
     auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
     const int64_t nd = k_quant ? K / 256 : K / 32;
     char * p = (char *) base;
@@ -154,7 +84,7 @@ void quantize_act(exec_ctx & ctx, const ggml_tensor * src, bool k_quant, q8_act 
     const int64_t ncols = src->ne[1] * src->ne[2] * src->ne[3];
     GGML_ASSERT(src->type == GGML_TYPE_F32 && src->nb[0] == 4);
     GGML_ASSERT(K % (k_quant ? 256 : 32) == 0);
-    carve(act, ctx.scratch(slot, q8_act::bytes(K, ncols, k_quant)), K, ncols, k_quant);
+    carve_act(act, ctx.scratch(slot, q8_act::bytes(K, ncols, k_quant)), K, ncols, k_quant);
     dim3 grid((unsigned) ceil_div(K, 256), (unsigned) ncols);
     if (k_quant) {
         hipLaunchKernelGGL(k_quantize_q8_K, grid, dim3(64), 0, ctx.stream, (const char *) src->data, K,
@@ -674,8 +604,13 @@ void mul_mat_vec(exec_ctx & ctx, ggml_tensor * dst, const q8_act * pre) {
 
     if (mmv_q_supported_type(src0->type)) {
         q8_act act;
-        if (pre) act = *pre;
-        else quantize_act(ctx, src1, is_k_quant(src0->type), act, 0);
+        const bool kq = is_k_quant(src0->type);
+        if (pre) {
+            act = *pre;
+        } else if (!ctx.qcache_get(src1, kq, act)) {
+            quantize_act(ctx, src1, kq, act, exec_ctx::QSLOT);
+            ctx.qcache_put(src1, kq, act);
+        }
         mmv_args a;
         a.W = (const uint8_t *) src0->data;
         a.nb01 = src0->nb[1]; a.nb02 = src0->nb[2]; a.nb03 = src0->nb[3];

@@ -9,6 +9,20 @@
 
 namespace mi355x {
 
+// activation quantization shared by mul_mat / mul_mat_id / flash-attn (q8_0 K)
+struct q8_act {
+    int8_t  * qs = nullptr;   // [ncols][K] int8
+    float   * d  = nullptr;   // [ncols][K/blk] scale (already rounded like the CPU's)
+    int16_t * s  = nullptr;   // [ncols][K/grp] partial sums (q8_K: 16-groups, q8_0: 32-blocks)
+    int64_t   K  = 0;
+    int64_t   ncols = 0;
+    bool      k_quant = false; // Q8_K (256-blocks) vs Q8_0 (32-blocks)
+    int64_t qs_stride() const { return K; }
+    int64_t d_stride()  const { return k_quant ? K / 256 : K / 32; }
+    int64_t s_stride()  const { return k_quant ? K / 16 : K / 32; }
+    static size_t bytes(int64_t K, int64_t ncols, bool k_quant);
+};
+
 // Per-(context, device) execution state: one HIP stream plus a stream-ordered
 // scratch arena for op temporaries (quantized activations, attention partials).
 struct exec_ctx {
@@ -24,6 +38,45 @@ struct exec_ctx {
     void * scratch(int slot, size_t bytes);
     void   free_scratch();
 
+    // Activation-quantization cache.  Slot QSLOT holds the last quantized MUL_MAT input;
+    // consecutive MUL_MATs that share src1 (Q/K/V, gate/up) reuse it, and fused producers
+    // (norm / mul kernels, k_fused.hip) fill it ahead of their consumer.  Keyed on the
+    // ggml node (and its data pointer) and cleared at the start of every graph_compute,
+    // because libllama re-uses node objects across graphs.
+    static constexpr int QSLOT = 0;
+    const ggml_tensor * qc_tensor = nullptr;
+    const void *        qc_data   = nullptr;
+    bool                qc_kquant = false;
+    q8_act              qc_act;
+    void qcache_clear() { qc_tensor = nullptr; qc_data = nullptr; }
+
+    // nodes already computed ahead of their position by a grouped launch (dispatch.cpp)
+    std::vector<const ggml_tensor *> done;
+
+    // Dynamic destinations: a KV-cache store (CPY into a view at offset n_past) changes its
+    // destination every token while the rest of the graph stays identical.  Kernels read
+    // such pointers from a device table refreshed before each graph launch, so a captured
+    // hipGraph can be replayed (the role of ggml-cuda's cpy dest-pointer indirection).
+    std::vector<const ggml_tensor *> dyn_nodes;   // CPY nodes of the current graph
+    std::vector<void *>              dyn_host;    // their destination pointers
+    void **                          dyn_dev = nullptr;
+    size_t                           dyn_cap = 0;
+    bool prepare_dyn(ggml_cgraph * g);            // scan + upload; false = table too small (backend.cpp)
+    void * const * dyn_slot(const ggml_tensor * cpy) const {
+        for (size_t k = 0; k < dyn_nodes.size(); ++k) {
+            if (dyn_nodes[k] == cpy) return dyn_dev + k;
+        }
+        return nullptr;
+    }
+    bool qcache_get(const ggml_tensor * t, bool k_quant, q8_act & act) const {
+        if (qc_tensor != t || qc_data != t->data || qc_kquant != k_quant) return false;
+        act = qc_act;
+        return true;
+    }
+    void qcache_put(const ggml_tensor * t, bool k_quant, const q8_act & act) {
+        qc_tensor = t; qc_data = t->data; qc_kquant = k_quant; qc_act = act;
+    }
+
     // kernel timing (HIP events on `stream`) for the roofline figure in bench.py
     bool   timing = false;
     struct timed { hipEvent_t beg, end; double bytes; int kind; };
@@ -38,7 +91,14 @@ struct exec_ctx {
     void   collect_timing();  // after a stream synchronize
 };
 
-enum timed_kind { TK_MMV = 0, TK_MMQ = 1, TK_FATTN = 2, TK_OTHER = 3 };
+enum timed_kind { TK_MMV = 0, TK_MMQ = 1, TK_FATTN = 2, TK_OTHER = 3, TK_GRAPH = 5, TK_GRAPH_HOST = 6 };
+
+// run-time switches (backend.cpp): GGML_MI355X_NO_FUSE=1 runs every node with its own
+// kernel, GGML_MI355X_NO_GRAPH=1 disables hipGraph replay; both also settable through
+// ggml_backend_mi355x_set_flags (fused/unfused and graph/eager runs are compared
+// bit-for-bit in tests/test_gpu_model.py)
+bool fusion_enabled();
+bool graphs_enabled();
 
 // supports / dispatch
 bool op_supported(const ggml_tensor * op);
@@ -53,30 +113,37 @@ void op_norm(exec_ctx & ctx, ggml_tensor * dst);
 void op_binary(exec_ctx & ctx, ggml_tensor * dst);
 void op_scale(exec_ctx & ctx, ggml_tensor * dst);
 void op_unary(exec_ctx & ctx, ggml_tensor * dst);
-void op_cpy(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst);
+// node = the CPY node (its destination may live in the dynamic-pointer table) or nullptr
+void op_cpy(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst, const ggml_tensor * node);
 void op_rope(exec_ctx & ctx, ggml_tensor * dst);
+void op_rope_multi(exec_ctx & ctx, ggml_tensor * const * nodes, int n, void * const * const * cache);
 void op_soft_max(exec_ctx & ctx, ggml_tensor * dst);
-void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst);
+// mm: the MUL_MAT consuming (a reshape of) dst, whose input the exact kernel may quantize
+void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm = nullptr);
 void op_argsort(exec_ctx & ctx, ggml_tensor * dst);
 void op_sum_rows(exec_ctx & ctx, ggml_tensor * dst);
 void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst);
 
-// activation quantization shared by mul_mat / mul_mat_id / flash-attn (q8_0 K)
-struct q8_act {
-    int8_t  * qs = nullptr;   // [ncols][K] int8
-    float   * d  = nullptr;   // [ncols][K/blk] scale (already rounded like the CPU's)
-    int16_t * s  = nullptr;   // [ncols][K/grp] partial sums (q8_K: 16-groups, q8_0: 32-blocks)
-    int64_t   K  = 0;
-    int64_t   ncols = 0;
-    bool      k_quant = false; // Q8_K (256-blocks) vs Q8_0 (32-blocks)
-    int64_t qs_stride() const { return K; }
-    int64_t d_stride()  const { return k_quant ? K / 256 : K / 32; }
-    int64_t s_stride()  const { return k_quant ? K / 16 : K / 32; }
-    static size_t bytes(int64_t K, int64_t ncols, bool k_quant);
-};
-
 // quantizes ncols rows of an f32 tensor (row i = (i1, i2, i3) flattened) into act
 void quantize_act(exec_ctx & ctx, const ggml_tensor * src, bool k_quant, q8_act & act, int slot);
+// fused epilogues of a grouped decode GEMV (k_gemv.hip), per matrix of the group
+struct gemv_epi {
+    ggml_tensor *  silu[3]     = {nullptr, nullptr, nullptr};   // UNARY SILU of the output
+    void * const * f16out[3]   = {nullptr, nullptr, nullptr};   // dyn slot: f16 CPY of the output
+    ggml_tensor *  rope[3]     = {nullptr, nullptr, nullptr};   // ROPE (NORM mode) of the output
+    void * const * rope_f16[3] = {nullptr, nullptr, nullptr};   // dyn slot: f16 CPY of the rope
+};
+bool gemv_supported(const ggml_tensor * mm);
+bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
+void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi);
+
+// lays out a q8_act (qs | d | s, 256-B aligned) in `base`
+void carve_act(q8_act & act, void * base, int64_t K, int64_t ncols, bool k_quant);
+
+// fused producers (k_fused.hip); false = pattern not applicable, nothing launched
+bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm);
+bool fused_mul_quant(exec_ctx & ctx, ggml_tensor * mul, const ggml_tensor * mm);
+
 void quantize_act_raw(hipStream_t stream, const float * x, int64_t K, int64_t ncols, int64_t row_stride_elems,
                       bool k_quant, q8_act & act);
 

@@ -54,16 +54,19 @@ struct llb {
 bool dump_cb(struct ggml_tensor * t, bool ask, void * ud) {
     auto * h = (llb *) ud;
     if (ask) return h->dump;
-    if (t->type != GGML_TYPE_F32 || ggml_nelements(t) > (1 << 22)) return true;
     dump_rec r;
     r.name = t->name;
     r.op = (int) t->op;
     for (int i = 0; i < 4; ++i) r.ne[i] = t->ne[i];
+    if (t->type != GGML_TYPE_F32 || ggml_nelements(t) > (1 << 22)) {   // order only, no data
+        h->recs.push_back(std::move(r));
+        return true;
+    }
     r.data.resize(ggml_nelements(t));
     if (ggml_is_contiguous(t)) {
         ggml_backend_tensor_get(t, r.data.data(), 0, ggml_nbytes(t));
     } else {
-        return true;
+        r.data.clear();
     }
     h->recs.push_back(std::move(r));
     return true;
@@ -190,6 +193,28 @@ double llb_time_gen(void * hp, int n_gen) {
         llama_synchronize(h->ctx);
         tok = std::rand() % h->n_vocab;
     }
+    return now_s() - t0;
+}
+
+// test_gen with the host time split: seconds inside llama_decode (graph build, scheduling,
+// input upload, launch) and inside llama_synchronize (waiting for the device)
+double llb_time_gen_split(void * hp, int n_gen, double * t_decode, double * t_sync) {
+    auto * h = (llb *) hp;
+    int32_t tok = llama_vocab_get_add_bos(h->vocab) ? llama_vocab_bos(h->vocab) : std::rand() % h->n_vocab;
+    double td = 0, ts = 0;
+    const double t0 = now_s();
+    for (int i = 0; i < n_gen; ++i) {
+        const double a = now_s();
+        if (llama_decode(h->ctx, llama_batch_get_one(&tok, 1)) != 0) return -1.0;
+        const double b = now_s();
+        llama_synchronize(h->ctx);
+        const double c = now_s();
+        td += b - a;
+        ts += c - b;
+        tok = std::rand() % h->n_vocab;
+    }
+    *t_decode = td;
+    *t_sync = ts;
     return now_s() - t0;
 }
 
