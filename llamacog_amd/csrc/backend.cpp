@@ -441,9 +441,15 @@ static void mi_backend_synchronize(ggml_backend_t backend) {
 static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.qcache_clear();
     ex.done.clear();
+    ex.pend = exec_ctx::pending_pro();
+    ex.post_add = nullptr;
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) {
         i += op_compute(ex, cgraph, i);
+    }
+    if (ex.post_add) {   // a deferred in-place ADD with no later launch to carry it
+        op_binary(ex, ex.post_add);
+        ex.post_add = nullptr;
     }
 }
 

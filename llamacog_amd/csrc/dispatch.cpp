@@ -259,6 +259,66 @@ static bool overlaps_any(const ggml_tensor * t, const std::vector<const ggml_ten
     return false;
 }
 
+static bool f32c(const ggml_tensor * t) { return t && t->type == GGML_TYPE_F32 && ggml_is_contiguous(t); }
+
+// Defer a producer chain into the prologue of the GEMV of `mm` (its direct consumer, the next
+// node): kind 1 = [add] -> norm -> [mul], kind 2 = mul (a * b).  The chain's outputs must not
+// overlap its inputs (other workgroups of the consuming launch still read the inputs while
+// workgroup 0 writes the outputs).
+static bool defer_to_prologue(exec_ctx & ctx, int kind, ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul,
+                              const ggml_tensor * mm) {
+    // GGML_MI355X_NO_PROLOGUE: 1 = off, 2 = norm chains only, 3 = FFN products only,
+    // 4 = no deferred in-place ADD
+    static const int mode = getenv("GGML_MI355X_NO_PROLOGUE") ? atoi(getenv("GGML_MI355X_NO_PROLOGUE")) : 0;
+    if (mode == 1 || (mode == 2 && kind == 2) || (mode == 3 && kind == 1)) return false;
+    if (!mm || mm->op != GGML_OP_MUL_MAT || !gemv_prologue_ok(mm)) return false;
+    const ggml_tensor * last = mul ? mul : norm;
+    if (mm->src[1] != last) return false;
+    const int64_t K = last->ne[0];
+    if (ggml_nrows(last) != 1 || K != mm->src[0]->ne[0]) return false;
+    std::vector<const ggml_tensor *> ins, outs;
+    if (kind == 1) {
+        if (!f32c(norm) || !f32c(norm->src[0])) return false;
+        if (add) {
+            if (!f32c(add) || !f32c(add->src[0]) || !f32c(add->src[1]) || norm->src[0] != add) return false;
+            if (!ggml_are_same_shape(add->src[0], add->src[1]) || !ggml_are_same_shape(add, norm)) return false;
+            ins.push_back(add->src[0]); ins.push_back(add->src[1]); outs.push_back(add);
+        } else {
+            ins.push_back(norm->src[0]);
+        }
+        outs.push_back(norm);
+        if (mul) {
+            if (!f32c(mul) || !f32c(mul->src[1]) || ggml_nelements(mul->src[1]) != K) return false;
+            ins.push_back(mul->src[1]); outs.push_back(mul);
+        }
+    } else {
+        if (!f32c(mul) || !f32c(mul->src[0]) || !f32c(mul->src[1])) return false;
+        if (!ggml_are_same_shape(mul->src[0], mul->src[1]) || !ggml_are_same_shape(mul, mul->src[0])) return false;
+        ins.push_back(mul->src[0]); ins.push_back(mul->src[1]); outs.push_back(mul);
+    }
+    // an in-place ADD (its output over one of its inputs) is stored by the next launch
+    bool add_later = false;
+    for (const ggml_tensor * o : outs) {
+        for (const ggml_tensor * in : ins) {
+            if (!overlaps(o, in)) continue;
+            const bool allow = mode != 4 && !(mode == 5 && mm->src[0]->ne[1] != 4096) && !(mode == 6 && mm->src[0]->ne[1] == 4096);
+            if (allow && o == add && (in == add->src[0] || in == add->src[1]) && o->data == in->data) {
+                add_later = true;
+                continue;
+            }
+            return false;
+        }
+    }
+    for (const ggml_tensor * in : ins) {
+        if (((uintptr_t) in->data) % 16 != 0) return false;
+    }
+    ctx.pend.kind = kind;
+    ctx.pend.add = add; ctx.pend.norm = norm; ctx.pend.mul = mul;
+    ctx.pend.consumer = mm;
+    ctx.pend.add_later = add_later;
+    return true;
+}
+
 // decode mat-vec: launch node i together with up to two later MUL_MATs on the same src1
 // (Q/K/V, gate/up) in one grouped kernel, with fused epilogues: the SiLU that follows a
 // projection, the NORM-mode ROPE of a projection, and f16 KV-cache stores (CPY) of a
@@ -328,7 +388,41 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
         add_epilogues(nm, j);
         ++nm;
     }
+    ggml_tensor * add_later = nullptr;
+    if (ctx.pend.kind && ctx.pend.consumer == mm0) {
+        const auto pd = ctx.pend;
+        ctx.pend = exec_ctx::pending_pro();
+        // every workgroup reads the prologue inputs while the launch writes its outputs, and a
+        // deferred ADD reads them after the launch: no output of the launch may overlap them
+        // (ggml-alloc re-uses the memory of inputs whose last consumer, in graph order, ran)
+        std::vector<const ggml_tensor *> pins;
+        if (pd.kind == 1) {
+            if (pd.add) { pins.push_back(pd.add->src[0]); pins.push_back(pd.add->src[1]); }
+            else pins.push_back(pd.norm->src[0]);
+            if (pd.mul) pins.push_back(pd.mul->src[1]);
+        } else {
+            pins.push_back(pd.mul->src[0]); pins.push_back(pd.mul->src[1]);
+        }
+        bool clash = false;
+        for (const ggml_tensor * o : outs) {
+            for (const ggml_tensor * in : pins) clash = clash || overlaps(o, in);
+        }
+        if (!clash) {
+            epi.pro = pd.kind;
+            epi.pro_add = pd.add; epi.pro_norm = pd.norm; epi.pro_mul = pd.mul;
+            epi.pro_add_later = pd.add_later;
+            if (pd.add_later) add_later = pd.add;
+        } else if (pd.kind == 1) {
+            if (!fused_norm(ctx, pd.add, pd.norm, pd.mul, mm0)) {
+                if (pd.add) op_binary(ctx, pd.add);
+                op_rms_norm(ctx, pd.norm, pd.mul ? pd.mul->src[1] : nullptr, pd.mul);
+            }
+        } else if (!fused_mul_quant(ctx, pd.mul, mm0)) {
+            op_binary(ctx, pd.mul);
+        }
+    }
     gemv_group(ctx, mms, nm, &epi);
+    if (add_later) ctx.post_add = add_later;
     // node i+1 when it is node i's SiLU is consumed here; everything else is skipped later
     const bool next_absorbed = epi.silu[0] && epi.silu[0] == at(g, i + 1, n);
     for (const ggml_tensor * t : absorbed) {
@@ -372,6 +466,24 @@ static int op_rope_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
 
 int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
     ggml_tensor * node = ggml_graph_node(cgraph, i);
+    if (ctx.pend.kind && ctx.pend.consumer != node) {
+        // the deferred producer chain must run before anything else: do it stand-alone
+        const auto pd = ctx.pend;
+        ctx.pend = exec_ctx::pending_pro();
+        if (pd.kind == 1) {
+            if (!fused_norm(ctx, pd.add, pd.norm, pd.mul, nullptr)) {
+                if (pd.add) op_binary(ctx, pd.add);
+                op_rms_norm(ctx, pd.norm, pd.mul ? pd.mul->src[1] : nullptr, pd.mul);
+            }
+        } else if (!fused_mul_quant(ctx, pd.mul, nullptr)) {
+            op_binary(ctx, pd.mul);
+        }
+    }
+    if (ctx.post_add && !(node->op == GGML_OP_MUL_MAT && fusion_enabled() && gemv_supported(node) &&
+                          std::find(ctx.done.begin(), ctx.done.end(), node) == ctx.done.end())) {
+        op_binary(ctx, ctx.post_add);   // its inputs are untouched so far: store it now
+        ctx.post_add = nullptr;
+    }
     if (ggml_is_empty(node)) return 1;
     if (!ctx.done.empty()) {
         auto it = std::find(ctx.done.begin(), ctx.done.end(), node);
@@ -400,6 +512,9 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             // src/llama-graph.cpp:464-497); the norm output is still written, so other
             // readers of it stay correct.
             ggml_tensor * mul = norm_weight_mul(cgraph, i, n);
+            if (fusion_enabled() && defer_to_prologue(ctx, 1, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
+                return mul ? 2 : 1;
+            }
             if (fusion_enabled() && fused_norm(ctx, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
                 return mul ? 2 : 1;
             }
@@ -415,14 +530,19 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                 ggml_tensor * nx = at(cgraph, i + 1, n);
                 if (nx && nx->op == GGML_OP_RMS_NORM && nx->src[0] == node) {
                     ggml_tensor * mul = norm_weight_mul(cgraph, i + 1, n);
-                    if (fused_norm(ctx, node, nx, mul, at(cgraph, i + (mul ? 3 : 2), n))) return mul ? 3 : 2;
+                    const int used = mul ? 3 : 2;
+                    if (defer_to_prologue(ctx, 1, node, nx, mul, at(cgraph, i + used, n))) return used;
+                    if (fused_norm(ctx, node, nx, mul, at(cgraph, i + used, n))) return used;
                 }
             }
             op_binary(ctx, node);
             return 1;
         case GGML_OP_MUL:
             // gated-FFN product feeding the down projection: multiply + quantize in one pass
-            if (fusion_enabled() && fused_mul_quant(ctx, node, at(cgraph, i + 1, n))) return 1;
+            if (fusion_enabled()) {
+                if (defer_to_prologue(ctx, 2, nullptr, nullptr, node, at(cgraph, i + 1, n))) return 1;
+                if (fused_mul_quant(ctx, node, at(cgraph, i + 1, n))) return 1;
+            }
             op_binary(ctx, node);
             return 1;
         case GGML_OP_SUB:

@@ -9,6 +9,7 @@
 // there are few of them (decode).
 #include "ops.h"
 #include "rope.h"
+#include "quant_act.h"
 
 #include <cmath>
 
@@ -341,16 +342,21 @@ __global__ __launch_bounds__(256) void k_rms_norm(const char * __restrict__ x, t
     float * yr = (float *) (y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
     const int64_t ne0 = tx.ne[0];
     double sum = 0.0;
-    for (int64_t i = threadIdx.x; i < ne0; i += 256) {
-        const float v = xr[i];
-        sum += (double) (v * v);
-    }
+    if (tx.nb[0] == 4 && ne0 % 256 == 0 && ((uintptr_t) xr) % 16 == 0) {
+        // the canonical partition shared with the fused kernels (quant_act.h norm_sumsq)
+        sum = norm_sumsq(xr, nullptr, ne0, threadIdx.x & 63);
+    } else {
+        for (int64_t i = threadIdx.x; i < ne0; i += 256) {
+            const float v = xr[i];
+            sum += (double) (v * v);
+        }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
-    __shared__ double part[4];
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
-    __syncthreads();
-    sum = part[0] + part[1] + part[2] + part[3];
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
+        __shared__ double part[4];
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+        __syncthreads();
+        sum = part[0] + part[1] + part[2] + part[3];
+    }
     const float mean = (float) (sum / (double) ne0);
     const float scale = 1.0f / sqrtf(mean + eps);
     if (y2) {

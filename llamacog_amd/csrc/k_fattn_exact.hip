@@ -14,7 +14,7 @@
 //
 // MI355X structure: one workgroup per (q row, KV head) covers the G = H/Hkv query heads of
 // that head (GQA) so each K/V row is read once for all of them.  The cache is walked in
-// chunks of CH positions (CH*D*2 = 64 KiB of V):
+// chunks of CH positions (CH*D*2 = 64 KiB of K and of V, both staged in LDS):
 //   A. the chunk's mask is read first: the last unmasked position bounds all later work;
 //   0. V rows up to it are streamed HBM -> LDS with global_load_lds (dwordx4, async),
 //      overlapping phases 1-2;
@@ -37,31 +37,37 @@ __device__ __forceinline__ float f16r(float x) {
     return __half2float(__float2half_rn(x));
 }
 
+// lane l of a 16-lane DPP row reads lane l + N of the same row (0 past the row end)
+template <int N>
+__device__ __forceinline__ float row_shl(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x100 + N, 0xf, 0xf, true));
+}
+
 // ggml_vec_dot_f16 (AVX-512) of a K row with q (f16-rounded floats), computed by the 16
 // lanes of a lane group: lane l holds kv[m] = K[16m + l] and produces the lane-l partial of
 // the 16 x 4 accumulator layout (elements 64i + 16j + l, accumulators j = 0..3 FMA'd over
-// i), then the partials are summed in _mm512_reduce_add_ps's tree (8 / 4 / 2 / 1).  The
-// result is valid in lane l == 0.
+// i), then the partials are summed in _mm512_reduce_add_ps's tree (8 / 4 / 2 / 1).  qv[m]
+// is q[16m + l].  The result is valid in lane l == 0.
 template <int D>
-__device__ __forceinline__ float dot_f16_avx512_x16(const float (&kv)[D / 16], const float * q, int l) {
+__device__ __forceinline__ float dot_f16_avx512_x16(const float (&kv)[D / 16], const float (&qv)[D / 16]) {
     float acc4[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-        float acc = __fmul_rn(kv[jj], q[16 * jj + l]);
+        float acc = __fmul_rn(kv[jj], qv[jj]);
 #pragma unroll
-        for (int i = 1; i < D / 64; ++i) acc = fmaf(kv[4 * i + jj], q[64 * i + 16 * jj + l], acc);
+        for (int i = 1; i < D / 64; ++i) acc = fmaf(kv[4 * i + jj], qv[4 * i + jj], acc);
         acc4[jj] = acc;
     }
     float w = __fadd_rn(__fadd_rn(acc4[0], acc4[2]), __fadd_rn(acc4[1], acc4[3]));
-    w = __fadd_rn(w, __shfl_down(w, 8, 16));    // t3[i] = w[8+i] + w[i]
-    w = __fadd_rn(w, __shfl_down(w, 4, 16));    // t6[i] = t3[4+i] + t3[i]
-    w = __fadd_rn(w, __shfl_down(w, 2, 16));    // (t6[0]+t6[2]), (t6[1]+t6[3])
-    w = __fadd_rn(w, __shfl_down(w, 1, 16));
+    w = __fadd_rn(w, row_shl<8>(w));    // t3[i] = w[8+i] + w[i]
+    w = __fadd_rn(w, row_shl<4>(w));    // t6[i] = t3[4+i] + t3[i]
+    w = __fadd_rn(w, row_shl<2>(w));    // (t6[0]+t6[2]), (t6[1]+t6[3])
+    w = __fadd_rn(w, row_shl<1>(w));
     return w;
 }
 
 template <int D> struct fax_cfg {
-    static constexpr int CH = 32768 / D;                 // positions per chunk (64 KiB of f16 V)
+    static constexpr int CH = 32768 / D < 256 ? 32768 / D : 256;   // positions per chunk (<= 64 KiB of f16 K / V)
     static constexpr int RPP = 512 / D;                  // V rows per 1 KiB global_load_lds piece
     static constexpr int PER = CH >= 256 ? CH / 256 : 1; // positions per thread in phase 2
     static constexpr int TPD = 256 / D;                  // threads sharing one output dim d
@@ -83,7 +89,8 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
     const int nel = G * D;
 
     __shared__ __attribute__((aligned(16))) uint16_t vl[CH * D];   // V chunk, [pos][D] f16
-    __shared__ float qf[FAX_GMAX][D];
+    __shared__ __attribute__((aligned(16))) uint16_t kl[CH * D];   // K chunk, [pos][D] f16
+    __shared__ __attribute__((aligned(16))) float qt[FAX_GMAX][16][D / 16];   // q[g][16m + l] at [g][l][m]
     __shared__ float sc[FAX_GMAX][CH + U];   // scores -> vs coefficient (0 where masked)
     __shared__ float cm[FAX_GMAX][CH + U];   // ms coefficient (1 where masked)
     __shared__ float mk[CH + U];             // mask values of the chunk (-inf = skipped)
@@ -94,7 +101,7 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
     for (int i = tid; i < nel; i += 256) {
         const int g = i / D, d = i % D;
         const float * qrow = (const float *) (a.q + iq1 * a.nbq1 + (hk * G + g) * a.nbq2 + iq3 * a.nbq3);
-        qf[g][d] = f16r(qrow[d]);
+        qt[g][d % 16][d / 16] = f16r(qrow[d]);
     }
     if (tid < FAX_GMAX) mcarry[tid] = -INFINITY;
     if (tid < 2) lastj[tid] = -1;
@@ -126,9 +133,17 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
         __syncthreads();
         if (tid == 0) lastj[par ^ 1] = -1;   // the next chunk's slot (last read before this chunk)
         const int nrun = lastj[par] + 1;      // positions past the last unmasked one are skipped
-        // ---- phase 0: V rows [0, nrun) HBM -> LDS (async; waited on before phase 3) --------
+        // ---- phase 0: K rows [0, nrun) HBM -> LDS (all in flight at once, then waited on),
+        // then V rows [0, nrun) (async; waited on before phase 3, overlapping phases 1-2) ----
         {
             const int r_in = lane / (D / 8), col = lane % (D / 8);
+            for (int p = wave; p * C::RPP < nrun; p += 4) {
+                const int row = min(p * C::RPP + r_in, nrun - 1);
+                const char * src = kbase + (c0 + row) * a.nbk1 + col * 16;
+                __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (kl + p * 512), 16, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
             for (int p = wave; p * C::RPP < nrun; p += 4) {
                 const int row = min(p * C::RPP + r_in, nrun - 1);
                 const char * src = vbase + (c0 + row) * a.nbv1 + col * 16;
@@ -144,12 +159,15 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
             for (int j = tid >> 4; j < nrun; j += 16) {
                 const float mv = mk[j];           // uniform over the 16 lanes of a position
                 if (mv == -INFINITY) continue;
-                const char * krow = kbase + (c0 + j) * a.nbk1;
+                const uint16_t * krow = kl + j * D;
                 float kv[D / 16];
 #pragma unroll
-                for (int m = 0; m < D / 16; ++m) kv[m] = h2f(ld2(krow + 2 * (16 * m + l)));
+                for (int m = 0; m < D / 16; ++m) kv[m] = h2f(krow[16 * m + l]);
                 for (int g = 0; g < G; ++g) {
-                    const float w = dot_f16_avx512_x16<D>(kv, qf[g], l);
+                    float qv[D / 16];
+#pragma unroll
+                    for (int m = 0; m < D / 16; ++m) qv[m] = qt[g][l][m];
+                    const float w = dot_f16_avx512_x16<D>(kv, qv);
                     if (l == 0) {
                         float s = __fmul_rn(w, a.scale);
                         if (a.softcap != 0.0f) s = __fmul_rn(a.softcap, tanhf(s));
@@ -297,15 +315,15 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a, int64_t nq3) {
 // test hook: the K·Q scores exactly as phase 1 of k_fattn_exact computes them
 // (q [D] f32 is f16-rounded first), 16 lanes per cache row; D = 128
 __global__ void k_fattn_scores_d128(const float * q, const uint16_t * k, int64_t n, float * s) {
-    __shared__ float qf[128];
-    for (int i = threadIdx.x; i < 128; i += blockDim.x) qf[i] = f16r(q[i]);
-    __syncthreads();
     const int l = threadIdx.x & 15;
     const int64_t j = ((int64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    float kv[8];
+    float kv[8], qv[8];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) kv[m] = j < n ? h2f(k[j * 128 + 16 * m + l]) : 0.0f;
-    const float w = dot_f16_avx512_x16<128>(kv, qf, l);
+    for (int m = 0; m < 8; ++m) {
+        kv[m] = j < n ? h2f(k[j * 128 + 16 * m + l]) : 0.0f;
+        qv[m] = f16r(q[16 * m + l]);
+    }
+    const float w = dot_f16_avx512_x16<128>(kv, qv);
     if (l == 0 && j < n) s[j] = w;
 }
 

@@ -9,8 +9,9 @@
 //   MUL (silu(gate) * up) -> (MUL_MAT down)       k_mul_quant    (build_ffn LLM_FFN_PAR)
 //
 // Arithmetic: ADD/MUL are single f32 ops; RMS_NORM sums float(x*x) in double
-// (ops.cpp:3270-3316), scale = 1/sqrtf(float(sum/ne0)+eps), y = x*scale; quantizers are
-// quant_act.h's (bit-exact with the CPU).  All run with rows in registers: one 256-thread
+// (ops.cpp:3270-3316; the canonical partition of quant_act.h norm_sumsq), scale =
+// 1/sqrtf(float(sum/ne0)+eps), y = x*scale; quantizers are quant_act.h's (bit-exact with the
+// CPU's).  All run with rows in registers: one 256-thread
 // workgroup per row, each thread owning NV float4 slices (ne0 = 1024*NV).
 #include "ops.h"
 #include "quant_act.h"
@@ -44,24 +45,15 @@ __global__ __launch_bounds__(256) void k_norm_fused(const norm_fused_args p) {
             v[k].z = __fadd_rn(v[k].z, bb.z); v[k].w = __fadd_rn(v[k].w, bb.w);
         }
     }
+    // the canonical sum (quant_act.h norm_sumsq), identical to the GEMV prologue's; every
+    // wave computes it from memory, so the (possibly in-place) ADD output is stored only
+    // after all waves have read the inputs
+    const double sum = norm_sumsq(p.a + ro, p.b ? p.b + ro : nullptr, p.ne0, lane);
+    __syncthreads();
     if (p.xsum) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) *(float4 *) (p.xsum + ro + 4 * (tid + 256 * k)) = v[k];
     }
-    double sum = 0.0;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-        sum += (double) __fmul_rn(v[k].x, v[k].x);
-        sum += (double) __fmul_rn(v[k].y, v[k].y);
-        sum += (double) __fmul_rn(v[k].z, v[k].z);
-        sum += (double) __fmul_rn(v[k].w, v[k].w);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
-    __shared__ double part[4];
-    if (lane == 0) part[wave] = sum;
-    __syncthreads();
-    sum = part[0] + part[1] + part[2] + part[3];
     const float mean = (float) (sum / (double) p.ne0);
     const float scale = 1.0f / sqrtf(mean + p.eps);
 

@@ -19,6 +19,7 @@
 //     f16 KV cache (destination read from the dynamic-pointer table, exec_ctx::dyn_slot).
 #include "ops.h"
 #include "rope.h"
+#include "quant_act.h"
 
 namespace mi355x {
 
@@ -43,6 +44,16 @@ __device__ __forceinline__ void k4_scales_g(uint32_t s0, uint32_t s1, uint32_t s
 struct g_q4_K {
     static constexpr int per_block = 4, blk_bytes = 144;
     struct act { int a[16]; int bs0, bs1; float dy; };
+    // activation element of the k-th (0..63) value of task t, in act.a order
+    __device__ static int elem(int t, int k) { return 64 * t + k; }
+    // act from the task's 64 quantized values (4 per int, act order), its 16-sums, block scale
+    __device__ static void pack(act & x, const int (&q4)[16], const int (&g16)[4], float d) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x.a[i] = q4[i];
+        x.bs0 = g16[0] + g16[1];
+        x.bs1 = g16[2] + g16[3];
+        x.dy = d;
+    }
     __device__ static void load(const gemv_act & A, int t, act & x) {
         const int b = t >> 2, j = t & 3;
         const int4 * v = (const int4 *) (A.qs + b * 256 + 64 * j);
@@ -92,6 +103,8 @@ struct g_q4_K {
 struct g_q5_K {
     static constexpr int per_block = 4, blk_bytes = 176;
     using act = g_q4_K::act;
+    __device__ static int elem(int t, int k) { return g_q4_K::elem(t, k); }
+    __device__ static void pack(act & x, const int (&q4)[16], const int (&g16)[4], float d) { g_q4_K::pack(x, q4, g16, d); }
     __device__ static void load(const gemv_act & A, int t, act & x) { g_q4_K::load(A, t, x); }
     struct raw { uint4 hdr, ha, hb, qa, qb; };
     __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
@@ -134,6 +147,19 @@ struct g_q5_K {
 struct g_q6_K {
     static constexpr int per_block = 4, blk_bytes = 210;
     struct act { int4 a0, a1, a2, a3; int b0, b1, b2, b3; float dy; };
+    // task (b, h, lr): four groups of 16 at 256b + 128h + 16lr + 32g
+    __device__ static int elem(int t, int k) {
+        const int b = t >> 2, h = (t >> 1) & 1, lr = t & 1;
+        return 256 * b + 128 * h + 16 * lr + 32 * (k >> 4) + (k & 15);
+    }
+    __device__ static void pack(act & x, const int (&q4)[16], const int (&g16)[4], float d) {
+        x.a0 = make_int4(q4[0], q4[1], q4[2], q4[3]);
+        x.a1 = make_int4(q4[4], q4[5], q4[6], q4[7]);
+        x.a2 = make_int4(q4[8], q4[9], q4[10], q4[11]);
+        x.a3 = make_int4(q4[12], q4[13], q4[14], q4[15]);
+        x.b0 = 32 * g16[0]; x.b1 = 32 * g16[1]; x.b2 = 32 * g16[2]; x.b3 = 32 * g16[3];
+        x.dy = d;
+    }
     __device__ static void load(const gemv_act & A, int t, act & x) {
         const int b = t >> 2, h = (t >> 1) & 1, lr = t & 1;
         const int8_t * ap = A.qs + b * 256 + 128 * h + 16 * lr;
@@ -193,6 +219,9 @@ struct g_q6_K {
 struct g_q8_0 {
     static constexpr int per_block = 1, blk_bytes = 34;
     struct act { int4 a0, a1; float dy; };
+    static constexpr bool no_prologue = true;
+    __device__ static int elem(int, int) { return 0; }
+    __device__ static void pack(act &, const int (&)[16], const int (&)[4], float) {}
     __device__ static void load(const gemv_act & A, int t, act & x) {
         const int4 * ap = (const int4 *) (A.qs + (int64_t) t * 32);
         x.a0 = ap[0]; x.a1 = ap[1];
@@ -223,6 +252,9 @@ struct g_q8_0 {
 struct g_q4_0 {
     static constexpr int per_block = 1, blk_bytes = 18;
     struct act { int4 a0, a1; int s8; float dy; };
+    static constexpr bool no_prologue = true;
+    __device__ static int elem(int, int) { return 0; }
+    __device__ static void pack(act &, const int (&)[16], const int (&)[4], float) {}
     __device__ static void load(const gemv_act & A, int t, act & x) {
         const int4 * ap = (const int4 *) (A.qs + (int64_t) t * 32);
         x.a0 = ap[0]; x.a1 = ap[1];
@@ -275,7 +307,116 @@ struct gemv_args {
     rope_params rp;
     const int32_t * rope_pos; const float * rope_ff; int64_t rope_d;
     int need_pairs;
+    // activation prologue (instead of a separate producer kernel), K-quant weights, one wave
+    // covering a row's tasks per WPR group:
+    //   pro 1: x = pa (+ pb); y = rms_norm(x) (eps); yw = y * pw; act = Q8_K(yw)
+    //   pro 2: yw = pa * pb; act = Q8_K(yw)
+    // workgroup 0 also stores the graph nodes' outputs (o_add, o_norm, o_mul) and the Q8_K
+    // activation (cq, cd, cs) for later launches that share the input
+    int pro;
+    const float * pa; const float * pb; const float * pw; float eps; int64_t pk;
+    float * o_add; float * o_norm; float * o_mul;
+    int8_t * cq; float * cd; int16_t * cs;
+    // a deferred in-place ADD stored by workgroup 0 (x[i] = x[i] + y[i], n elements)
+    float * post_add; const float * post_b; int64_t post_n;
 };
+
+// the prologue: this lane's task activation, Q8_K-quantized across the 4 lanes of a block
+// (quantize_row_q8_K_ref: first index of max |x|, iscale = -127/max, min(127, rint), d = 1/iscale).
+// A task's 64 values are four runs of 16 contiguous elements (T::elem(t, 16g) .. +15), read as
+// float4 and kept in registers between the max and the quantization passes.
+template <class T>
+__device__ __forceinline__ void prologue_act(const gemv_args & p, int tt, int lane, bool writer, typename T::act & x) {
+    float scale = 1.0f;
+    if (p.pro == 1) {
+        const double s = norm_sumsq(p.pa, p.pb, p.pk, lane);
+        const float mean = (float) (s / (double) p.pk);
+        scale = 1.0f / sqrtf(mean + p.eps);
+    }
+    float v[64];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int base = T::elem(tt, 16 * g);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int e = base + 4 * c;
+            const float4 a4 = *(const float4 *) (p.pa + e);
+            float xa[4] = {a4.x, a4.y, a4.z, a4.w}, yn[4], yw[4];
+            if (p.pro == 1) {
+                if (p.pb) {
+                    const float4 b4 = *(const float4 *) (p.pb + e);
+                    xa[0] = __fadd_rn(xa[0], b4.x); xa[1] = __fadd_rn(xa[1], b4.y);
+                    xa[2] = __fadd_rn(xa[2], b4.z); xa[3] = __fadd_rn(xa[3], b4.w);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) yn[i] = __fmul_rn(xa[i], scale);
+                if (p.pw) {
+                    const float4 w4 = *(const float4 *) (p.pw + e);
+                    yw[0] = __fmul_rn(yn[0], w4.x); yw[1] = __fmul_rn(yn[1], w4.y);
+                    yw[2] = __fmul_rn(yn[2], w4.z); yw[3] = __fmul_rn(yn[3], w4.w);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) yw[i] = yn[i];
+                }
+                if (writer) {
+                    if (p.o_add) *(float4 *) (p.o_add + e) = make_float4(xa[0], xa[1], xa[2], xa[3]);
+                    if (p.o_norm) *(float4 *) (p.o_norm + e) = make_float4(yn[0], yn[1], yn[2], yn[3]);
+                    if (p.o_mul) *(float4 *) (p.o_mul + e) = make_float4(yw[0], yw[1], yw[2], yw[3]);
+                }
+            } else {
+                const float4 b4 = *(const float4 *) (p.pb + e);
+                yw[0] = __fmul_rn(xa[0], b4.x); yw[1] = __fmul_rn(xa[1], b4.y);
+                yw[2] = __fmul_rn(xa[2], b4.z); yw[3] = __fmul_rn(xa[3], b4.w);
+                if (writer) *(float4 *) (p.o_mul + e) = make_float4(yw[0], yw[1], yw[2], yw[3]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[16 * g + 4 * c + i] = yw[i];
+        }
+    }
+    // first max |v| of the task (element order = k order), then of the block (4 lanes,
+    // lowest element index on ties)
+    float amax = 0.0f, vmax = 0.0f;
+    int kmax = 64;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        const float ax = fabsf(v[k]);
+        if (ax > amax) { amax = ax; vmax = v[k]; kmax = k; }
+    }
+    int imax = kmax < 64 ? T::elem(tt, kmax) : 0x7fffffff;
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+        const float oa = __shfl_xor(amax, o, WAVE);
+        const float ov = __shfl_xor(vmax, o, WAVE);
+        const int   oi = __shfl_xor(imax, o, WAVE);
+        if (oa > amax || (oa == amax && oi < imax)) { amax = oa; vmax = ov; imax = oi; }
+    }
+    const float iscale = amax == 0.0f ? 0.0f : -127.0f / vmax;
+    const float d = amax == 0.0f ? 0.0f : 1.0f / iscale;
+    int q4[16], g16[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint32_t packed = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int k = 4 * i + c;
+            int iv = 0;
+            if (amax != 0.0f) {
+                iv = (int) rintf(__fmul_rn(iscale, v[k]));
+                iv = iv < 127 ? iv : 127;
+            }
+            g16[k >> 4] += iv;
+            packed |= (uint32_t) (iv & 0xff) << (8 * c);
+        }
+        q4[i] = (int) packed;
+        if (writer) *(uint32_t *) (p.cq + T::elem(tt, 4 * i)) = packed;
+    }
+    if (writer) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) p.cs[T::elem(tt, 16 * g) / 16] = (int16_t) g16[g];
+        if ((tt & 3) == 0) p.cd[T::elem(tt, 0) / 256] = d;
+    }
+    T::pack(x, q4, g16, d);
+}
 
 // epilogue of one output row; v = this row's sum, vp = the sum of its rope partner row^1
 __device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t M, int64_t row, float v, float vp) {
@@ -393,7 +534,11 @@ __global__ __launch_bounds__(256) void k_gemv_pipe(const gemv_args p, const int6
     const bool active = t < p.ntasks;
     const int tt = active ? t : 0;
     typename T::act x;
-    T::load(p.A, tt, x);
+    if (p.pro) prologue_act<T>(p, tt, lane, blockIdx.x == 0 && wave < WPR && active, x);
+    else T::load(p.A, tt, x);
+    if (p.post_add && blockIdx.x == 0) {
+        for (int64_t i = threadIdx.x; i < p.post_n; i += 256) p.post_add[i] = __fadd_rn(p.post_add[i], p.post_b[i]);
+    }
 
     auto locate = [&](int64_t g, int & mi, int64_t & row0) {
         mi = 0;
@@ -525,6 +670,7 @@ static void launch_t(hipStream_t st, gemv_args & a, int nmat) {
     int64_t Mt = 0;
     for (int i = 0; i < nmat; ++i) Mt += a.M[i];
     if (launch_pipe_t<T>(st, a, nmat, Mt)) return;
+    GGML_ASSERT(!a.pro && "mi355x: GEMV prologue needs the pipelined kernel");
     // WPR depends on K only, so a row's summation order (and its bits) is the same whether
     // the matrix is launched alone or grouped; R (rows per wave: activation reuse, loads in
     // flight) is then the largest that keeps >= 2048 waves on the chip
@@ -544,6 +690,7 @@ static void launch_t(hipStream_t st, gemv_args & a, int nmat) {
     }
 }
 
+
 static bool is_kq(ggml_type t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
 
 bool gemv_supported(const ggml_tensor * mm) {
@@ -560,6 +707,17 @@ bool gemv_supported(const ggml_tensor * mm) {
 
 bool gemv_epilogue_ok(const ggml_tensor * mm) { return gemv_supported(mm); }
 
+// prologue: K-quant weights, K a multiple of 256 with ntasks = K/64 <= 256 (the pipelined
+// kernel), every activation aligned for 16-byte loads
+bool gemv_prologue_ok(const ggml_tensor * mm) {
+    if (!gemv_supported(mm) || !is_kq(mm->src[0]->type)) return false;
+    const int64_t K = mm->src[0]->ne[0];
+    if (K % 256 != 0 || K / 64 > 4 * WAVE) return false;
+    static int pipe = -1;
+    if (pipe < 0) pipe = getenv("GGML_MI355X_GEMV_PIPE") ? atoi(getenv("GGML_MI355X_GEMV_PIPE")) : 1;
+    return pipe != 0;
+}
+
 // one launch for up to three MUL_MATs sharing src1 (all gemv_supported, same weight type
 // and K); silu[i] = optional SiLU output for matrix i
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi) {
@@ -574,11 +732,34 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
     if (ctx.timing) ctx.time_begin(TK_MMV, bytes, ev_beg);
 
     q8_act act;
-    if (!ctx.qcache_get(src1, kq, act)) {
+    gemv_args a = {};
+    const int pro = epi ? epi->pro : 0;
+    if (pro) {
+        GGML_ASSERT(kq && gemv_prologue_ok(mms[0]));
+        const int64_t K = src1->ne[0];
+        carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(K, 1, true)), K, 1, true);
+        a.pro = pro;
+        a.pk = K;
+        a.cq = act.qs; a.cd = act.d; a.cs = act.s;
+        if (pro == 1) {
+            const ggml_tensor * add = epi->pro_add;
+            const ggml_tensor * nrm = epi->pro_norm;
+            a.pa = add ? (const float *) add->src[0]->data : (const float *) nrm->src[0]->data;
+            a.pb = add ? (const float *) add->src[1]->data : nullptr;
+            a.o_add = add && !epi->pro_add_later ? (float *) add->data : nullptr;
+            a.o_norm = (float *) nrm->data;
+            memcpy(&a.eps, nrm->op_params, sizeof(float));
+            a.pw = epi->pro_mul ? (const float *) epi->pro_mul->src[1]->data : nullptr;
+            a.o_mul = epi->pro_mul ? (float *) epi->pro_mul->data : nullptr;
+        } else {
+            a.pa = (const float *) epi->pro_mul->src[0]->data;
+            a.pb = (const float *) epi->pro_mul->src[1]->data;
+            a.o_mul = (float *) epi->pro_mul->data;
+        }
+    } else if (!ctx.qcache_get(src1, kq, act)) {
         quantize_act(ctx, src1, kq, act, exec_ctx::QSLOT);
         ctx.qcache_put(src1, kq, act);
     }
-    gemv_args a = {};
     for (int i = 0; i < nmat; ++i) {
         const ggml_tensor * w = mms[i]->src[0];
         a.W[i] = (const uint8_t *) w->data;
@@ -599,6 +780,14 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         }
     }
     a.A = {act.qs, act.d, act.s};
+    if (ctx.post_add) {
+        ggml_tensor * ad = ctx.post_add;
+        // in place over src[0] or src[1]: x = out (aliasing one input), y = the other input
+        a.post_add = (float *) ad->data;
+        a.post_b = (const float *) (ad->src[0]->data == ad->data ? ad->src[1]->data : ad->src[0]->data);
+        a.post_n = ggml_nelements(ad);
+        ctx.post_add = nullptr;
+    }
     const int64_t nblk = src1->ne[0] / ggml_blck_size(wt);
     switch (wt) {
         case GGML_TYPE_Q4_K: a.ntasks = (int) (nblk * 4); launch_t<g_q4_K>(ctx.stream, a, nmat); break;
@@ -608,6 +797,7 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         case GGML_TYPE_Q4_0: a.ntasks = (int) nblk;       launch_t<g_q4_0>(ctx.stream, a, nmat); break;
         default: GGML_ABORT("mi355x: gemv type");
     }
+    if (pro) ctx.qcache_put(src1, true, act);   // written by workgroup 0 of this launch
     if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
 }
 

@@ -53,6 +53,17 @@ struct exec_ctx {
     // nodes already computed ahead of their position by a grouped launch (dispatch.cpp)
     std::vector<const ggml_tensor *> done;
 
+    // producer nodes deferred into the prologue of the next MUL_MAT's GEMV (dispatch.cpp)
+    struct pending_pro {
+        int kind = 0;                      // 0 none, 1 norm chain, 2 FFN product
+        ggml_tensor * add = nullptr; ggml_tensor * norm = nullptr; ggml_tensor * mul = nullptr;
+        const ggml_tensor * consumer = nullptr;
+        bool add_later = false;            // the ADD is in place: store it in the next launch
+    } pend;
+    // an in-place residual ADD whose inputs the previous GEMV prologue read: the next GEMV
+    // launch stores it (workgroup 0), before any node can read it
+    ggml_tensor * post_add = nullptr;
+
     // Dynamic destinations: a KV-cache store (CPY into a view at offset n_past) changes its
     // destination every token while the rest of the graph stays identical.  Kernels read
     // such pointers from a device table refreshed before each graph launch, so a captured
@@ -132,9 +143,15 @@ struct gemv_epi {
     void * const * f16out[3]   = {nullptr, nullptr, nullptr};   // dyn slot: f16 CPY of the output
     ggml_tensor *  rope[3]     = {nullptr, nullptr, nullptr};   // ROPE (NORM mode) of the output
     void * const * rope_f16[3] = {nullptr, nullptr, nullptr};   // dyn slot: f16 CPY of the rope
+    // activation prologue (k_gemv.hip prologue_act): 1 = [ADD] -> RMS_NORM -> [MUL w],
+    // 2 = MUL (gated-FFN product); the launch also writes these nodes' outputs
+    int pro = 0;
+    ggml_tensor * pro_add = nullptr; ggml_tensor * pro_norm = nullptr; ggml_tensor * pro_mul = nullptr;
+    bool pro_add_later = false;      // compute the ADD for the norm but do not store it
 };
 bool gemv_supported(const ggml_tensor * mm);
 bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
+bool gemv_prologue_ok(const ggml_tensor * mm);   // the consumer can run an activation prologue
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi);
 
 // lays out a q8_act (qs | d | s, 256-B aligned) in `base`

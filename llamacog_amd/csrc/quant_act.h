@@ -82,4 +82,37 @@ __device__ __forceinline__ void q8_0_wave(const float (&vv)[4], int lane, bool v
     }
 }
 
+// canonical RMS-norm sum of squares of x = a (+ b) [K], as every wave and the stand-alone
+// norm kernel (k_fused.hip) compute it: lane l sums elements [l*K/64, (l+1)*K/64) in double,
+// in order, then the 64 partials are combined by the xor-butterfly of wave_sum
+__device__ __forceinline__ double norm_sumsq(const float * a, const float * b, int64_t K, int lane) {
+    const int64_t n = K / 64;
+    const float * pa = a + lane * n;
+    const float * pb = b ? b + lane * n : nullptr;
+    double s = 0.0;
+    // batches of 8 float4 loads in flight (one L2 round trip per 32 elements, not per 4)
+    for (int64_t k0 = 0; k0 < n; k0 += 32) {
+        float4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = min(k0 + 4 * u, n - 4);
+            x[u] = *(const float4 *) (pa + k);
+            if (pb) {
+                const float4 y = *(const float4 *) (pb + k);
+                x[u].x = __fadd_rn(x[u].x, y.x); x[u].y = __fadd_rn(x[u].y, y.y);
+                x[u].z = __fadd_rn(x[u].z, y.z); x[u].w = __fadd_rn(x[u].w, y.w);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (k0 + 4 * u >= n) break;
+            s += (double) __fmul_rn(x[u].x, x[u].x);
+            s += (double) __fmul_rn(x[u].y, x[u].y);
+            s += (double) __fmul_rn(x[u].z, x[u].z);
+            s += (double) __fmul_rn(x[u].w, x[u].w);
+        }
+    }
+    return wave_sum(s);
+}
+
 }  // namespace mi355x
