@@ -1,17 +1,270 @@
-// k_mmq.hip — batched (prefill) quantized mat-mul on MFMA.  Placeholder gate: until the
-// MFMA tile kernel lands every MUL_MAT goes through the column-grouped mat-vec path.
+// k_mmq.hip — batched (prefill) quantized MUL_MAT on MFMA (v_mfma_i32_16x16x32_i8).
+//
+// Same arithmetic contract as the mat-vec path (k_mmv.hip / k_gemv.hip): the activations are
+// quantized to Q8_K with the CPU's quantizer, every integer sub-block dot product is exact,
+// and the per-block combination is (dw*dy)*sumi - (dmin*dy)*summ in fp32 — the formula of
+// ggml_vec_dot_q4_K_q8_K / _q6_K_q8_K (ggml-cpu/quants.c:514-722).  The integer dot of a
+// 32-element chunk of 16 weight rows x 16 tokens is one MFMA; the sub-block scales (6-bit
+// for Q4_K/Q5_K per 32, int8 for Q6_K per 16) are applied to the int32 MFMA results in VALU
+// (Q6_K: one MFMA per 16-element half, the other half's A lanes zeroed).
+//
+// Tiling (MI355X): a 256-thread workgroup owns 64 weight rows x 64 tokens; per 256-element
+// K block the 64 rows' quant blocks and the 64 tokens' Q8_K rows are streamed HBM -> LDS with
+// global_load_lds (16 B per lane, 1 KiB per wave instruction), the rows' scales are unpacked
+// once into LDS, then each wave computes 16 rows x 64 tokens (four 16x16 MFMA tiles sharing
+// the A fragment).  MFMA layouts (verified by tools/mfma_layout.hip): lane l holds
+// A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15]; C[row 4(l>>4)+i][col l&15].
 #include "ops.h"
 
 namespace mi355x {
 
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void * lds_ptr_t;
+
+constexpr int MQ_BM = 64, MQ_BN = 64;
+
+// ---- weight traits: raw block bytes, per-row scale unpack, A fragments -------------------
+// unpack(): per-row sub-scales sc[16] (int), mins mn[8] (int), d, dmin of one block.
+// afrag(blk, c, h): 8 int8 of 32-element chunk c (0..7), k = 8h .. 8h+7 (h = lane>>4).
+struct mq_q4_K {
+    static constexpr int BLK = 144, NSC = 8;   // NSC sub-blocks of 256/NSC elements
+    __device__ static void unpack(const uint8_t * b, int * sc, int * mn, float & d, float & dmin) {
+        d = h2f(ld2(b)); dmin = h2f(ld2(b + 2));
+        const uint8_t * q = b + 4;
+        for (int j = 0; j < 8; ++j) {
+            int s, m;
+            scale_min_k4(j, q, s, m);
+            sc[j] = s; mn[j] = m;
+        }
+    }
+    __device__ static long afrag(const uint8_t * b, int c, int h) {
+        // chunk c = 2g + hi: qs[32g + k] low (hi = 0) or high nibbles
+        const uint2 v = ld8(b + 16 + 32 * (c >> 1) + 8 * h);
+        const int sh = 4 * (c & 1);
+        const uint32_t lo = (v.x >> sh) & 0x0f0f0f0f, hi = (v.y >> sh) & 0x0f0f0f0f;
+        return (long) lo | ((long) hi << 32);
+    }
+};
+
+struct mq_q5_K {
+    static constexpr int BLK = 176, NSC = 8;
+    __device__ static void unpack(const uint8_t * b, int * sc, int * mn, float & d, float & dmin) {
+        mq_q4_K::unpack(b, sc, mn, d, dmin);
+    }
+    __device__ static long afrag(const uint8_t * b, int c, int h) {
+        const uint2 v = ld8(b + 48 + 32 * (c >> 1) + 8 * h);
+        const uint2 qh = ld8(b + 16 + 8 * h);   // qh[l] bit c is element 32c + l's 5th bit
+        const int sh = 4 * (c & 1);
+        const uint32_t lo = ((v.x >> sh) & 0x0f0f0f0f) | (((qh.x >> c) & 0x01010101) << 4);
+        const uint32_t hi = ((v.y >> sh) & 0x0f0f0f0f) | (((qh.y >> c) & 0x01010101) << 4);
+        return (long) lo | ((long) hi << 32);
+    }
+};
+
+struct mq_q6_K {
+    static constexpr int BLK = 210, NSC = 16;
+    __device__ static void unpack(const uint8_t * b, int * sc, int * mn, float & d, float & dmin) {
+        d = h2f(ld2(b + 208)); dmin = 0.0f;
+        for (int j = 0; j < 16; ++j) sc[j] = (int8_t) b[192 + j];
+        for (int j = 0; j < 8; ++j) mn[j] = 0;
+    }
+    __device__ static long afrag(const uint8_t * b, int c, int h) {
+        // element e = 32c + 8h + i: n = e/128, grp = (e%128)/32, l = e%32
+        const int n = c >> 2, grp = c & 3, l0 = 8 * h;
+        const uint2 ql = ld8(b + 64 * n + 32 * (grp & 1) + l0);
+        const uint2 qh = ld8(b + 128 + 32 * n + l0);
+        const int shl = 4 * (grp >> 1), shh = 2 * grp;
+        const uint32_t lo = ((ql.x >> shl) & 0x0f0f0f0f) | (((qh.x >> shh) & 0x03030303) << 4);
+        const uint32_t hi = ((ql.y >> shl) & 0x0f0f0f0f) | (((qh.y >> shh) & 0x03030303) << 4);
+        // q - 32 per byte (q in 0..63): q ^ 0x20 for q >= 32, and additionally | 0xc0 for q < 32
+        const uint32_t r0 = (lo ^ 0x20202020u) | (((~lo & 0x20202020u) >> 5) * 0xc0u);
+        const uint32_t r1 = (hi ^ 0x20202020u) | (((~hi & 0x20202020u) >> 5) * 0xc0u);
+        return (long) r0 | ((long) r1 << 32);
+    }
+};
+
+struct mmq_args {
+    const uint8_t * W; int64_t nb01; int64_t M; int64_t K; int64_t nblk;
+    const int8_t * xq; const float * xd; const int16_t * xs;   // Q8_K SoA: [T][K], [T][K/256], [T][K/16]
+    int64_t T;
+    float * dst; int64_t nb1;   // dst[t * nb1 + m*4]
+};
+
+template <class W>
+__global__ __launch_bounds__(256) void k_mmq(const mmq_args p) {
+    constexpr int RS = (W::BLK + 15) / 16 * 16;   // LDS row stride of the weight tile
+    __shared__ __attribute__((aligned(16))) uint8_t wq[MQ_BM * RS];
+    __shared__ __attribute__((aligned(16))) int8_t xq[MQ_BN * 256];
+    __shared__ int wsc[MQ_BM][W::NSC];
+    __shared__ int wmn[MQ_BM][8];
+    __shared__ float wd[MQ_BM], wdm[MQ_BM];
+    __shared__ float xd[MQ_BN];
+    __shared__ int xs[MQ_BN][8];   // Q8_K sums per 32-element chunk
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t row0 = (int64_t) blockIdx.x * MQ_BM;
+    const int64_t tok0 = (int64_t) blockIdx.y * MQ_BN;
+    const int h = lane >> 4, c16 = lane & 15;
+
+    float acc[4][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[n][i] = 0.0f;
+
+    for (int64_t b = 0; b < p.nblk; ++b) {
+        // ---- stage: weight blocks of the 64 rows (LDS row stride RS = BLK rounded up to 16 B;
+        // the last 16-byte read of a block runs into the next block or the buffer padding),
+        // Q8_K rows of the 64 tokens (LDS-DMA) ----------------------------------------------
+        constexpr int RC = (W::BLK + 15) / 16;     // 16-byte chunks per row
+        for (int c = tid; c < MQ_BM * RC; c += 256) {
+            const int r = c / RC, k = c % RC;
+            const int64_t row = min(row0 + r, p.M - 1);
+            const uint4 v = ld16(p.W + row * p.nb01 + b * W::BLK + 16 * k);
+            *(uint4 *) (wq + r * RS + 16 * k) = v;
+        }
+        for (int c0 = wave * 64; c0 < MQ_BN * 16; c0 += 256) {
+            const int c = c0 + lane;
+            const int t = c >> 4, part = c & 15;
+            const int64_t tok = min(tok0 + t, p.T - 1);
+            const int8_t * src = p.xq + tok * p.K + b * 256 + 16 * part;
+            __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (xq + 16 * c0), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // ---- per-row scales, per-token scale and chunk sums --------------------------------
+        if (tid < MQ_BM) {
+            int sc[16], mn[8];
+            float d, dmin;
+            W::unpack(wq + tid * RS, sc, mn, d, dmin);
+#pragma unroll
+            for (int j = 0; j < W::NSC; ++j) wsc[tid][j] = sc[j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wmn[tid][j] = mn[j];
+            wd[tid] = d; wdm[tid] = dmin;
+        } else if (tid < MQ_BM + MQ_BN) {
+            const int t = tid - MQ_BM;
+            const int64_t tok = min(tok0 + t, p.T - 1);
+            xd[t] = p.xd[tok * (p.K / 256) + b];
+            const int16_t * s16 = p.xs + tok * (p.K / 16) + b * 16;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xs[t][j] = s16[2 * j] + s16[2 * j + 1];
+        }
+        __syncthreads();
+        // ---- MFMA over the 8 chunks of 32 --------------------------------------------------
+        const int rA = 16 * wave + c16;            // A row of this lane
+        int sumi[4][4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sumi[n][i] = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const long a = W::afrag(wq + rA * RS, c, h);
+            if constexpr (W::NSC == 8) {
+                int scv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) scv[i] = wsc[16 * wave + 4 * h + i][c];
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 32 * c + 8 * h);
+                    v4i r = {0, 0, 0, 0};
+                    r = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, bf, r, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sumi[n][i] += r[i] * scv[i];
+                }
+            } else {
+                // two 16-element sub-blocks per chunk: lanes h < 2 hold the first, h >= 2 the second
+                const long a0 = h < 2 ? a : 0, a1 = h < 2 ? 0 : a;
+                int sc0[4], sc1[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    sc0[i] = wsc[16 * wave + 4 * h + i][2 * c];
+                    sc1[i] = wsc[16 * wave + 4 * h + i][2 * c + 1];
+                }
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 32 * c + 8 * h);
+                    v4i r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
+                    r0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, bf, r0, 0, 0, 0);
+                    r1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, bf, r1, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sumi[n][i] += r0[i] * sc0[i] + r1[i] * sc1[i];
+                }
+            }
+        }
+        // ---- block combination (fp32) --------------------------------------------------------
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = 16 * wave + 4 * h + i;
+            const float dw = wd[r], dmw = wdm[r];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int t = 16 * n + c16;
+                const float dy = xd[t];
+                if constexpr (W::NSC == 8) {
+                    int summ = 0;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) summ += wmn[r][j] * xs[t][j];
+                    acc[n][i] += (dw * dy) * (float) sumi[n][i] - (dmw * dy) * (float) summ;
+                } else {
+                    acc[n][i] += (dw * dy) * (float) sumi[n][i];
+                }
+            }
+        }
+        __syncthreads();   // the LDS tiles are refilled next block
+    }
+    // ---- store ----------------------------------------------------------------------------
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int64_t t = tok0 + 16 * n + c16;
+        if (t >= p.T) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t m = row0 + 16 * wave + 4 * h + i;
+            if (m < p.M) *(float *) ((char *) p.dst + t * p.nb1 + m * 4) = acc[n][i];
+        }
+    }
+}
+
+// ---- host --------------------------------------------------------------------------------------
 bool mmq_supported(const ggml_tensor * dst) {
-    (void) dst;
-    return false;
+    static const bool off = getenv("GGML_MI355X_NO_MMQ") && atoi(getenv("GGML_MI355X_NO_MMQ")) != 0;
+    if (off) return false;
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    if (w->type != GGML_TYPE_Q4_K && w->type != GGML_TYPE_Q5_K && w->type != GGML_TYPE_Q6_K) return false;
+    if (x->type != GGML_TYPE_F32 || dst->type != GGML_TYPE_F32) return false;
+    if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1) return false;
+    if (x->ne[1] < 16) return false;             // decode stays on the mat-vec path
+    if (w->ne[0] % 256 != 0 || x->nb[0] != 4 || dst->nb[0] != 4) return false;
+    return true;
 }
 
 void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
-    (void) ctx; (void) dst;
-    GGML_ABORT("mi355x: mmq not built");
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * x = dst->src[1];
+    hipEvent_t ev = nullptr;
+    const double flops = 2.0 * (double) w->ne[0] * (double) w->ne[1] * (double) x->ne[1];
+    if (ctx.timing) ctx.time_begin(TK_MMQ, flops, ev);
+    q8_act act;
+    if (!ctx.qcache_get(x, true, act)) {
+        quantize_act(ctx, x, true, act, exec_ctx::QSLOT);
+        ctx.qcache_put(x, true, act);
+    }
+    mmq_args p;
+    p.W = (const uint8_t *) w->data; p.nb01 = w->nb[1]; p.M = w->ne[1]; p.K = w->ne[0]; p.nblk = w->ne[0] / 256;
+    p.xq = act.qs; p.xd = act.d; p.xs = act.s;
+    p.T = x->ne[1];
+    p.dst = (float *) dst->data; p.nb1 = dst->nb[1];
+    const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(p.T, MQ_BN));
+    switch (w->type) {
+        case GGML_TYPE_Q4_K: hipLaunchKernelGGL(k_mmq<mq_q4_K>, grid, dim3(256), 0, ctx.stream, p); break;
+        case GGML_TYPE_Q5_K: hipLaunchKernelGGL(k_mmq<mq_q5_K>, grid, dim3(256), 0, ctx.stream, p); break;
+        case GGML_TYPE_Q6_K: hipLaunchKernelGGL(k_mmq<mq_q6_K>, grid, dim3(256), 0, ctx.stream, p); break;
+        default: GGML_ABORT("mi355x: mmq type");
+    }
+    if (ctx.timing) ctx.time_end(TK_MMQ, flops, ev);
 }
 
 }  // namespace mi355x

@@ -161,3 +161,21 @@ def test_flash_attn_f16_llama_shapes_vs_oracle(K, n_kv, n_q, Hkv, G):
     ref = O.flash_attn(q, k.view(np.uint8), v.view(np.uint8), m.view(np.uint16), O.F16, D, H, Hkv, n_kv, 1 / np.sqrt(D))
     same = (out.view(np.uint32) == ref.view(np.uint32)).mean()
     assert same > 0.99 and np.abs(out - ref).max() / np.abs(ref).max() < 2e-3, same
+
+
+@pytest.mark.parametrize("name,Kd,M", [("q4_K", 4096, 256), ("q5_K", 4096, 200), ("q6_K", 4096, 136),
+                                        ("q4_K", 14336, 128), ("q6_K", 14336, 64)])
+def test_mul_mat_prefill_mfma_vs_oracle(K, name, Kd, M):
+    """Batched MUL_MAT (T >= 16) on the MFMA int8 path (k_mmq.hip): exact integer sub-block
+    dots, fp32 block combination -> max |err| / max |ref| < 2e-6 like the mat-vec path."""
+    from llamacog_amd import gguf_synth as gs
+    t = {"q4_K": O.Q4_K, "q5_K": O.Q5_K, "q6_K": O.Q6_K}[name]
+    rng = np.random.default_rng(21)
+    blk, bs = gs.BLOCK[t]
+    wq = gs.make_blocks(t, M * Kd // blk, rng).reshape(M, -1)
+    for T in (16, 64, 100):
+        x = rng.standard_normal((T, Kd)).astype(np.float32)
+        y = K.mul_mat(t, wq, Kd, M, x)
+        ref = O.mul_mat(t, wq, Kd, M, x)
+        err = np.abs(y - ref).max() / np.abs(ref).max()
+        assert err < 2e-6, (name, T, err)
