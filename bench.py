@@ -28,6 +28,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+MFMA_I8_PEAK_TOPS = 2500.0   # dense int8 MFMA, no sparsity (MI355X_MICROARCH.md)
+# algorithmic work of one pp512 of Llama-3-8B: 2*6.98e9*512 layer matmuls +
+# output (last token) + attention
+PP512_FLOP = 7.22e12
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
 
 
 def parse():
@@ -160,6 +165,14 @@ def main():
     mv_ms, mv_bytes, mv_n = la.kernel_timing(plugin, 0)
     fa_ms, fa_bytes, fa_n = la.kernel_timing(plugin, 2)
     achieved = (mv_bytes / (mv_ms * 1e-3)) / 1e9 if mv_ms > 0 else None
+    # HBM bytes per GEMV launch from the PMC pass (rocprofv3 --pmc FETCH_SIZE, x2 gfx950
+    # correction), committed with its command under profiles/ (scripts/gpu_round_artifacts.sh)
+    traffic = None
+    if os.path.exists(TRAFFIC_FILE):
+        try:
+            traffic = json.load(open(TRAFFIC_FILE)).get("gemv_bytes_per_launch")
+        except Exception:
+            traffic = None
     wbytes = gguf_synth.weight_bytes_per_token(
         gguf_synth.ModelConfig(**{**cfg.__dict__, "n_layer": a.layers or cfg.n_layer}))
 
@@ -195,17 +208,23 @@ def main():
             },
             "pp_tok_s": round(pp_tps, 2) if pp_tps else None,
             "pp_tokens": a.pp,
+            "pp_roofline": ({"bound": "mfma", "unit": "TFLOP/s", "peak": MFMA_I8_PEAK_TOPS,
+                             "achieved": round(PP512_FLOP / (a.pp / pp_tps) / 1e12, 2),
+                             "frac": round(PP512_FLOP / (a.pp / pp_tps) / 1e12 / MFMA_I8_PEAK_TOPS, 4),
+                             "note": "whole pp512 (all kernels), Llama-3-8B algorithmic FLOPs"}
+                            if (pp_tps and a.pp == 512 and a.config == "llama3-8b-q4km" and not a.layers) else None),
             "weight_bytes_per_token": wbytes,
             "model_bw_GBs": round(wbytes * (a.steps / t_local) / 1e9, 1),
             "model_bw_frac_of_8TBs": round(wbytes * (a.steps / t_local) / 1e9 / HBM_PEAK_GBS, 4),
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_mmv_q (quantized mat-vec, all decode MUL_MATs)",
+                "kernel": "k_gemv_pipe (quantized decode GEMV, every decode MUL_MAT)",
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": "profiles/r01/pmc_traffic.json" if traffic else None,
                 "launches": mv_n,
                 "avg_launch_us": round(1e3 * mv_ms / mv_n, 3) if mv_n else None,
                 "algorithmic_bytes_per_launch": round(mv_bytes / mv_n) if mv_n else None,

@@ -92,6 +92,8 @@ void exec_ctx::free_scratch() {
     if (dyn_dev) (void) hipFree(dyn_dev);
     dyn_dev = nullptr;
     dyn_cap = 0;
+    if (fa_cnt) (void) hipFree(fa_cnt);
+    fa_cnt = nullptr;
 }
 
 hipEvent_t exec_ctx::get_event() {

@@ -5,6 +5,7 @@
 // layout (ggml.h:576-608) and runs exactly the launcher graph_compute would run for that
 // node, so tests exercise the product path without a ggml context or graph.
 #include "ops.h"
+#include "fattn.h"
 #include "../../include/ggml-mi355x.h"
 
 #include <cstring>
@@ -287,6 +288,54 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv(int wtype, int64_t K, int64
 //            positions of which the first b are unmasked (Llama-3-8B layout);
 //         1: fused residual ADD + RMS_NORM + MUL + Q8_K quantization of one row of a floats.
 // Returns the average device time per launch in microseconds.
+// streaming-read reference for the roofline: every byte of a buffer read once with 16-byte
+// loads, 8 in flight per lane, grid-stride over `grid` workgroups
+typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_stream_read(const v4u_t * __restrict__ p, int64_t n16, uint32_t * out) {
+    uint32_t acc = 0;
+    const int64_t stride = (int64_t) gridDim.x * 256;
+    int64_t i = (int64_t) blockIdx.x * 256 + threadIdx.x;
+    for (; i + 7 * stride < n16; i += 8 * stride) {
+        v4u_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    for (; i < n16; i += stride) { const v4u_t v = p[i]; acc ^= v.x ^ v.y ^ v.z ^ v.w; }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// the decode GEMV's q4_K access pattern without its arithmetic: a wave reads R = 4 rows of
+// 16 blocks x 144 B, lane t taking block t/4's 16-byte header and quant chunks 16+32j, 32+32j
+// (j = t%4) — three 16-byte loads per row; MODE 1 instead reads the same bytes as contiguous
+// 16-byte chunks (2304 B = 144 chunks: lane t takes chunks t, t+64 and t+128 < 144)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_pattern_read(const uint8_t * __restrict__ w, int64_t nrows, uint32_t * out) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row0 = ((int64_t) blockIdx.x * 4 + wave) * 4;
+    uint32_t acc = 0;
+    uint4 v[12];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint8_t * rp = w + min(row0 + r, nrows - 1) * 2304;
+        if (MODE == 0) {
+            const uint8_t * blk = rp + (lane >> 2) * 144;
+            const int j = lane & 3;
+            v[3 * r + 0] = ld16(blk);
+            v[3 * r + 1] = ld16(blk + 16 + 32 * j);
+            v[3 * r + 2] = ld16(blk + 32 + 32 * j);
+        } else {
+            v[3 * r + 0] = ld16(rp + 16 * lane);
+            v[3 * r + 1] = ld16(rp + 16 * (lane + 64));
+            v[3 * r + 2] = lane + 128 < 144 ? ld16(rp + 16 * (lane + 128)) : make_uint4(0, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 12; ++i) acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t b, int iters) {
     scoped_ctx sc(nullptr);
     hipEvent_t e0, e1;
@@ -302,7 +351,40 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
     };
     std::function<void()> run;
     ggml_tensor Q, K, V, Mk, O, X, R, A, N, Wt, Mu;
-    if (which == 0) {
+    unsigned long long * prof = nullptr;
+    if (which == 2) {
+        MI_CHECK(hipMalloc(&prof, 6 * sizeof(unsigned long long)));
+        MI_CHECK(hipMemset(prof, 0, 6 * sizeof(unsigned long long)));
+        g_fa_prof = prof;
+        which = 0;
+    }
+    if (which == 200 || which == 201) {
+        // q4_K-row access pattern (k_pattern_read) over a bytes (rows of 2304 B), b copies
+        const int64_t nrows = a / 2304, copies = std::max<int64_t>(1, b);
+        char * buf = (char *) dalloc((size_t) (nrows * 2304 * copies), 0x11);
+        uint32_t * o = (uint32_t *) dalloc(64, 0);
+        int64_t c = 0;
+        const int mode = which - 200;
+        run = [=, &sc]() mutable {
+            const uint8_t * p = (const uint8_t *) buf + (c % copies) * nrows * 2304;
+            const dim3 grid((unsigned) ceil_div(nrows, 16));
+            if (mode == 0) hipLaunchKernelGGL(k_pattern_read<0>, grid, dim3(256), 0, sc.ex.stream, p, nrows, o);
+            else           hipLaunchKernelGGL(k_pattern_read<1>, grid, dim3(256), 0, sc.ex.stream, p, nrows, o);
+            ++c;
+        };
+    } else if (which >= 100) {
+        // streaming read of a bytes per launch over b rotating copies, grid = which - 100 (x64)
+        const int64_t bytes = a, copies = std::max<int64_t>(1, b);
+        const int grid = (which - 100) * 64;
+        char * buf = (char *) dalloc((size_t) (bytes * copies), 0x11);
+        uint32_t * o = (uint32_t *) dalloc(64, 0);
+        int64_t c = 0;
+        run = [=, &sc]() mutable {
+            hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, sc.ex.stream,
+                               (const v4u_t *) (buf + (c % copies) * bytes), bytes / 16, o);
+            ++c;
+        };
+    } else if (which == 0) {
         const int64_t D = 128, H = 32, Hkv = 8, n_kv = a;
         float * q = (float *) dalloc(D * H * 4, 0x3c);
         void * k = dalloc(D * Hkv * n_kv * 2, 0x3c);
@@ -362,6 +444,16 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
     MI_CHECK(hipEventDestroy(e0));
     MI_CHECK(hipEventDestroy(e1));
     MI_CHECK(hipStreamSynchronize(sc.ex.stream));
+    if (prof) {
+        unsigned long long h[6];
+        MI_CHECK(hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost));
+        const char * nm[6] = {"A(mask)", "0(V issue)", "1(scores)", "2(softmax coef)", "3(wait V)", "3(recurrence)"};
+        fprintf(stderr, "FA phases (s_memtime ticks per launch, wg 0):");
+        for (int i = 0; i < 6; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double) h[i] / (iters + 3));
+        fprintf(stderr, "\n");
+        g_fa_prof = nullptr;
+        MI_CHECK(hipFree(prof));
+    }
     for (void * p : bufs) MI_CHECK(hipFree(p));
     return ms * 1000.0 / iters;
 }

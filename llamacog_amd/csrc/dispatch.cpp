@@ -8,6 +8,7 @@
 #include "ops.h"
 
 #include <algorithm>
+#include <cstdio>
 
 namespace mi355x {
 
@@ -235,6 +236,13 @@ static ggml_tensor * rope_of(ggml_cgraph * g, const ggml_tensor * mm, int p, int
     for (int k = p + 1; k < n && k <= p + 4; ++k) {
         ggml_tensor * r = ggml_graph_node(g, k);
         if (r->op != GGML_OP_ROPE) continue;
+        static const bool dbg = getenv("GGML_MI355X_DEBUG_FUSE") != nullptr;
+        if (dbg) {
+            const ggml_tensor * x = r->src[0];
+            fprintf(stderr, "[mi355x] rope cand %s: base_ok=%d data_ok=%d contig=%d/%d mode=%d ne=%lld,%lld,%lld n_dims=%d\n",
+                    r->name, base_of(x) == mm, x->data == mm->data, ggml_is_contiguous(x), ggml_is_contiguous(r),
+                    r->op_params[2], (long long) x->ne[0], (long long) x->ne[1], (long long) x->ne[2], r->op_params[1]);
+        }
         const ggml_tensor * x = r->src[0];
         if (base_of(x) != mm || x->data != mm->data || !ggml_is_contiguous(x) || !ggml_is_contiguous(r)) return nullptr;
         if (r->op_params[2] != 0 || r->type != GGML_TYPE_F32) return nullptr;   // NORM mode only
@@ -261,15 +269,46 @@ static bool overlaps_any(const ggml_tensor * t, const std::vector<const ggml_ten
 
 static bool f32c(const ggml_tensor * t) { return t && t->type == GGML_TYPE_F32 && ggml_is_contiguous(t); }
 
+static bool is_view_op(const ggml_tensor * t) {
+    return t->op == GGML_OP_NONE || t->op == GGML_OP_VIEW || t->op == GGML_OP_RESHAPE ||
+           t->op == GGML_OP_PERMUTE || t->op == GGML_OP_TRANSPOSE;
+}
+
+// Is the memory of `t` (produced before node `from`) never read again except by `allowed`
+// nodes (which this launch computes from registers), before a later node overwrites it?
+// ggml-alloc re-uses a tensor's memory once its last consumer has run, so the first later
+// node whose output overlaps `t` ends its life.  A graph output, or a tensor still live at
+// the end of the graph (a later split may read it), is never dead.
+static bool dead_after(ggml_cgraph * g, int n, int from, const ggml_tensor * t,
+                       const std::vector<const ggml_tensor *> & allowed) {
+    if (!t || (t->flags & GGML_TENSOR_FLAG_OUTPUT)) return false;
+    for (int k = from; k < n; ++k) {
+        const ggml_tensor * c = ggml_graph_node(g, k);
+        if (is_view_op(c)) continue;
+        const bool ok = std::find(allowed.begin(), allowed.end(), c) != allowed.end();
+        if (!ok) {
+            for (int s = 0; s < GGML_MAX_SRC; ++s) {
+                if (c->src[s] && overlaps(c->src[s], t)) return false;
+            }
+        }
+        if (overlaps(c, t)) return true;
+    }
+    return false;
+}
+
+
+
 // Defer a producer chain into the prologue of the GEMV of `mm` (its direct consumer, the next
 // node): kind 1 = [add] -> norm -> [mul], kind 2 = mul (a * b).  The chain's outputs must not
 // overlap its inputs (other workgroups of the consuming launch still read the inputs while
 // workgroup 0 writes the outputs).
-static bool defer_to_prologue(exec_ctx & ctx, int kind, ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul,
-                              const ggml_tensor * mm) {
-    // GGML_MI355X_NO_PROLOGUE: 1 = off, 2 = norm chains only, 3 = FFN products only,
-    // 4 = no deferred in-place ADD
-    static const int mode = getenv("GGML_MI355X_NO_PROLOGUE") ? atoi(getenv("GGML_MI355X_NO_PROLOGUE")) : 0;
+static bool defer_to_prologue(exec_ctx & ctx, ggml_cgraph * g, int n, int kind, ggml_tensor * add, ggml_tensor * norm,
+                              ggml_tensor * mul, const ggml_tensor * mm) {
+    // GGML_MI355X_NO_PROLOGUE: 0 = on, 1 = off (default: every workgroup re-reading the
+    // producer's inputs costs more than the separate fused producer kernel, measured on
+    // Llama-3-8B decode: 331 tok/s off vs 225 on), 2 = norm chains only, 3 = FFN products
+    // only, 4 = no deferred in-place ADD
+    static const int mode = getenv("GGML_MI355X_NO_PROLOGUE") ? atoi(getenv("GGML_MI355X_NO_PROLOGUE")) : 1;
     if (mode == 1 || (mode == 2 && kind == 2) || (mode == 3 && kind == 1)) return false;
     if (!mm || mm->op != GGML_OP_MUL_MAT || !gemv_prologue_ok(mm)) return false;
     const ggml_tensor * last = mul ? mul : norm;
@@ -296,6 +335,17 @@ static bool defer_to_prologue(exec_ctx & ctx, int kind, ggml_tensor * add, ggml_
         if (!ggml_are_same_shape(mul->src[0], mul->src[1]) || !ggml_are_same_shape(mul, mul->src[0])) return false;
         ins.push_back(mul->src[0]); ins.push_back(mul->src[1]); outs.push_back(mul);
     }
+    // the projections that will read the chain's activation in the consuming launch (those
+    // sharing src1 with mm, of its type and K): a chain output read by nothing else is never
+    // stored (dead_after), so it may share memory with the chain's inputs
+    std::vector<const ggml_tensor *> readers;
+    const int pm = node_index(g, mm);
+    for (int k = pm; k < n && k <= pm + 12; ++k) {
+        const ggml_tensor * c = ggml_graph_node(g, k);
+        if (c->op == GGML_OP_MUL_MAT && c->src[1] == last && c->src[0]->type == mm->src[0]->type &&
+            c->src[0]->ne[0] == K && gemv_supported(c)) readers.push_back(c);
+    }
+    bool need_norm = false, need_mul = false;
     // an in-place ADD (its output over one of its inputs) is stored by the next launch
     bool add_later = false;
     for (const ggml_tensor * o : outs) {
@@ -304,6 +354,11 @@ static bool defer_to_prologue(exec_ctx & ctx, int kind, ggml_tensor * add, ggml_
             const bool allow = mode != 4 && !(mode == 5 && mm->src[0]->ne[1] != 4096) && !(mode == 6 && mm->src[0]->ne[1] == 4096);
             if (allow && o == add && (in == add->src[0] || in == add->src[1]) && o->data == in->data) {
                 add_later = true;
+                continue;
+            }
+            if (o == norm && mul && dead_after(g, n, node_index(g, norm) + 1, norm, {mul})) { need_norm = true; continue; }
+            if (o == last && dead_after(g, n, node_index(g, last) + 1, last, readers)) {
+                if (o == norm) need_norm = true; else need_mul = true;
                 continue;
             }
             return false;
@@ -316,6 +371,8 @@ static bool defer_to_prologue(exec_ctx & ctx, int kind, ggml_tensor * add, ggml_
     ctx.pend.add = add; ctx.pend.norm = norm; ctx.pend.mul = mul;
     ctx.pend.consumer = mm;
     ctx.pend.add_later = add_later;
+    ctx.pend.need_elide_norm = need_norm;
+    ctx.pend.need_elide_mul = need_mul;
     return true;
 }
 
@@ -373,7 +430,20 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
             }
         }
     };
+    // a projection (or its rope) read only by this launch's register epilogues is not stored,
+    // and no longer constrains which other projections may join the launch
+    auto settle = [&](int m, int pm) {
+        if (dead_after(g, n, pm + 1, mms[m], absorbed)) {
+            epi.elide_dst[m] = true;
+            outs.erase(std::remove(outs.begin(), outs.end(), (const ggml_tensor *) mms[m]), outs.end());
+        }
+        if (epi.rope[m] && epi.rope_f16[m] && dead_after(g, n, node_index(g, epi.rope[m]) + 1, epi.rope[m], absorbed)) {
+            epi.elide_rope[m] = true;
+            outs.erase(std::remove(outs.begin(), outs.end(), (const ggml_tensor *) epi.rope[m]), outs.end());
+        }
+    };
     add_epilogues(0, i);
+    settle(0, i);
 
     for (int j = i + 1; j < n && j <= i + 12 && nm < 3; ++j) {
         ggml_tensor * c = ggml_graph_node(g, j);
@@ -381,11 +451,29 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
         if (std::find(ctx.done.begin(), ctx.done.end(), c) != ctx.done.end()) continue;
         if (c->src[0]->type != mm0->src[0]->type || c->src[0]->ne[0] != mm0->src[0]->ne[0]) continue;
         const ggml_tensor * o[1] = {c};
-        if (overlaps_any(c, outs) || !can_hoist(g, i, j, o, 1, absorbed)) continue;
+        if (overlaps_any(c, outs) || !can_hoist(g, i, j, o, 1, absorbed)) {
+            static const bool dbg = getenv("GGML_MI355X_DEBUG_FUSE") != nullptr;
+            if (dbg) {
+                fprintf(stderr, "[mi355x] group %s + %s rejected: overlap=%d hoist=%d", mm0->name, c->name,
+                        overlaps_any(c, outs), can_hoist(g, i, j, o, 1, absorbed));
+                for (const ggml_tensor * t : outs) if (overlaps(c, t)) fprintf(stderr, " [overlaps %s]", t->name);
+                for (int k = i + 1; k < j; ++k) {
+                    const ggml_tensor * t = ggml_graph_node(g, k);
+                    if (std::find(absorbed.begin(), absorbed.end(), t) != absorbed.end()) continue;
+                    bool hit = overlaps(c, t);
+                    for (int s2 = 0; s2 < GGML_MAX_SRC; ++s2) hit = hit || overlaps(c, t->src[s2]);
+                    if (hit && t->op != GGML_OP_VIEW && t->op != GGML_OP_RESHAPE && t->op != GGML_OP_PERMUTE &&
+                        t->op != GGML_OP_TRANSPOSE && t->op != GGML_OP_NONE) fprintf(stderr, " [hoist blocked by %s %s]", ggml_op_name(t->op), t->name);
+                }
+                fprintf(stderr, "\n");
+            }
+            continue;
+        }
         mms[nm] = c;
         absorbed.push_back(c);
         outs.push_back(c);
         add_epilogues(nm, j);
+        settle(nm, j);
         ++nm;
     }
     ggml_tensor * add_later = nullptr;
@@ -405,21 +493,57 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
         }
         bool clash = false;
         for (const ggml_tensor * o : outs) {
-            for (const ggml_tensor * in : pins) clash = clash || overlaps(o, in);
+            for (const ggml_tensor * in : pins) {
+                if (overlaps(o, in)) {
+                    clash = true;
+                    static const bool dbgc = getenv("GGML_MI355X_DEBUG_FUSE") != nullptr;
+                    if (dbgc) fprintf(stderr, "[mi355x] prologue of %s: output %s overlaps input %s\n", mm0->name, o->name, in->name);
+                }
+            }
         }
         if (!clash) {
             epi.pro = pd.kind;
             epi.pro_add = pd.add; epi.pro_norm = pd.norm; epi.pro_mul = pd.mul;
             epi.pro_add_later = pd.add_later;
             if (pd.add_later) add_later = pd.add;
-        } else if (pd.kind == 1) {
-            if (!fused_norm(ctx, pd.add, pd.norm, pd.mul, mm0)) {
-                if (pd.add) op_binary(ctx, pd.add);
-                op_rms_norm(ctx, pd.norm, pd.mul ? pd.mul->src[1] : nullptr, pd.mul);
+            // the chain's intermediates: the norm output is read by the MUL only, the
+            // activation by this launch's projections only (from the prologue's registers)
+            std::vector<const ggml_tensor *> users = absorbed;
+            users.push_back(mm0);
+            if (pd.kind == 1) {
+                std::vector<const ggml_tensor *> nu = pd.mul ? std::vector<const ggml_tensor *>{pd.mul} : users;
+                epi.elide_norm = dead_after(g, n, node_index(g, pd.norm) + 1, pd.norm, nu);
             }
-        } else if (!fused_mul_quant(ctx, pd.mul, mm0)) {
-            op_binary(ctx, pd.mul);
+            if (pd.mul) epi.elide_mul = dead_after(g, n, node_index(g, pd.mul) + 1, pd.mul, users);
+            // the deferral counted on outputs that the actual group cannot elide: run the
+            // chain on its own (its kernels are in-place safe)
+            if ((pd.need_elide_norm && !epi.elide_norm) || (pd.need_elide_mul && !epi.elide_mul)) {
+                clash = true;
+                epi.pro = 0; epi.pro_add = epi.pro_norm = epi.pro_mul = nullptr;
+                epi.pro_add_later = false; epi.elide_norm = epi.elide_mul = false;
+                add_later = nullptr;
+            }
         }
+        if (clash) {
+            if (pd.kind == 1) {
+                if (!fused_norm(ctx, pd.add, pd.norm, pd.mul, mm0)) {
+                    if (pd.add) op_binary(ctx, pd.add);
+                    op_rms_norm(ctx, pd.norm, pd.mul ? pd.mul->src[1] : nullptr, pd.mul);
+                }
+            } else if (!fused_mul_quant(ctx, pd.mul, mm0)) {
+                op_binary(ctx, pd.mul);
+            }
+        }
+    }
+    static const bool dbg = getenv("GGML_MI355X_DEBUG_FUSE") != nullptr;
+    if (dbg) {
+        fprintf(stderr, "[mi355x] gemv @%d %s: nmat=%d pro=%d elide_norm=%d elide_mul=%d", i, mm0->name, nm, epi.pro,
+                epi.elide_norm, epi.elide_mul);
+        for (int m = 0; m < nm; ++m) {
+            fprintf(stderr, " | %s silu=%d rope=%d rope_f16=%d f16=%d elide=%d/%d", mms[m]->name, epi.silu[m] != nullptr,
+                    epi.rope[m] != nullptr, epi.rope_f16[m] != nullptr, epi.f16out[m] != nullptr, epi.elide_dst[m], epi.elide_rope[m]);
+        }
+        fprintf(stderr, "\n");
     }
     gemv_group(ctx, mms, nm, &epi);
     if (add_later) ctx.post_add = add_later;
@@ -512,7 +636,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             // src/llama-graph.cpp:464-497); the norm output is still written, so other
             // readers of it stay correct.
             ggml_tensor * mul = norm_weight_mul(cgraph, i, n);
-            if (fusion_enabled() && defer_to_prologue(ctx, 1, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
+            if (fusion_enabled() && defer_to_prologue(ctx, cgraph, n, 1, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
                 return mul ? 2 : 1;
             }
             if (fusion_enabled() && fused_norm(ctx, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
@@ -531,7 +655,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                 if (nx && nx->op == GGML_OP_RMS_NORM && nx->src[0] == node) {
                     ggml_tensor * mul = norm_weight_mul(cgraph, i + 1, n);
                     const int used = mul ? 3 : 2;
-                    if (defer_to_prologue(ctx, 1, node, nx, mul, at(cgraph, i + used, n))) return used;
+                    if (defer_to_prologue(ctx, cgraph, n, 1, node, nx, mul, at(cgraph, i + used, n))) return used;
                     if (fused_norm(ctx, node, nx, mul, at(cgraph, i + used, n))) return used;
                 }
             }
@@ -540,7 +664,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
         case GGML_OP_MUL:
             // gated-FFN product feeding the down projection: multiply + quantize in one pass
             if (fusion_enabled()) {
-                if (defer_to_prologue(ctx, 2, nullptr, nullptr, node, at(cgraph, i + 1, n))) return 1;
+                if (defer_to_prologue(ctx, cgraph, n, 2, nullptr, nullptr, node, at(cgraph, i + 1, n))) return 1;
                 if (fused_mul_quant(ctx, node, at(cgraph, i + 1, n))) return 1;
             }
             op_binary(ctx, node);

@@ -22,9 +22,15 @@ struct fa_args {
     // qmode 0 none, 1 Q8_K, 2 Q8_0 over the flat [n_q][H*D] output rows
     int qmode;
     int8_t * qs; float * qd; int16_t * qsum;
+    // per-Q8_K-block arrival counters of the fused output quantization (zeroed, self-resetting)
+    int * cnt;
+    // microbenchmark hook: per-phase s_memtime cycles of workgroup (0,0) (nullable)
+    unsigned long long * prof;
 };
 
-constexpr int FAX_GMAX = 8;     // max query heads per KV head in the exact kernel
+// set by mi355x_bench_op (capi.cpp) only; copied into fa_args.prof
+extern unsigned long long * g_fa_prof;
+
 
 // launch the CPU-exact f16 kernel (k_fattn_exact.hip); D in {64, 128, 256}
 void launch_fattn_exact(hipStream_t stream, const fa_args & a, int64_t nq3);

@@ -19,6 +19,8 @@
 
 namespace mi355x {
 
+unsigned long long * g_fa_prof = nullptr;
+
 template <int EPL>  // elements of D per lane (D = 64*EPL)
 __global__ __launch_bounds__(256) void k_fattn_vec(const fa_args a) {
     constexpr int D = 64 * EPL;
@@ -269,6 +271,7 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     a.nchunks = (int) nchunks;
     a.part = nullptr;
     a.qmode = 0;
+    a.prof = g_fa_prof;
     a.qs = nullptr; a.qd = nullptr; a.qsum = nullptr;
     if (nchunks > 1) a.part = (float *) ctx.scratch(1, sizeof(float) * nchunks * rows * (a.D + 2));
 
@@ -276,18 +279,25 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     const double bytes = (double) (ggml_nbytes(k) + ggml_nbytes(v)) + (double) ggml_nbytes(q) + (double) ggml_nbytes(dst);
     if (ctx.timing) ctx.time_begin(TK_FATTN, bytes, ev);
     static const bool fast = getenv("GGML_MI355X_FA_FAST") != nullptr && atoi(getenv("GGML_MI355X_FA_FAST")) != 0;
-    if (!fast && a.k_type == GGML_TYPE_F16 && a.H / a.Hkv <= FAX_GMAX) {
+    a.cnt = nullptr;
+    if (!fast && a.k_type == GGML_TYPE_F16) {
         // fused quantization of the output for the next MUL_MAT (decode: one row)
         q8_act act;
         if (mm && a.n_q == 1 && nq3 == 1 && mmv_q_supported_type(mm->src[0]->type) &&
             mm->src[1]->ne[0] == a.H * a.D && ggml_nrows(mm->src[1]) == 1 && ggml_is_contiguous(dst)) {
             const ggml_type wt = mm->src[0]->type;
             const bool kq = wt == GGML_TYPE_Q4_K || wt == GGML_TYPE_Q5_K || wt == GGML_TYPE_Q6_K;
-            const int64_t G = a.H / a.Hkv;
-            if ((G * a.D) % (kq ? 256 : 32) == 0 && (a.H * a.D) % (kq ? 256 : 32) == 0) {
+            // Q8_K blocks span 256/D whole heads (D divides 256 or equals it); their
+            // workgroups meet on a counter (allocated outside any capture, zeroed once)
+            if (kq && !ctx.fa_cnt && !ctx.capturing) {
+                MI_CHECK(hipMalloc(&ctx.fa_cnt, exec_ctx::FA_CNT * sizeof(int)));
+                MI_CHECK(hipMemsetAsync(ctx.fa_cnt, 0, exec_ctx::FA_CNT * sizeof(int), ctx.stream));
+            }
+            if ((a.H * a.D) % (kq ? 256 : 32) == 0 && (!kq || (ctx.fa_cnt && (a.H * a.D) / 256 <= exec_ctx::FA_CNT))) {
                 carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(a.H * a.D, 1, kq)), a.H * a.D, 1, kq);
                 a.qmode = kq ? 1 : 2;
                 a.qs = act.qs; a.qd = act.d; a.qsum = act.s;
+                a.cnt = ctx.fa_cnt;
             }
         }
         launch_fattn_exact(ctx.stream, a, nq3);

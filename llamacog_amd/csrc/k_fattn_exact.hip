@@ -12,16 +12,23 @@
 //     vec_mad_f16 / vec_scale_f16 roundings (vec.h:262-290, 410-440): y = f16(fma(v,vs,y)),
 //     y = f16(y*ms); S = S*ms + vs (not contracted); expf taken in double and rounded.
 //
-// MI355X structure: one workgroup per (q row, KV head) covers the G = H/Hkv query heads of
-// that head (GQA) so each K/V row is read once for all of them.  The cache is walked in
-// chunks of CH positions (CH*D*2 = 64 KiB of K and of V, both staged in LDS):
-//   A. the chunk's mask is read first: the last unmasked position bounds all later work;
-//   0. V rows up to it are streamed HBM -> LDS with global_load_lds (dwordx4, async),
-//      overlapping phases 1-2;
-//   1. all scores in parallel (one position per thread, the K row held in VGPRs);
-//   2. per-head prefix max (wave scans) and the (ms, vs) coefficient of every position;
-//   3. the f16 recurrence — sequential over positions, parallel over the G*D elements, V
-//      read from LDS.  Each thread carries E independent chains to hide the dependency.
+// MI355X structure: one workgroup of 256 threads per (query row, query head) — 32 CUs busy
+// for a Llama-3-8B decode step rather than one per KV head.  The cache is walked in chunks
+// of CH positions:
+//   A. the chunk's mask; the last unmasked position (wave ballots) bounds all later work;
+//   0. V rows up to it are streamed HBM -> LDS with global_load_lds (async, overlapping 1-2);
+//   1. scores: 4 lanes per position (lane q holds the AVX-512 lane partials 4q..4q+3), K
+//      read straight from HBM with every load of the chunk in flight at once, q in VGPRs,
+//      the reduction tree across the quad by DPP quad_perm;
+//   2. prefix max over positions (wave scans) and the (ms, vs) coefficient of every
+//      position, plus a per-batch flag marking batches with a masked position or a max
+//      update;
+//   3. the f16 recurrence — sequential over positions, one chain per output dimension, V
+//      from LDS; a flagged-free batch is two dependent instructions per position
+//      (v_fma_mix_f32, v_cvt_f16_f32).
+// Output: O = y / S; optional Q8_0 / Q8_K quantization of the [H*D] row for the following
+// MUL_MAT: Q8_0 blocks lie inside one head; a Q8_K block spanning 256/D heads is quantized
+// by the last of its workgroups to finish (device-scope counter, self-resetting).
 #include "fattn.h"
 #include "quant_act.h"
 
@@ -43,292 +50,360 @@ __device__ __forceinline__ float row_shl(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x100 + N, 0xf, 0xf, true));
 }
 
-// ggml_vec_dot_f16 (AVX-512) of a K row with q (f16-rounded floats), computed by the 16
-// lanes of a lane group: lane l holds kv[m] = K[16m + l] and produces the lane-l partial of
-// the 16 x 4 accumulator layout (elements 64i + 16j + l, accumulators j = 0..3 FMA'd over
-// i), then the partials are summed in _mm512_reduce_add_ps's tree (8 / 4 / 2 / 1).  qv[m]
-// is q[16m + l].  The result is valid in lane l == 0.
-template <int D>
-__device__ __forceinline__ float dot_f16_avx512_x16(const float (&kv)[D / 16], const float (&qv)[D / 16]) {
-    float acc4[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-        float acc = __fmul_rn(kv[jj], qv[jj]);
-#pragma unroll
-        for (int i = 1; i < D / 64; ++i) acc = fmaf(kv[4 * i + jj], qv[4 * i + jj], acc);
-        acc4[jj] = acc;
-    }
-    float w = __fadd_rn(__fadd_rn(acc4[0], acc4[2]), __fadd_rn(acc4[1], acc4[3]));
-    w = __fadd_rn(w, row_shl<8>(w));    // t3[i] = w[8+i] + w[i]
-    w = __fadd_rn(w, row_shl<4>(w));    // t6[i] = t3[4+i] + t3[i]
-    w = __fadd_rn(w, row_shl<2>(w));    // (t6[0]+t6[2]), (t6[1]+t6[3])
-    w = __fadd_rn(w, row_shl<1>(w));
-    return w;
+// lane q of a quad reads lane (q | 2) / (q | 1): quad_perm [2,3,2,3] / [1,1,3,3]
+__device__ __forceinline__ float quad_from_plus2(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xEE, 0xf, 0xf, false));
 }
-
-template <int D> struct fax_cfg {
-    static constexpr int CH = 32768 / D < 256 ? 32768 / D : 256;   // positions per chunk (<= 64 KiB of f16 K / V)
-    static constexpr int RPP = 512 / D;                  // V rows per 1 KiB global_load_lds piece
-    static constexpr int PER = CH >= 256 ? CH / 256 : 1; // positions per thread in phase 2
-    static constexpr int TPD = 256 / D;                  // threads sharing one output dim d
-    static constexpr int U = 8;                          // phase-3 positions per register batch
-};
+__device__ __forceinline__ float quad_from_plus1(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xF5, 0xf, 0xf, false));
+}
 
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
-// E = query heads per thread in phase 3 (thread owns dim d = tid % D of heads tid/D + TPD*e)
-template <int D, int E>
+// one step of the f16 accumulation, y = f16(fma(v, vs, y)) with v and y as f16 bits in the low
+// halves: v_fma_mix_f32 converts both exactly and rounds the fma once to f32, v_cvt_f16_f32
+// rounds that to f16 — the CPU's cvtph_ps / fmadd_ps / cvtps_ph sequence, two dependent
+// instructions (written out so the compiler neither fuses the two roundings into
+// v_fma_mixlo_f16 nor re-packs y between steps)
+__device__ __forceinline__ uint32_t f16_mad(uint32_t vbits, float vs, uint32_t ybits) {
+    float t;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(vbits), "v"(vs), "v"(ybits));
+    uint32_t r;
+    asm("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
+// ggml_vec_dot_f16 (AVX-512) of a K row with q, computed by the 4 lanes of a quad.  Lane q
+// holds, for m < D/16, kh[m] = the 4 halves K[16m + 4q .. 16m + 4q + 3] and qf[m][c] =
+// q[16m + 4q + c] (f16-rounded): the AVX-512 lane partials l = 4q + c (accumulator j = m % 4
+// FMA'd over i = m / 4), REDUCE (x0+x2)+(x1+x3), then _mm512_reduce_add_ps's tree: t3[i] =
+// w[i] + w[8+i] (quad lanes 0,1 with 2,3), t6[i] = t3[i] + t3[4+i] (lane 0 with 1),
+// (t6[0]+t6[2]) + (t6[1]+t6[3]).  fp add is commutative, so only the association matters.
+// The result is valid in quad lane 0.
+template <int D>
+__device__ __forceinline__ float dot_f16_avx512_q4(const uint2 (&kh)[D / 16], const float (&qf)[D / 16][4]) {
+    float w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float acc[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const uint2 k0 = kh[jj];
+            const uint32_t h0 = (c < 2 ? k0.x : k0.y) >> (16 * (c & 1));
+            float a = __fmul_rn(h2f((uint16_t) h0), qf[jj][c]);
+#pragma unroll
+            for (int i = 1; i < D / 64; ++i) {
+                const uint2 ki = kh[4 * i + jj];
+                const uint32_t hi = (c < 2 ? ki.x : ki.y) >> (16 * (c & 1));
+                a = fmaf(h2f((uint16_t) hi), qf[4 * i + jj][c], a);
+            }
+            acc[jj] = a;
+        }
+        w[c] = __fadd_rn(__fadd_rn(acc[0], acc[2]), __fadd_rn(acc[1], acc[3]));
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = __fadd_rn(w[c], quad_from_plus2(w[c]));   // t3 (lanes 0, 1)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = __fadd_rn(w[c], quad_from_plus1(w[c]));   // t6 (lane 0)
+    return __fadd_rn(__fadd_rn(w[0], w[2]), __fadd_rn(w[1], w[3]));
+}
+
+template <int D> struct fax_cfg {
+    static constexpr int CH = D <= 128 ? 256 : 128;   // positions per chunk (V chunk <= 64 KiB)
+    static constexpr int NP = CH / 64;                // score passes per chunk (64 positions each)
+    static constexpr int RPP = 512 / D;               // V rows per 1 KiB global_load_lds piece
+    static constexpr int U = 16;                      // phase-3 positions per batch
+};
+
+template <int D>
 __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
     using C = fax_cfg<D>;
-    constexpr int CH = C::CH, U = C::U;
+    constexpr int CH = C::CH, U = C::U, NM = D / 16;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int qd = tid & 3;                 // lane in the quad of a position (phase 1)
     const int64_t iq1 = blockIdx.x;
-    const int64_t hk = blockIdx.y % a.Hkv;
-    const int64_t iq3 = blockIdx.y / a.Hkv;
-    const int G = (int) (a.H / a.Hkv);
-    const int nel = G * D;
+    const int64_t h = blockIdx.y % a.H;
+    const int64_t iq3 = blockIdx.y / a.H;
+    const int64_t hk = h / (a.H / a.Hkv);
 
     __shared__ __attribute__((aligned(16))) uint16_t vl[CH * D];   // V chunk, [pos][D] f16
-    __shared__ __attribute__((aligned(16))) uint16_t kl[CH * D];   // K chunk, [pos][D] f16
-    __shared__ __attribute__((aligned(16))) float qt[FAX_GMAX][16][D / 16];   // q[g][16m + l] at [g][l][m]
-    __shared__ float sc[FAX_GMAX][CH + U];   // scores -> vs coefficient (0 where masked)
-    __shared__ float cm[FAX_GMAX][CH + U];   // ms coefficient (1 where masked)
-    __shared__ float mk[CH + U];             // mask values of the chunk (-inf = skipped)
-    __shared__ float red[FAX_GMAX][4];
-    __shared__ float mcarry[FAX_GMAX];
-    __shared__ int lastj[2];
+    __shared__ float sc[CH + 3 * U];    // scores -> vs coefficient (0 where masked)
+    __shared__ float cm[CH + 3 * U];    // ms coefficient (1 where masked)
+    __shared__ float mk[CH + 3 * U];    // mask values of the chunk (-inf = skipped)
+    __shared__ uint32_t wflag[4];    // per wave: batches needing the general step (mask / max update)
+    __shared__ int wlast[4];
+    __shared__ float wmax[4];
 
-    for (int i = tid; i < nel; i += 256) {
-        const int g = i / D, d = i % D;
-        const float * qrow = (const float *) (a.q + iq1 * a.nbq1 + (hk * G + g) * a.nbq2 + iq3 * a.nbq3);
-        qt[g][d % 16][d / 16] = f16r(qrow[d]);
-    }
-    if (tid < FAX_GMAX) mcarry[tid] = -INFINITY;
-    if (tid < 2) lastj[tid] = -1;
-
-    // phase-3 state: dim d of heads gh[e]
-    const int d = tid % D;
-    float y[E], S[E];
-    int gh[E];
+    // q of this head, f16-rounded, in the quad layout of dot_f16_avx512_q4
+    float qf[NM][4];
+    {
+        const float * qrow = (const float *) (a.q + iq1 * a.nbq1 + h * a.nbq2 + iq3 * a.nbq3);
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-        y[e] = 0.0f; S[e] = 0.0f;
-        gh[e] = min(tid / D + C::TPD * e, G - 1);
+        for (int m = 0; m < NM; ++m) {
+            const float4 q4 = *(const float4 *) (qrow + 16 * m + 4 * qd);
+            qf[m][0] = f16r(q4.x); qf[m][1] = f16r(q4.y); qf[m][2] = f16r(q4.z); qf[m][3] = f16r(q4.w);
+        }
     }
+    const float slope = a.max_bias > 0.0f
+        ? (float) ((uint32_t) h < a.n_head_log2 ? pow((double) a.m0, (double) (h + 1))
+                                               : pow((double) a.m1, (double) (2 * ((uint32_t) h - a.n_head_log2) + 1)))
+        : 1.0f;
+
+    // phase-3 state: output dim d = tid (threads < D)
+    const int d = tid;
+    uint32_t yb = 0;   // f16 bits (low half)
+    float S = 0.0f;
+    float mcarry = -INFINITY;   // running max of the previous chunks (uniform)
 
     const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
     const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
     const char * mrow = a.mask ? a.mask + (iq1 % a.mask_ne1) * a.nbm1 : nullptr;
-    __syncthreads();
 
-    int par = 0;
-    for (int64_t c0 = 0; c0 < a.n_kv; c0 += CH, par ^= 1) {
+    const bool prof = a.prof && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0;
+    unsigned long long tp = prof ? __builtin_amdgcn_s_memtime() : 0, pc[6] = {0, 0, 0, 0, 0, 0};
+    auto mark = [&](int i) {
+        if (prof) { const unsigned long long t = __builtin_amdgcn_s_memtime(); pc[i] += t - tp; tp = t; }
+    };
+
+    for (int64_t c0 = 0; c0 < a.n_kv; c0 += CH) {
         const int nch = (int) min((int64_t) CH, a.n_kv - c0);
         // ---- phase A: mask of the chunk; the last unmasked position bounds all later work --
-        for (int j = tid; j < CH + U; j += 256) {
-            const float mv = j < nch ? (mrow ? h2f(*(const uint16_t *) (mrow + 2 * (c0 + j))) : 0.0f) : -INFINITY;
-            mk[j] = mv;
-            if (mv != -INFINITY) atomicMax(&lastj[par], j);
+        int last = -1;
+        for (int j0 = 0; j0 < CH + U; j0 += 256) {
+            const int j = j0 + tid;
+            float mv = -INFINITY;
+            if (j < nch) mv = mrow ? h2f(*(const uint16_t *) (mrow + 2 * (c0 + j))) : 0.0f;
+            if (j < CH + U) mk[j] = mv;
+            const unsigned long long b = __ballot(mv != -INFINITY);
+            if (b) last = j0 + 64 * wave + 63 - __clzll(b);
         }
+        if (lane == 0) wlast[wave] = last;
         __syncthreads();
-        if (tid == 0) lastj[par ^ 1] = -1;   // the next chunk's slot (last read before this chunk)
-        const int nrun = lastj[par] + 1;      // positions past the last unmasked one are skipped
-        // ---- phase 0: K rows [0, nrun) HBM -> LDS (all in flight at once, then waited on),
-        // then V rows [0, nrun) (async; waited on before phase 3, overlapping phases 1-2) ----
+        const int nrun = max(max(wlast[0], wlast[1]), max(wlast[2], wlast[3])) + 1;
+        mark(0);
+        if (nrun == 0) { __syncthreads(); continue; }   // whole chunk masked
+        // ---- phase 0: V rows [0, nrun) HBM -> LDS (async; waited on before phase 3) -------
         {
             const int r_in = lane / (D / 8), col = lane % (D / 8);
-            for (int p = wave; p * C::RPP < nrun; p += 4) {
-                const int row = min(p * C::RPP + r_in, nrun - 1);
-                const char * src = kbase + (c0 + row) * a.nbk1 + col * 16;
-                __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (kl + p * 512), 16, 0, 0);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
             for (int p = wave; p * C::RPP < nrun; p += 4) {
                 const int row = min(p * C::RPP + r_in, nrun - 1);
                 const char * src = vbase + (c0 + row) * a.nbv1 + col * 16;
                 __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (vl + p * 512), 16, 0, 0);
             }
         }
-        // ---- phase 1: scores, 16 lanes per position ----------------------------------------
-        // lane l of the 16 computes the AVX-512 lane-l partial of ggml_vec_dot_f16
-        // (accumulators j = 0..3 over i: elements 64i + 16j + l), then the 16 partials are
-        // summed in _mm512_reduce_add_ps's tree (8 / 4 / 2 / 1) across the lanes
+        mark(1);
+        // ---- phase 1: scores, 4 lanes per position, every K load of the chunk in flight ----
         {
-            const int l = tid & 15;
-            for (int j = tid >> 4; j < nrun; j += 16) {
-                const float mv = mk[j];           // uniform over the 16 lanes of a position
-                if (mv == -INFINITY) continue;
-                const uint16_t * krow = kl + j * D;
-                float kv[D / 16];
+            uint2 kh[C::NP][NM];
 #pragma unroll
-                for (int m = 0; m < D / 16; ++m) kv[m] = h2f(krow[16 * m + l]);
-                for (int g = 0; g < G; ++g) {
-                    float qv[D / 16];
+            for (int p = 0; p < C::NP; ++p) {
+                const int j = min(64 * p + (tid >> 2), nrun - 1);
+                const char * krow = kbase + (c0 + j) * a.nbk1 + 8 * qd;
 #pragma unroll
-                    for (int m = 0; m < D / 16; ++m) qv[m] = qt[g][l][m];
-                    const float w = dot_f16_avx512_x16<D>(kv, qv);
-                    if (l == 0) {
-                        float s = __fmul_rn(w, a.scale);
-                        if (a.softcap != 0.0f) s = __fmul_rn(a.softcap, tanhf(s));
-                        const uint32_t hh = (uint32_t) (hk * G + g);
-                        const float slope = a.max_bias > 0.0f
-                            ? (float) (hh < a.n_head_log2 ? pow((double) a.m0, (double) (hh + 1))
-                                                          : pow((double) a.m1, (double) (2 * (hh - a.n_head_log2) + 1))) : 1.0f;
-                        sc[g][j] = __fadd_rn(s, __fmul_rn(slope, mv));
-                    }
+                for (int m = 0; m < NM; ++m) {
+                    if (64 * p < nrun) kh[p][m] = ld8(krow + 32 * m);
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < C::NP; ++p) {
+                if (64 * p >= nrun) break;
+                const int j = 64 * p + (tid >> 2);
+                const float w = dot_f16_avx512_q4<D>(kh[p], qf);
+                if (qd == 0 && j < nrun) {
+                    float s = __fmul_rn(w, a.scale);
+                    if (a.softcap != 0.0f) s = __fmul_rn(a.softcap, tanhf(s));
+                    sc[j] = __fadd_rn(s, __fmul_rn(slope, mk[j]));
                 }
             }
         }
         __syncthreads();
-        // ---- phase 2: prefix max per head and the (ms, vs) coefficients --------------------
-        // masked positions (and the padding up to a multiple of U) get ms = 1, vs = 0
-        if (nrun > 0) {
-            for (int g = 0; g < G; ++g) {
-                float lm = -INFINITY;
+        mark(2);
+        // ---- phase 2: prefix max and the (ms, vs) coefficients (one position per thread) ---
+        {
+            const int j = tid;
+            const bool live = j < nrun && j < CH && mk[j] != -INFINITY;
+            const float sj = live ? sc[j] : -INFINITY;
+            float sm = sj;   // inclusive max-scan over the wave
 #pragma unroll
-                for (int p = 0; p < C::PER; ++p) {
-                    const int j = tid * C::PER + p;
-                    if (j < nrun && mk[j] != -INFINITY) lm = fmaxf(lm, sc[g][j]);
-                }
-                float sm = lm;   // inclusive max-scan over the 256 threads
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const float t = __shfl_up(sm, o, WAVE);
-                    if (lane >= o) sm = fmaxf(sm, t);
-                }
-                if (lane == 63) red[g][wave] = sm;
-                __syncthreads();
-                float prev = mcarry[g];
-                for (int w = 0; w < wave; ++w) prev = fmaxf(prev, red[g][w]);
-                const float ex = __shfl_up(sm, 1, WAVE);
-                if (lane > 0) prev = fmaxf(prev, ex);
-                float M = prev;
-#pragma unroll
-                for (int p = 0; p < C::PER; ++p) {
-                    const int j = tid * C::PER + p;
-                    if (j >= nrun) break;
-                    if (mk[j] == -INFINITY) { cm[g][j] = 1.0f; sc[g][j] = 0.0f; continue; }
-                    const float s = sc[g][j];
-                    if (s > M) {
-                        cm[g][j] = M == -INFINITY ? 0.0f : expf_cr(M - s);   // ms, applied before the add
-                        sc[g][j] = 1.0f;                                       // vs
-                        M = s;
+            for (int o = 1; o < 64; o <<= 1) {
+                const float t = __shfl_up(sm, o, WAVE);
+                if (lane >= o) sm = fmaxf(sm, t);
+            }
+            if (lane == 63) wmax[wave] = sm;
+            __syncthreads();
+            float M = mcarry;   // max over every position before j
+            for (int w = 0; w < wave; ++w) M = fmaxf(M, wmax[w]);
+            const float ex = __shfl_up(sm, 1, WAVE);
+            if (lane > 0) M = fmaxf(M, ex);
+            if (j < CH) {
+                if (j < nrun) {
+                    if (!live) {
+                        cm[j] = 1.0f; sc[j] = 0.0f;
+                    } else if (sj > M) {
+                        cm[j] = M == -INFINITY ? 0.0f : expf_cr(M - sj);   // ms, applied before the add
+                        sc[j] = 1.0f;                                       // vs
                     } else {
-                        cm[g][j] = 1.0f;
-                        sc[g][j] = expf_cr(s - M);
+                        cm[j] = 1.0f;
+                        sc[j] = expf_cr(sj - M);
                     }
                 }
-                if (tid < U) { cm[g][nrun + tid] = 1.0f; sc[g][nrun + tid] = 0.0f; }
-                __syncthreads();
-                if (tid == 255) mcarry[g] = fmaxf(mcarry[g], fmaxf(fmaxf(red[g][0], red[g][1]), fmaxf(red[g][2], red[g][3])));
             }
+            if (tid < U) { cm[nrun + tid] = 1.0f; sc[nrun + tid] = 0.0f; mk[nrun + tid] = -INFINITY; }
+            // batch flags: a masked position, a max update or padding inside the batch
+            const bool general = j < nrun ? (!live || sj > M) : (j < nrun + U);
+            const unsigned long long bw = __ballot(j < CH && general);
+            if (lane == 0) {
+                uint32_t f = 0;
+#pragma unroll
+                for (int b = 0; b < 64 / U; ++b) f |= ((bw >> (U * b)) & ((1ull << U) - 1)) ? 1u << b : 0u;
+                wflag[wave] = f;
+            }
+            mcarry = fmaxf(fmaxf(mcarry, fmaxf(wmax[0], wmax[1])), fmaxf(wmax[2], wmax[3]));
         }
+        mark(3);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        mark(4);
+        uint32_t bmask = 0;   // bit n: batch n takes the general step (uniform)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) bmask |= wflag[w] << ((64 / U) * w);
+        bmask = __builtin_amdgcn_readfirstlane(bmask);
         // ---- phase 3: sequential f16 recurrence (V from LDS) --------------------------------
-        // y = f16(y*ms) is the identity for ms == 1 (y is f16-exact), so it is applied at every
-        // position; masked / padded positions keep the state by a select (their V rows are
-        // not loaded, and -0 must survive)
-        if (tid < min(G, C::TPD) * D) {
-            for (int j = 0; j < nrun; j += U) {
-                uint16_t vv[U];
-                bool skip[U];
-                float msv[U][E], vsv[U][E];
+        // y = f16(y*ms) and S*ms only where the running max moved (ms != 1: y*1 and S*1 are
+        // identities); masked / padded positions keep the state (-0 must survive)
+        if (d < D) {
+            // batches of U positions, software-pipelined: batch n+1's V values and
+            // coefficients are read from LDS while batch n computes
+            // (a prefetch past the chunk end reads other LDS arrays or past the allocation, which
+            // reads as 0 — never used: batches at or past nrun do not run)
+            auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
+                const uint16_t * vp = vl + j * D + d;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    skip[u] = mk[j + u] == -INFINITY;
-                    vv[u] = vl[min(j + u, CH - 1) * D + d];
+                    vv[u] = vp[u * D];
+                    vs[u] = sc[j + u];
+                }
+            };
+            auto run = [&](int j, const uint32_t (&vv)[U], const float (&vs)[U]) {
+                if (((bmask >> (j / U)) & 1u) == 0) {
 #pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        msv[u][e] = cm[gh[e]][j + u];
-                        vsv[u][e] = sc[gh[e]][j + u];
+                    for (int u = 0; u < U; ++u) {
+                        yb = f16_mad(vv[u], vs[u], yb);
+                        S = __fadd_rn(S, vs[u]);   // not contracted on the CPU
                     }
+                    return;
                 }
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const float v = skip[u] ? 0.0f : h2f(vv[u]);
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        const float ms = msv[u][e];
-                        const float vs = vsv[u][e];
-                        const float yn = f16r(fmaf(v, vs, f16r(__fmul_rn(y[e], ms))));
-                        y[e] = skip[u] ? y[e] : yn;
-                        S[e] = __fadd_rn(__fmul_rn(S[e], ms), vs);   // identity where skipped; not contracted on the CPU
+                    if (__builtin_amdgcn_readfirstlane(__float_as_uint(mk[j + u])) == 0xff800000u) continue;
+                    const uint32_t msb = __builtin_amdgcn_readfirstlane(__float_as_uint(cm[j + u]));
+                    if (msb != 0x3f800000u) {
+                        const float ms = __uint_as_float(msb);
+                        float t = __fmul_rn(h2f((uint16_t) yb), ms);
+                        asm("" : "+v"(t));   // two roundings, as f16r
+                        yb = f2h(t);
+                        S = __fmul_rn(S, ms);
                     }
+                    yb = f16_mad(vv[u], vs[u], yb);
+                    S = __fadd_rn(S, vs[u]);
                 }
+            };
+            uint32_t va[U], vb[U];
+            float sa[U], sb[U];
+            ldb(0, va, sa);
+            for (int j = 0; j < nrun; j += 2 * U) {
+                ldb(j + U, vb, sb);
+                run(j, va, sa);
+                if (j + U >= nrun) break;
+                ldb(j + 2 * U, va, sa);
+                run(j + U, vb, sb);
             }
         }
         __syncthreads();
+        mark(5);
     }
-    float * ol = (float *) vl;   // output staging for the fused quantization (V chunk is dead)
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        const int g = tid / D + C::TPD * e;
-        if (g >= G) break;
-        const int64_t h = hk * G + g;
-        float * drow = (float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H + h * a.nb1_dst + iq3 * a.nb2_dst);
-        const float o = __fmul_rn(y[e], 1.0f / S[e]);
-        drow[d] = o;
-        if (a.qmode) ol[g * D + d] = o;
+    if (prof) {
+        for (int i = 0; i < 6; ++i) a.prof[i] += pc[i];
     }
-    if (a.qmode) {
-        // the G*D outputs of this KV head are a contiguous, 256-aligned slice of the flat
-        // [H*D] row the following MUL_MAT quantizes (checked on the host)
-        __syncthreads();
-        const int64_t K = a.H * D;
-        const int64_t c00 = hk * G * D;
-        for (int b = wave; b < nel / 256; b += 4) {
-            const float4 v4 = *(const float4 *) (ol + 256 * b + 4 * lane);
-            const float q[4] = {v4.x, v4.y, v4.z, v4.w};
-            const int64_t c0 = c00 + 256 * b;
-            if (a.qmode == 1) {
-                q8K_wave(q, lane, a.qs + iq1 * K + c0, a.qsum + iq1 * (K / 16) + c0 / 16, a.qd + iq1 * (K / 256) + c0 / 256);
-            } else {
-                q8_0_wave(q, lane, true, a.qs + iq1 * K + c0, a.qd + iq1 * (K / 32) + c0 / 32, a.qsum + iq1 * (K / 32) + c0 / 32);
-            }
-        }
-    }
-}
 
-template <int D>
-static void launch_d(hipStream_t st, const fa_args & a, dim3 grid) {
-    constexpr int TPD = 256 / D;
-    const int64_t per = ceil_div(a.H / a.Hkv, TPD);   // heads per thread
-    if (per <= 1)      hipLaunchKernelGGL((k_fattn_exact<D, 1>), grid, dim3(256), 0, st, a);
-    else if (per <= 2) hipLaunchKernelGGL((k_fattn_exact<D, 2>), grid, dim3(256), 0, st, a);
-    else if (per <= 4) hipLaunchKernelGGL((k_fattn_exact<D, 4>), grid, dim3(256), 0, st, a);
-    else               hipLaunchKernelGGL((k_fattn_exact<D, (D >= 256 ? 8 : 4)>), grid, dim3(256), 0, st, a);
+    // ---- output and its optional quantization ------------------------------------------------
+    float * drow = (float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H + h * a.nb1_dst + iq3 * a.nb2_dst);
+    const float o = d < D ? __fmul_rn(h2f((uint16_t) yb), 1.0f / S) : 0.0f;
+    if (d < D) drow[d] = o;
+    if (a.qmode == 2) {
+        // Q8_0: the head's D outputs are D/32 whole blocks of the flat [H*D] row
+        const int64_t K = a.H * D;
+        float * ol = (float *) sc;
+        __syncthreads();
+        if (d < D) ol[d] = o;
+        __syncthreads();
+        for (int b0 = 256 * wave; b0 < D; b0 += 1024) {
+            const bool valid = b0 + 4 * lane < D;
+            float q[4] = {0.f, 0.f, 0.f, 0.f};
+            if (valid) { const float4 v4 = *(const float4 *) (ol + b0 + 4 * lane); q[0] = v4.x; q[1] = v4.y; q[2] = v4.z; q[3] = v4.w; }
+            const int64_t c0 = h * D + b0;
+            q8_0_wave(q, lane, valid, a.qs + iq1 * K + c0, a.qd + iq1 * (K / 32) + c0 / 32, a.qsum + iq1 * (K / 32) + c0 / 32);
+        }
+    } else if (a.qmode == 1) {
+        // Q8_K: block b = 256 elements = NH heads; the last of its NH workgroups quantizes it
+        constexpr int NH = D >= 256 ? 1 : 256 / D;
+        const int64_t K = a.H * D;
+        const int64_t blk = (h * D) / 256;
+        __shared__ int is_last;
+        if (NH > 1) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __syncthreads();
+            if (tid == 0) {
+                const int prev = __hip_atomic_fetch_add(a.cnt + blk, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                is_last = prev == NH - 1;
+                if (is_last) __hip_atomic_store(a.cnt + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+        } else {
+            if (tid == 0) is_last = 1;
+            __syncthreads();
+        }
+        if (is_last && wave == 0) {
+            const float * brow = (const float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H) + 256 * blk;
+            float q[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) q[c] = __hip_atomic_load(brow + 4 * lane + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int64_t c0 = 256 * blk;
+            q8K_wave(q, lane, a.qs + iq1 * K + c0, a.qsum + iq1 * (K / 16) + c0 / 16, a.qd + iq1 * (K / 256) + c0 / 256);
+        }
+    }
 }
 
 void launch_fattn_exact(hipStream_t st, const fa_args & a, int64_t nq3) {
-    GGML_ASSERT(a.H % a.Hkv == 0 && a.H / a.Hkv <= FAX_GMAX);
-    const dim3 grid((unsigned) a.n_q, (unsigned) (a.Hkv * nq3));
+    GGML_ASSERT(a.H % a.Hkv == 0);
+    const dim3 grid((unsigned) a.n_q, (unsigned) (a.H * nq3));
     switch (a.D) {
-        case 64:  launch_d<64>(st, a, grid); break;
-        case 128: launch_d<128>(st, a, grid); break;
-        case 256: launch_d<256>(st, a, grid); break;
+        case 64:  hipLaunchKernelGGL(k_fattn_exact<64>, grid, dim3(256), 0, st, a); break;
+        case 128: hipLaunchKernelGGL(k_fattn_exact<128>, grid, dim3(256), 0, st, a); break;
+        case 256: hipLaunchKernelGGL(k_fattn_exact<256>, grid, dim3(256), 0, st, a); break;
         default: GGML_ABORT("mi355x: FA head size %d", (int) a.D);
     }
 }
 
 // test hook: the K·Q scores exactly as phase 1 of k_fattn_exact computes them
-// (q [D] f32 is f16-rounded first), 16 lanes per cache row; D = 128
+// (q [D] f32 is f16-rounded first), 4 lanes per cache row; D = 128
 __global__ void k_fattn_scores_d128(const float * q, const uint16_t * k, int64_t n, float * s) {
-    const int l = threadIdx.x & 15;
-    const int64_t j = ((int64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    float kv[8], qv[8];
+    const int qd = threadIdx.x & 3;
+    const int64_t j = ((int64_t) blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    uint2 kh[8];
+    float qf[8][4];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-        kv[m] = j < n ? h2f(k[j * 128 + 16 * m + l]) : 0.0f;
-        qv[m] = f16r(q[16 * m + l]);
+        kh[m] = j < n ? ld8(k + j * 128 + 16 * m + 4 * qd) : make_uint2(0, 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) qf[m][c] = f16r(q[16 * m + 4 * qd + c]);
     }
-    const float w = dot_f16_avx512_x16<128>(kv, qv);
-    if (l == 0 && j < n) s[j] = w;
+    const float w = dot_f16_avx512_q4<128>(kh, qf);
+    if (qd == 0 && j < n) s[j] = w;
 }
 
 void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int64_t n, float * s) {
-    hipLaunchKernelGGL(k_fattn_scores_d128, dim3((unsigned) ceil_div(n * 16, 256)), dim3(256), 0, st, q, k, n, s);
+    hipLaunchKernelGGL(k_fattn_scores_d128, dim3((unsigned) ceil_div(n * 4, 256)), dim3(256), 0, st, q, k, n, s);
 }
 
 }  // namespace mi355x

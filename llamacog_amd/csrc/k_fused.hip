@@ -11,8 +11,7 @@
 // Arithmetic: ADD/MUL are single f32 ops; RMS_NORM sums float(x*x) in double
 // (ops.cpp:3270-3316; the canonical partition of quant_act.h norm_sumsq), scale =
 // 1/sqrtf(float(sum/ne0)+eps), y = x*scale; quantizers are quant_act.h's (bit-exact with the
-// CPU's).  All run with rows in registers: one 256-thread
-// workgroup per row, each thread owning NV float4 slices (ne0 = 1024*NV).
+// CPU's).  All run with rows in registers.
 #include "ops.h"
 #include "quant_act.h"
 
@@ -29,37 +28,52 @@ struct norm_fused_args {
     int8_t * qs; float * qd; int16_t * qsum;
 };
 
+// one workgroup of BT = min(ne0/4, 1024) threads per row; thread t owns the float4s at
+// element 4 (t + BT k), k < NV, so wave w's 256 elements of slice k are the canonical
+// partition's j = w + (BT/64) k (quant_act.h norm_sumsq) and one Q8_K block / eight Q8_0
+// blocks of the quantized output.  The sum of squares is formed once per row: every thread
+// writes its (j, l) partials to LDS, wave 0 adds them in j order and butterflies.
 template <int NV>
-__global__ __launch_bounds__(256) void k_norm_fused(const norm_fused_args p) {
+__global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int BT = blockDim.x, NW = BT >> 6;
     const int64_t row = blockIdx.x;
     const int64_t ro = row * p.ne0;
+    __shared__ double qp[NV * 16][64];
+    __shared__ double tot;
     float4 v[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-        const int64_t e = 4 * (tid + 256 * k);
+        const int64_t e = 4 * (tid + BT * k);
         v[k] = *(const float4 *) (p.a + ro + e);
         if (p.b) {
             const float4 bb = *(const float4 *) (p.b + ro + e);
             v[k].x = __fadd_rn(v[k].x, bb.x); v[k].y = __fadd_rn(v[k].y, bb.y);
             v[k].z = __fadd_rn(v[k].z, bb.z); v[k].w = __fadd_rn(v[k].w, bb.w);
         }
+        qp[wave + NW * k][lane] = norm_q4(v[k]);
     }
-    // the canonical sum (quant_act.h norm_sumsq), identical to the GEMV prologue's; every
-    // wave computes it from memory, so the (possibly in-place) ADD output is stored only
-    // after all waves have read the inputs
-    const double sum = norm_sumsq(p.a + ro, p.b ? p.b + ro : nullptr, p.ne0, lane);
-    __syncthreads();
+    // each thread stores only elements it has itself read: in-place ADD output is safe
     if (p.xsum) {
 #pragma unroll
-        for (int k = 0; k < NV; ++k) *(float4 *) (p.xsum + ro + 4 * (tid + 256 * k)) = v[k];
+        for (int k = 0; k < NV; ++k) *(float4 *) (p.xsum + ro + 4 * (tid + BT * k)) = v[k];
     }
+    __syncthreads();
+    if (wave == 0) {
+        double s = 0.0;
+        const int nj = NW * NV;
+        for (int jj = 0; jj < nj; ++jj) s += qp[jj][lane];
+        s = wave_sum(s);
+        if (lane == 0) tot = s;
+    }
+    __syncthreads();
+    const double sum = tot;
     const float mean = (float) (sum / (double) p.ne0);
     const float scale = 1.0f / sqrtf(mean + p.eps);
 
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-        const int64_t e = 4 * (tid + 256 * k);
+        const int64_t e = 4 * (tid + BT * k);
         float4 y;
         y.x = __fmul_rn(v[k].x, scale); y.y = __fmul_rn(v[k].y, scale);
         y.z = __fmul_rn(v[k].z, scale); y.w = __fmul_rn(v[k].w, scale);
@@ -71,8 +85,7 @@ __global__ __launch_bounds__(256) void k_norm_fused(const norm_fused_args p) {
             *(float4 *) (p.yw + ro + e) = y;
         }
         const float q[4] = {y.x, y.y, y.z, y.w};
-        // the wave's 256 elements of slice k are one Q8_K block / eight Q8_0 blocks
-        const int64_t c0 = 1024 * k + 256 * wave;
+        const int64_t c0 = 4 * (int64_t) BT * k + 256 * wave;
         if (p.qmode == 1) {
             q8K_wave(q, lane, p.qs + ro + c0, p.qsum + row * (p.ne0 / 16) + c0 / 16, p.qd + row * (p.ne0 / 256) + c0 / 256);
         } else if (p.qmode == 2) {
@@ -126,7 +139,8 @@ static int consumer_qmode(const ggml_tensor * mm, const ggml_tensor * x) {
 
 bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm) {
     const int64_t ne0 = norm->ne[0];
-    if (ne0 % 1024 != 0 || ne0 > 8192) return false;
+    // ne0 <= 4096: one float4 per thread; above: whole 4096-element slices per 1024 threads
+    if (ne0 % 256 != 0 || (ne0 > 4096 && ne0 % 4096 != 0) || ne0 > 16384) return false;
     if (!f32_contig(norm) || !f32_contig(norm->src[0])) return false;
     if (add && (!f32_contig(add->src[0]) || !f32_contig(add->src[1]) || !ggml_are_same_shape(add->src[0], add->src[1]) ||
                 !ggml_are_same_shape(add, norm) || norm->src[0] != add)) return false;
@@ -154,15 +168,13 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     } else {
         p.qs = nullptr; p.qd = nullptr; p.qsum = nullptr;
     }
-    switch (ne0 / 1024) {
-        case 1: hipLaunchKernelGGL(k_norm_fused<1>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
-        case 2: hipLaunchKernelGGL(k_norm_fused<2>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
-        case 3: hipLaunchKernelGGL(k_norm_fused<3>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
-        case 4: hipLaunchKernelGGL(k_norm_fused<4>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
-        case 5: hipLaunchKernelGGL(k_norm_fused<5>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
-        case 6: hipLaunchKernelGGL(k_norm_fused<6>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
-        case 7: hipLaunchKernelGGL(k_norm_fused<7>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
-        default: hipLaunchKernelGGL(k_norm_fused<8>, dim3((unsigned) nrows), dim3(256), 0, ctx.stream, p); break;
+    const int nv = ne0 <= 4096 ? 1 : (int) (ne0 / 4096);
+    const dim3 block((unsigned) (ne0 / (4 * nv)));
+    switch (nv) {
+        case 1: hipLaunchKernelGGL(k_norm_fused<1>, dim3((unsigned) nrows), block, 0, ctx.stream, p); break;
+        case 2: hipLaunchKernelGGL(k_norm_fused<2>, dim3((unsigned) nrows), block, 0, ctx.stream, p); break;
+        case 3: hipLaunchKernelGGL(k_norm_fused<3>, dim3((unsigned) nrows), block, 0, ctx.stream, p); break;
+        default: hipLaunchKernelGGL(k_norm_fused<4>, dim3((unsigned) nrows), block, 0, ctx.stream, p); break;
     }
     if (qmode) ctx.qcache_put(out, qmode == 1, act);
     return true;

@@ -18,12 +18,44 @@
 //   * optional f16 epilogue: the V projection also performs the CPY of its output into the
 //     f16 KV cache (destination read from the dynamic-pointer table, exec_ctx::dyn_slot).
 #include "ops.h"
+#include <hip/hip_ext.h>
 #include "rope.h"
 #include "quant_act.h"
 
 namespace mi355x {
 
 struct gemv_act { const int8_t * qs; const float * d; const int16_t * s; };
+
+// weight loads: streamed once per token, so non-temporal (MI355X_MICROARCH.md, nt-weights:
+// once-read decode weights land sooner with the nt policy)
+#ifndef GEMV_NT
+#define GEMV_NT 0
+#endif
+typedef unsigned int gv4u __attribute__((ext_vector_type(4)));
+typedef unsigned int gv2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 wld16(const uint8_t * p) {
+#if GEMV_NT
+    const gv4u v = __builtin_nontemporal_load((const gv4u *) p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return ld16(p);
+#endif
+}
+__device__ __forceinline__ uint2 wld8(const uint8_t * p) {
+#if GEMV_NT
+    const gv2u v = __builtin_nontemporal_load((const gv2u *) p);
+    return make_uint2(v.x, v.y);
+#else
+    return ld8(p);
+#endif
+}
+__device__ __forceinline__ uint32_t wld2(const uint8_t * p) {
+#if GEMV_NT
+    return __builtin_nontemporal_load((const unsigned short *) p);
+#else
+    return ld2(p);
+#endif
+}
 
 // ---- per-type tasks: load(): activation slice of task t; dot(): that task's weight slice of
 // one row -> fp32 contribution (same formula as k_mmv.hip's tasks) ------------------------------
@@ -71,9 +103,9 @@ struct g_q4_K {
     __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const int b = t >> 2, j = t & 3;
         const uint8_t * blk = wrow + (int64_t) b * 144;
-        w.hdr = ld16(blk);
-        w.qa  = ld16(blk + 16 + 32 * j);
-        w.qb  = ld16(blk + 32 + 32 * j);
+        w.hdr = wld16(blk);
+        w.qa  = wld16(blk + 16 + 32 * j);
+        w.qb  = wld16(blk + 32 + 32 * j);
     }
     __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
         raw w;
@@ -110,11 +142,11 @@ struct g_q5_K {
     __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const int b = t >> 2, j = t & 3;
         const uint8_t * blk = wrow + (int64_t) b * 176;
-        w.hdr = ld16(blk);
-        w.ha  = ld16(blk + 16);
-        w.hb  = ld16(blk + 32);
-        w.qa  = ld16(blk + 48 + 32 * j);
-        w.qb  = ld16(blk + 64 + 32 * j);
+        w.hdr = wld16(blk);
+        w.ha  = wld16(blk + 16);
+        w.hb  = wld16(blk + 32);
+        w.qa  = wld16(blk + 48 + 32 * j);
+        w.qb  = wld16(blk + 64 + 32 * j);
     }
     __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
         raw w;
@@ -175,11 +207,11 @@ struct g_q6_K {
     __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const int b = t >> 2, h = (t >> 1) & 1, lr = t & 1;
         const uint8_t * blk = wrow + (int64_t) b * 210;
-        w.la = ld16(blk + 64 * h + 16 * lr);
-        w.lb = ld16(blk + 64 * h + 32 + 16 * lr);
-        w.hh = ld16(blk + 128 + 32 * h + 16 * lr);
-        w.sc8 = ld8(blk + 192 + 8 * h);
-        w.d16 = ld2(blk + 208);
+        w.la = wld16(blk + 64 * h + 16 * lr);
+        w.lb = wld16(blk + 64 * h + 32 + 16 * lr);
+        w.hh = wld16(blk + 128 + 32 * h + 16 * lr);
+        w.sc8 = wld8(blk + 192 + 8 * h);
+        w.d16 = wld2(blk + 208);
     }
     __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
         raw w;
@@ -230,9 +262,9 @@ struct g_q8_0 {
     struct raw { uint4 qa, qb; uint32_t d16; };
     __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const uint8_t * blk = wrow + (int64_t) t * 34;
-        w.d16 = ld2(blk);
-        w.qa = ld16(blk + 2);
-        w.qb = ld16(blk + 18);
+        w.d16 = wld2(blk);
+        w.qa = wld16(blk + 2);
+        w.qb = wld16(blk + 18);
     }
     __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
         raw w;
@@ -264,8 +296,8 @@ struct g_q4_0 {
     struct raw { uint4 q; uint32_t d16; };
     __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const uint8_t * blk = wrow + (int64_t) t * 18;
-        w.d16 = ld2(blk);
-        w.q = ld16(blk + 2);
+        w.d16 = wld2(blk);
+        w.q = wld16(blk + 2);
     }
     __device__ static float dot(const uint8_t * wrow, int t, const act & x) {
         raw r;
@@ -367,7 +399,7 @@ __device__ __forceinline__ void prologue_act(const gemv_args & p, int tt, int la
                 const float4 b4 = *(const float4 *) (p.pb + e);
                 yw[0] = __fmul_rn(xa[0], b4.x); yw[1] = __fmul_rn(xa[1], b4.y);
                 yw[2] = __fmul_rn(xa[2], b4.z); yw[3] = __fmul_rn(xa[3], b4.w);
-                if (writer) *(float4 *) (p.o_mul + e) = make_float4(yw[0], yw[1], yw[2], yw[3]);
+                if (writer && p.o_mul) *(float4 *) (p.o_mul + e) = make_float4(yw[0], yw[1], yw[2], yw[3]);
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[16 * g + 4 * c + i] = yw[i];
@@ -420,13 +452,13 @@ __device__ __forceinline__ void prologue_act(const gemv_args & p, int tt, int la
 
 // epilogue of one output row; v = this row's sum, vp = the sum of its rope partner row^1
 __device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t M, int64_t row, float v, float vp) {
-    p.dst[mi][row] = v;
+    if (p.dst[mi]) p.dst[mi][row] = v;
     if (p.f16out[mi]) (*p.f16out[mi])[row] = f2h(v);
     if (p.silu[mi]) {
         const int64_t nvec = (M / 16) * 16;
         p.silu[mi][row] = row < nvec ? v / (1.0f + v_expf_avx512(-v)) : v / (1.0f + expf_cr(-v));
     }
-    if (p.rope_out[mi]) {
+    if (p.rope_out[mi] || p.rope_f16[mi]) {
         const int64_t i0 = row % p.rope_d;
         float o = v;
         if (i0 < p.rp.n_dims) {
@@ -436,7 +468,7 @@ __device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t 
             rope_rotate(odd ? vp : v, odd ? v : vp, c, sn, o0, o1);
             o = odd ? o1 : o0;
         }
-        p.rope_out[mi][row] = o;
+        if (p.rope_out[mi]) p.rope_out[mi][row] = o;
         if (p.rope_f16[mi]) (*p.rope_f16[mi])[row] = f2h(o);
     }
 }
@@ -603,6 +635,11 @@ __global__ __launch_bounds__(256) void k_gemv_pipe(const gemv_args p, const int6
 }
 
 // ---- host ----------------------------------------------------------------------------------------
+// kernel-timing mode: the GEMV kernel itself is launched with start/stop events
+// (hipExtLaunchKernel records them at the dispatch's start and completion, without extra
+// marker packets around it), so bench.py's per-launch time is the kernel's own duration
+static thread_local hipEvent_t t_ev_beg = nullptr, t_ev_end = nullptr;
+
 static int g_gemv_lds = -1;   // GGML_MI355X_GEMV_LDS: 1 = stage weights through LDS
 
 template <class T, int R, int WPR>
@@ -622,9 +659,11 @@ static void launch_g(hipStream_t st, gemv_args & a, int nmat) {
     }
     const size_t slab = (size_t) RB * maxrow;
     if (g_gemv_lds && rows16 && slab <= 64 * 1024) {
-        hipLaunchKernelGGL((k_gemv<T, R, WPR, true>), dim3((unsigned) a.blk0[nmat]), dim3(256), slab, st, a);
+        hipExtLaunchKernelGGL((k_gemv<T, R, WPR, true>), dim3((unsigned) a.blk0[nmat]), dim3(256), (uint32_t) slab, st,
+                              t_ev_beg, t_ev_end, 0, a);
     } else {
-        hipLaunchKernelGGL((k_gemv<T, R, WPR, false>), dim3((unsigned) a.blk0[nmat]), dim3(256), 0, st, a);
+        hipExtLaunchKernelGGL((k_gemv<T, R, WPR, false>), dim3((unsigned) a.blk0[nmat]), dim3(256), 0, st,
+                              t_ev_beg, t_ev_end, 0, a);
     }
 }
 
@@ -639,7 +678,11 @@ static void launch_pipe(hipStream_t st, gemv_args & a, int nmat) {
     for (int i = nmat; i < GEMV_MAXMAT; ++i) a.blk0[i] = a.blk0[nmat];
     const int64_t ng = a.blk0[nmat];
     const int64_t grid = std::min<int64_t>(ng, g_gemv_wgs);
-    hipLaunchKernelGGL((k_gemv_pipe<T, R, WPR>), dim3((unsigned) grid), dim3(256), 0, st, a, ng);
+    if (t_ev_beg) {
+        hipExtLaunchKernelGGL((k_gemv_pipe<T, R, WPR>), dim3((unsigned) grid), dim3(256), 0, st, t_ev_beg, t_ev_end, 0, a, ng);
+    } else {
+        hipLaunchKernelGGL((k_gemv_pipe<T, R, WPR>), dim3((unsigned) grid), dim3(256), 0, st, a, ng);
+    }
 }
 
 template <class T>
@@ -725,11 +768,9 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
     const ggml_tensor * src1 = mms[0]->src[1];
     const ggml_type wt = mms[0]->src[0]->type;
     const bool kq = is_kq(wt);
-    hipEvent_t ev_beg = nullptr;
     double bytes = 0;
     for (int i = 0; i < nmat; ++i) bytes += (double) ggml_nbytes(mms[i]->src[0]) + (double) ggml_nbytes(mms[i]);
     bytes += (double) src1->ne[0] * (kq ? 1.14 : 1.0);
-    if (ctx.timing) ctx.time_begin(TK_MMV, bytes, ev_beg);
 
     q8_act act;
     gemv_args a = {};
@@ -747,14 +788,14 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
             a.pa = add ? (const float *) add->src[0]->data : (const float *) nrm->src[0]->data;
             a.pb = add ? (const float *) add->src[1]->data : nullptr;
             a.o_add = add && !epi->pro_add_later ? (float *) add->data : nullptr;
-            a.o_norm = (float *) nrm->data;
+            a.o_norm = epi->elide_norm ? nullptr : (float *) nrm->data;
             memcpy(&a.eps, nrm->op_params, sizeof(float));
             a.pw = epi->pro_mul ? (const float *) epi->pro_mul->src[1]->data : nullptr;
-            a.o_mul = epi->pro_mul ? (float *) epi->pro_mul->data : nullptr;
+            a.o_mul = epi->pro_mul && !epi->elide_mul ? (float *) epi->pro_mul->data : nullptr;
         } else {
             a.pa = (const float *) epi->pro_mul->src[0]->data;
             a.pb = (const float *) epi->pro_mul->src[1]->data;
-            a.o_mul = (float *) epi->pro_mul->data;
+            a.o_mul = epi->elide_mul ? nullptr : (float *) epi->pro_mul->data;
         }
     } else if (!ctx.qcache_get(src1, kq, act)) {
         quantize_act(ctx, src1, kq, act, exec_ctx::QSLOT);
@@ -765,12 +806,12 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         a.W[i] = (const uint8_t *) w->data;
         a.nb01[i] = w->nb[1];
         a.M[i] = w->ne[1];
-        a.dst[i] = (float *) mms[i]->data;
+        a.dst[i] = epi && epi->elide_dst[i] ? nullptr : (float *) mms[i]->data;
         a.silu[i] = epi && epi->silu[i] ? (float *) epi->silu[i]->data : nullptr;
         a.f16out[i] = epi ? (uint16_t * const *) epi->f16out[i] : nullptr;
-        a.rope_out[i] = epi && epi->rope[i] ? (float *) epi->rope[i]->data : nullptr;
+        a.rope_out[i] = epi && epi->rope[i] && !epi->elide_rope[i] ? (float *) epi->rope[i]->data : nullptr;
         a.rope_f16[i] = epi ? (uint16_t * const *) epi->rope_f16[i] : nullptr;
-        if (a.rope_out[i]) {
+        if (epi && epi->rope[i]) {
             const ggml_tensor * r = epi->rope[i];
             rope_params_of(r, a.rp);
             a.rope_pos = (const int32_t *) r->src[1]->data;
@@ -789,6 +830,10 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         ctx.post_add = nullptr;
     }
     const int64_t nblk = src1->ne[0] / ggml_blck_size(wt);
+    if (ctx.timing) {
+        t_ev_beg = ctx.get_event();
+        t_ev_end = ctx.get_event();
+    }
     switch (wt) {
         case GGML_TYPE_Q4_K: a.ntasks = (int) (nblk * 4); launch_t<g_q4_K>(ctx.stream, a, nmat); break;
         case GGML_TYPE_Q5_K: a.ntasks = (int) (nblk * 4); launch_t<g_q5_K>(ctx.stream, a, nmat); break;
@@ -798,7 +843,10 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         default: GGML_ABORT("mi355x: gemv type");
     }
     if (pro) ctx.qcache_put(src1, true, act);   // written by workgroup 0 of this launch
-    if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
+    if (ctx.timing) {
+        ctx.pending.push_back({t_ev_beg, t_ev_end, bytes, TK_MMV});
+        t_ev_beg = t_ev_end = nullptr;
+    }
 }
 
 }  // namespace mi355x

@@ -35,6 +35,10 @@ struct exec_ctx {
     size_t  slot_size[N_SLOTS] = {0, 0, 0, 0};
     bool    capturing = false;   // hipGraph capture in progress: growing is forbidden
 
+    // arrival counters of the flash-attention output quantization (k_fattn_exact.hip)
+    static constexpr int FA_CNT = 1024;
+    int *   fa_cnt = nullptr;
+
     void * scratch(int slot, size_t bytes);
     void   free_scratch();
 
@@ -59,6 +63,8 @@ struct exec_ctx {
         ggml_tensor * add = nullptr; ggml_tensor * norm = nullptr; ggml_tensor * mul = nullptr;
         const ggml_tensor * consumer = nullptr;
         bool add_later = false;            // the ADD is in place: store it in the next launch
+        bool need_elide_norm = false;      // deferral valid only if the launch elides these
+        bool need_elide_mul = false;
     } pend;
     // an in-place residual ADD whose inputs the previous GEMV prologue read: the next GEMV
     // launch stores it (workgroup 0), before any node can read it
@@ -143,6 +149,11 @@ struct gemv_epi {
     void * const * f16out[3]   = {nullptr, nullptr, nullptr};   // dyn slot: f16 CPY of the output
     ggml_tensor *  rope[3]     = {nullptr, nullptr, nullptr};   // ROPE (NORM mode) of the output
     void * const * rope_f16[3] = {nullptr, nullptr, nullptr};   // dyn slot: f16 CPY of the rope
+    // dead intermediates (read only by nodes this launch computes in registers, then
+    // overwritten): not stored
+    bool elide_dst[3]  = {false, false, false};   // the projection itself
+    bool elide_rope[3] = {false, false, false};   // its rope (kept only as the f16 cache row)
+    bool elide_norm = false, elide_mul = false;   // prologue RMS_NORM / MUL outputs
     // activation prologue (k_gemv.hip prologue_act): 1 = [ADD] -> RMS_NORM -> [MUL w],
     // 2 = MUL (gated-FFN product); the launch also writes these nodes' outputs
     int pro = 0;

@@ -82,34 +82,42 @@ __device__ __forceinline__ void q8_0_wave(const float (&vv)[4], int lane, bool v
     }
 }
 
-// canonical RMS-norm sum of squares of x = a (+ b) [K], as every wave and the stand-alone
-// norm kernel (k_fused.hip) compute it: lane l sums elements [l*K/64, (l+1)*K/64) in double,
-// in order, then the 64 partials are combined by the xor-butterfly of wave_sum
+// canonical RMS-norm sum of squares of x = a (+ b) [K] (K % 256 == 0), as every wave, the
+// stand-alone norm kernel and the fused norm kernel (k_fused.hip) compute it:
+//   q(j, l) = ((x[e]^2 + x[e+1]^2) + x[e+2]^2) + x[e+3]^2 in double, e = 256 j + 4 l
+//   s(l)    = q(0, l) + q(1, l) + ... in j order          (lane l of a wave)
+//   sum     = xor-butterfly of wave_sum over the 64 s(l)
+// Each float4 load of a wave covers 1 KiB of contiguous memory, and the (j, l) partials
+// can be formed by any thread holding that float4 (norm_q4), so a workgroup computes the
+// same value cooperatively.
+__device__ __forceinline__ double norm_q4(const float4 x) {
+    double q = (double) __fmul_rn(x.x, x.x);
+    q += (double) __fmul_rn(x.y, x.y);
+    q += (double) __fmul_rn(x.z, x.z);
+    q += (double) __fmul_rn(x.w, x.w);
+    return q;
+}
+
 __device__ __forceinline__ double norm_sumsq(const float * a, const float * b, int64_t K, int lane) {
-    const int64_t n = K / 64;
-    const float * pa = a + lane * n;
-    const float * pb = b ? b + lane * n : nullptr;
+    const int64_t n = K / 256;
     double s = 0.0;
-    // batches of 8 float4 loads in flight (one L2 round trip per 32 elements, not per 4)
-    for (int64_t k0 = 0; k0 < n; k0 += 32) {
+    // batches of 8 float4 loads in flight
+    for (int64_t j0 = 0; j0 < n; j0 += 8) {
         float4 x[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int64_t k = min(k0 + 4 * u, n - 4);
-            x[u] = *(const float4 *) (pa + k);
-            if (pb) {
-                const float4 y = *(const float4 *) (pb + k);
+            const int64_t e = 256 * min(j0 + u, n - 1) + 4 * lane;
+            x[u] = *(const float4 *) (a + e);
+            if (b) {
+                const float4 y = *(const float4 *) (b + e);
                 x[u].x = __fadd_rn(x[u].x, y.x); x[u].y = __fadd_rn(x[u].y, y.y);
                 x[u].z = __fadd_rn(x[u].z, y.z); x[u].w = __fadd_rn(x[u].w, y.w);
             }
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            if (k0 + 4 * u >= n) break;
-            s += (double) __fmul_rn(x[u].x, x[u].x);
-            s += (double) __fmul_rn(x[u].y, x[u].y);
-            s += (double) __fmul_rn(x[u].z, x[u].z);
-            s += (double) __fmul_rn(x[u].w, x[u].w);
+            if (j0 + u >= n) break;
+            s += norm_q4(x[u]);
         }
     }
     return wave_sum(s);
