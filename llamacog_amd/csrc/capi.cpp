@@ -230,7 +230,15 @@ GGML_BACKEND_API int mi355x_fa_scores_d128(const float * q, const uint16_t * k, 
 namespace mi355x {
 }
 
+extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int64_t M, int nmat, int copies, int iters, int epi_kind);
 extern "C" GGML_BACKEND_API double mi355x_bench_gemv(int wtype, int64_t K, int64_t M, int nmat, int copies, int iters) {
+    return mi355x_bench_gemv2(wtype, K, M, nmat, copies, iters, 0);
+}
+
+// epi_kind: 0 plain; 1 SiLU of matrix 0; 2 f16 (KV-cache) store of every matrix through a
+// dynamic-pointer slot; 3 NORM rope (Llama-3 parameters, head dim 128) of matrix 0 with its
+// f16 store; 4 activation prologue ADD -> RMS_NORM -> MUL (K-quants); 5 prologue MUL
+extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int64_t M, int nmat, int copies, int iters, int epi_kind) {
     const ggml_type t = (ggml_type) wtype;
     const size_t row = ggml_row_size(t, K);
     const size_t mat = row * (size_t) M;
@@ -260,12 +268,69 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv(int wtype, int64_t K, int64
         mms[m] = &Y[m];
     }
     if (!gemv_supported(mms[0])) return -1.0;
+    // epilogue / prologue operands
+    gemv_epi epi;
+    ggml_tensor S, Rt, P, A0, A1, Wn, Add, Nrm, Mul;
+    float * fbuf; uint16_t * hbuf; void ** slots; int32_t * pos;
+    MI_CHECK(hipMalloc(&fbuf, (M + 4 * K) * 4));
+    MI_CHECK(hipMalloc(&hbuf, M * 2 * nmat));
+    MI_CHECK(hipMalloc(&slots, 8 * nmat));
+    MI_CHECK(hipMalloc(&pos, 4));
+    MI_CHECK(hipMemset(fbuf, 0x3c, (M + 4 * K) * 4));
+    MI_CHECK(hipMemset(pos, 0, 4));
+    for (int m = 0; m < nmat; ++m) {
+        void * h = hbuf + m * M;
+        MI_CHECK(hipMemcpy(slots + m, &h, 8, hipMemcpyHostToDevice));
+    }
+    const int64_t nem[4] = {M, 1, 1, 1}, nek[4] = {K, 1, 1, 1};
+    if (epi_kind == 1) {
+        init_tensor(S, GGML_TYPE_F32, nem, fbuf);
+        epi.silu[0] = &S;
+    } else if (epi_kind == 2) {
+        for (int m = 0; m < nmat; ++m) epi.f16out[m] = (void * const *) (slots + m);
+    } else if (epi_kind == 3) {
+        const int64_t ner[4] = {128, M / 128, 1, 1}, nep[4] = {1, 1, 1, 1};
+        init_tensor(Rt, GGML_TYPE_F32, ner, fbuf);
+        init_tensor(P, GGML_TYPE_I32, nep, pos);
+        Rt.op = GGML_OP_ROPE;
+        Rt.src[0] = &Y[0];
+        Rt.src[1] = &P;
+        int32_t * op = Rt.op_params;
+        const float fb = 500000.0f, fs = 1.0f, ef = 0.0f, af = 1.0f, bf = 32.0f, bs = 1.0f;
+        op[1] = 128; op[2] = 0; op[4] = 8192;
+        memcpy(op + 5, &fb, 4); memcpy(op + 6, &fs, 4); memcpy(op + 7, &ef, 4);
+        memcpy(op + 8, &af, 4); memcpy(op + 9, &bf, 4); memcpy(op + 10, &bs, 4);
+        epi.rope[0] = &Rt;
+        epi.rope_f16[0] = (void * const *) slots;
+        epi.elide_rope[0] = true;
+    } else if (epi_kind == 4 || epi_kind == 5) {
+        init_tensor(A0, GGML_TYPE_F32, nek, fbuf + M);
+        init_tensor(A1, GGML_TYPE_F32, nek, fbuf + M + K);
+        init_tensor(Wn, GGML_TYPE_F32, nek, fbuf + M + 2 * K);
+        init_tensor(Add, GGML_TYPE_F32, nek, fbuf + M + 3 * K);
+        init_tensor(Nrm, GGML_TYPE_F32, nek, fbuf + M + 3 * K);
+        init_tensor(Mul, GGML_TYPE_F32, nek, x);
+        if (epi_kind == 4) {
+            Add.op = GGML_OP_ADD; Add.src[0] = &A0; Add.src[1] = &A1;
+            Nrm.op = GGML_OP_RMS_NORM; Nrm.src[0] = &Add;
+            const float eps = 1e-5f;
+            memcpy(Nrm.op_params, &eps, 4);
+            Mul.op = GGML_OP_MUL; Mul.src[0] = &Nrm; Mul.src[1] = &Wn;
+            epi.pro = 1; epi.pro_add = &Add; epi.pro_norm = &Nrm; epi.pro_mul = &Mul;
+            epi.elide_norm = true;
+        } else {
+            Mul.op = GGML_OP_MUL; Mul.src[0] = &A0; Mul.src[1] = &A1;
+            epi.pro = 2; epi.pro_mul = &Mul;
+        }
+        epi.elide_mul = true;
+        if (!gemv_prologue_ok(mms[0])) return -2.0;
+    }
     hipEvent_t e0, e1;
     MI_CHECK(hipEventCreate(&e0));
     MI_CHECK(hipEventCreate(&e1));
     auto run = [&](int it) {
         for (int m = 0; m < nmat; ++m) W[m].data = pool[(size_t) (it % copies) * nmat + m];
-        gemv_group(sc.ex, mms.data(), nmat, nullptr);
+        gemv_group(sc.ex, mms.data(), nmat, epi_kind ? &epi : nullptr);
     };
     run(0);   // quantizes X into the cache; later launches reuse it
     for (int i = 1; i < 4; ++i) run(i);
@@ -280,6 +345,7 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv(int wtype, int64_t K, int64
     for (auto p : pool) MI_CHECK(hipFree(p));
     MI_CHECK(hipFree(x));
     MI_CHECK(hipFree(y));
+    MI_CHECK(hipFree(fbuf)); MI_CHECK(hipFree(hbuf)); MI_CHECK(hipFree(slots)); MI_CHECK(hipFree(pos));
     return ms * 1000.0 / iters;
 }
 

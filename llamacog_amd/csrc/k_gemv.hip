@@ -323,6 +323,8 @@ struct g_q4_0 {
 
 // ---- kernel ------------------------------------------------------------------------------------
 constexpr int GEMV_MAXMAT = 3;
+constexpr int GEMV_ROPE_MAXPAIRS = 256;
+constexpr int GEMV_MAXG = 16;             // row groups per workgroup of the pipelined kernel with epilogues   // rope table of the fused epilogue: n_dims <= 512
 
 struct gemv_args {
     const uint8_t * W[GEMV_MAXMAT]; int64_t nb01[GEMV_MAXMAT]; int64_t M[GEMV_MAXMAT];
@@ -353,107 +355,125 @@ struct gemv_args {
     float * post_add; const float * post_b; int64_t post_n;
 };
 
-// the prologue: this lane's task activation, Q8_K-quantized across the 4 lanes of a block
-// (quantize_row_q8_K_ref: first index of max |x|, iscale = -127/max, min(127, rint), d = 1/iscale).
-// A task's 64 values are four runs of 16 contiguous elements (T::elem(t, 16g) .. +15), read as
-// float4 and kept in registers between the max and the quantization passes.
-template <class T>
-__device__ __forceinline__ void prologue_act(const gemv_args & p, int tt, int lane, bool writer, typename T::act & x) {
+// the activation prologue, once per workgroup (4 waves): wave w owns the Q8_K blocks
+// j = w, w+4, ... (256 consecutive elements each, lane l holding 4l..4l+3).
+//   pro 1: x = pa (+ pb); the canonical RMS-norm sum of squares (quant_act.h norm_sumsq:
+//          q(j, l) partials in LDS, summed in j order per lane, then the wave butterfly);
+//          y = x * scale; yw = y * pw
+//   pro 2: yw = pa * pb
+// then yw is quantized block by block with q8K_wave (the quantizer of the stand-alone and
+// fused producer kernels, so the bytes are theirs) into LDS, where the mat-vec's
+// task loads read it.  Workgroup 0 also stores the chain's node outputs and the quantized
+// activation for later launches that share it.  Returns the LDS activation.
+constexpr int GEMV_PRO_XREG = 4;   // blocks per wave kept in registers between the two passes
+
+template <int NWV>
+__device__ __forceinline__ gemv_act prologue_wg(const gemv_args & p, uint8_t * lds) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nb = (int) (p.pk / 256);
+    const bool writer = blockIdx.x == 0;
+    int8_t * qs = (int8_t *) lds;
+    int16_t * bs = (int16_t *) (lds + p.pk);
+    float * dd = (float *) (lds + p.pk + p.pk / 8);
+    double * qp = (double *) (lds + ((p.pk + p.pk / 8 + 4 * nb + 15) & ~(int64_t) 15));   // [nb][64], pro 1 only
     float scale = 1.0f;
+    float4 xr[GEMV_PRO_XREG], wr[GEMV_PRO_XREG];
+    auto load_x = [&](int j) {
+        const int64_t e = 256 * (int64_t) j + 4 * lane;
+        float4 x = *(const float4 *) (p.pa + e);
+        if (p.pb) {
+            const float4 y = *(const float4 *) (p.pb + e);
+            if (p.pro == 1) {
+                x.x = __fadd_rn(x.x, y.x); x.y = __fadd_rn(x.y, y.y); x.z = __fadd_rn(x.z, y.z); x.w = __fadd_rn(x.w, y.w);
+            } else {
+                x.x = __fmul_rn(x.x, y.x); x.y = __fmul_rn(x.y, y.y); x.z = __fmul_rn(x.z, y.z); x.w = __fmul_rn(x.w, y.w);
+            }
+        }
+        return x;
+    };
     if (p.pro == 1) {
-        const double s = norm_sumsq(p.pa, p.pb, p.pk, lane);
-        const float mean = (float) (s / (double) p.pk);
+#pragma unroll
+        for (int i = 0; i < GEMV_PRO_XREG; ++i) {
+            const int j = wave + NWV * i;
+            if (j < nb) {
+                xr[i] = load_x(j);
+                if (p.pw) wr[i] = *(const float4 *) (p.pw + 256 * (int64_t) j + 4 * lane);
+            }
+        }
+        for (int j = wave; j < nb; j += NWV) {
+            const int i = (j - wave) / NWV;
+            float4 x;
+            if (i < GEMV_PRO_XREG) {
+                x = xr[0];
+#pragma unroll
+                for (int k = 1; k < GEMV_PRO_XREG; ++k) x = i == k ? xr[k] : x;
+            } else {
+                x = load_x(j);
+            }
+            qp[j * 64 + lane] = norm_q4(x);
+            if (writer && p.o_add) *(float4 *) (p.o_add + 256 * (int64_t) j + 4 * lane) = x;
+        }
+        __syncthreads();
+        double sq = 0.0;
+        for (int j = 0; j < nb; ++j) sq += qp[j * 64 + lane];
+        sq = wave_sum(sq);
+        const float mean = (float) (sq / (double) p.pk);
         scale = 1.0f / sqrtf(mean + p.eps);
     }
-    float v[64];
+    for (int j = wave; j < nb; j += NWV) {
+        const int i = (j - wave) / NWV;
+        const int64_t e = 256 * (int64_t) j + 4 * lane;
+        float4 x;
+        if (p.pro == 1 && i < GEMV_PRO_XREG) {
+            x = xr[0];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const int base = T::elem(tt, 16 * g);
+            for (int k = 1; k < GEMV_PRO_XREG; ++k) x = i == k ? xr[k] : x;
+        } else {
+            x = load_x(j);
+        }
+        float v[4] = {x.x, x.y, x.z, x.w};
+        if (p.pro == 1) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int e = base + 4 * c;
-            const float4 a4 = *(const float4 *) (p.pa + e);
-            float xa[4] = {a4.x, a4.y, a4.z, a4.w}, yn[4], yw[4];
-            if (p.pro == 1) {
-                if (p.pb) {
-                    const float4 b4 = *(const float4 *) (p.pb + e);
-                    xa[0] = __fadd_rn(xa[0], b4.x); xa[1] = __fadd_rn(xa[1], b4.y);
-                    xa[2] = __fadd_rn(xa[2], b4.z); xa[3] = __fadd_rn(xa[3], b4.w);
-                }
+            for (int k = 0; k < 4; ++k) v[k] = __fmul_rn(v[k], scale);
+            if (writer && p.o_norm) *(float4 *) (p.o_norm + e) = make_float4(v[0], v[1], v[2], v[3]);
+            if (p.pw) {
+                float4 w4;
+                if (i < GEMV_PRO_XREG) {
+                    w4 = wr[0];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) yn[i] = __fmul_rn(xa[i], scale);
-                if (p.pw) {
-                    const float4 w4 = *(const float4 *) (p.pw + e);
-                    yw[0] = __fmul_rn(yn[0], w4.x); yw[1] = __fmul_rn(yn[1], w4.y);
-                    yw[2] = __fmul_rn(yn[2], w4.z); yw[3] = __fmul_rn(yn[3], w4.w);
+                    for (int k = 1; k < GEMV_PRO_XREG; ++k) w4 = i == k ? wr[k] : w4;
                 } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) yw[i] = yn[i];
+                    w4 = *(const float4 *) (p.pw + e);
                 }
-                if (writer) {
-                    if (p.o_add) *(float4 *) (p.o_add + e) = make_float4(xa[0], xa[1], xa[2], xa[3]);
-                    if (p.o_norm) *(float4 *) (p.o_norm + e) = make_float4(yn[0], yn[1], yn[2], yn[3]);
-                    if (p.o_mul) *(float4 *) (p.o_mul + e) = make_float4(yw[0], yw[1], yw[2], yw[3]);
-                }
-            } else {
-                const float4 b4 = *(const float4 *) (p.pb + e);
-                yw[0] = __fmul_rn(xa[0], b4.x); yw[1] = __fmul_rn(xa[1], b4.y);
-                yw[2] = __fmul_rn(xa[2], b4.z); yw[3] = __fmul_rn(xa[3], b4.w);
-                if (writer && p.o_mul) *(float4 *) (p.o_mul + e) = make_float4(yw[0], yw[1], yw[2], yw[3]);
+                v[0] = __fmul_rn(v[0], w4.x); v[1] = __fmul_rn(v[1], w4.y);
+                v[2] = __fmul_rn(v[2], w4.z); v[3] = __fmul_rn(v[3], w4.w);
             }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[16 * g + 4 * c + i] = yw[i];
         }
+        if (writer && p.o_mul) *(float4 *) (p.o_mul + e) = make_float4(v[0], v[1], v[2], v[3]);
+        q8K_wave(v, lane, qs + 256 * j, bs + 16 * j, dd + j);
     }
-    // first max |v| of the task (element order = k order), then of the block (4 lanes,
-    // lowest element index on ties)
-    float amax = 0.0f, vmax = 0.0f;
-    int kmax = 64;
-#pragma unroll
-    for (int k = 0; k < 64; ++k) {
-        const float ax = fabsf(v[k]);
-        if (ax > amax) { amax = ax; vmax = v[k]; kmax = k; }
-    }
-    int imax = kmax < 64 ? T::elem(tt, kmax) : 0x7fffffff;
-#pragma unroll
-    for (int o = 1; o < 4; o <<= 1) {
-        const float oa = __shfl_xor(amax, o, WAVE);
-        const float ov = __shfl_xor(vmax, o, WAVE);
-        const int   oi = __shfl_xor(imax, o, WAVE);
-        if (oa > amax || (oa == amax && oi < imax)) { amax = oa; vmax = ov; imax = oi; }
-    }
-    const float iscale = amax == 0.0f ? 0.0f : -127.0f / vmax;
-    const float d = amax == 0.0f ? 0.0f : 1.0f / iscale;
-    int q4[16], g16[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        uint32_t packed = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int k = 4 * i + c;
-            int iv = 0;
-            if (amax != 0.0f) {
-                iv = (int) rintf(__fmul_rn(iscale, v[k]));
-                iv = iv < 127 ? iv : 127;
-            }
-            g16[k >> 4] += iv;
-            packed |= (uint32_t) (iv & 0xff) << (8 * c);
-        }
-        q4[i] = (int) packed;
-        if (writer) *(uint32_t *) (p.cq + T::elem(tt, 4 * i)) = packed;
-    }
+    __syncthreads();
     if (writer) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) p.cs[T::elem(tt, 16 * g) / 16] = (int16_t) g16[g];
-        if ((tt & 3) == 0) p.cd[T::elem(tt, 0) / 256] = d;
+        for (int i = threadIdx.x; i < p.pk / 16; i += 64 * NWV) {
+            *(int4 *) (p.cq + 16 * i) = *(const int4 *) (qs + 16 * i);
+            p.cs[i] = bs[i];
+        }
+        for (int i = threadIdx.x; i < nb; i += 64 * NWV) p.cd[i] = dd[i];
     }
-    T::pack(x, q4, g16, d);
+    return gemv_act{qs, dd, bs};
+}
+
+// LDS bytes of the prologue: Q8_K activation (qs, bsums, d) + the norm partials
+static inline size_t prologue_lds_bytes(int pro, int64_t K) {
+    const int64_t nb = K / 256;
+    return (size_t) ((K + K / 8 + 4 * nb + 15) & ~(int64_t) 15) + (pro == 1 ? (size_t) nb * 64 * 8 : 0);
 }
 
 // epilogue of one output row; v = this row's sum, vp = the sum of its rope partner row^1
-__device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t M, int64_t row, float v, float vp) {
+__device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t M, int64_t row, float v, float vp,
+                                           const float2 * rtab = nullptr, uint16_t * const * f16p = nullptr) {
     if (p.dst[mi]) p.dst[mi][row] = v;
-    if (p.f16out[mi]) (*p.f16out[mi])[row] = f2h(v);
+    if (p.f16out[mi]) (f16p ? f16p[2 * mi] : *p.f16out[mi])[row] = f2h(v);
     if (p.silu[mi]) {
         const int64_t nvec = (M / 16) * 16;
         p.silu[mi][row] = row < nvec ? v / (1.0f + v_expf_avx512(-v)) : v / (1.0f + expf_cr(-v));
@@ -463,13 +483,14 @@ __device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t 
         float o = v;
         if (i0 < p.rp.n_dims) {
             float c, sn, o0, o1;
-            rope_cs(p.rp, (float) p.rope_pos[0], i0 / 2, p.rope_ff, c, sn);
+            if (rtab) { c = rtab[i0 / 2].x; sn = rtab[i0 / 2].y; }
+            else rope_cs(p.rp, (float) p.rope_pos[0], i0 / 2, p.rope_ff, c, sn);
             const bool odd = row & 1;
             rope_rotate(odd ? vp : v, odd ? v : vp, c, sn, o0, o1);
             o = odd ? o1 : o0;
         }
         if (p.rope_out[mi]) p.rope_out[mi][row] = o;
-        if (p.rope_f16[mi]) (*p.rope_f16[mi])[row] = f2h(o);
+        if (p.rope_f16[mi]) (f16p ? f16p[2 * mi + 1] : *p.rope_f16[mi])[row] = f2h(o);
     }
 }
 
@@ -557,21 +578,18 @@ __global__ __launch_bounds__(256) void k_gemv(const gemv_args p) {
 // weight slices into registers before computing the current one, so dequantization and the
 // dot products overlap the HBM stream instead of following it (a one-shot grid computes
 // only after its last load lands).  Needs ntasks <= 64*WPR (one pass over K per wave).
-template <class T, int R, int WPR>
-__global__ __launch_bounds__(256) void k_gemv_pipe(const gemv_args p, const int64_t ngroups) {
-    constexpr int RPG = (4 / WPR) * R;   // rows per group
+// MODE: 0 = plain stores (no prologue, no epilogue), 1 = epilogues, 2 = activation prologue +
+// epilogues.  The lean modes keep the register footprint (and so the number of resident
+// workgroups) of the plain mat-vec: 90 VGPRs at R = 2 against 134 with the prologue compiled in.
+template <class T, int R, int WPR, int MODE, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const int64_t ngroups) {
+    constexpr int NT = 64 * NWV;
+    constexpr int RPG = (NWV / WPR) * R;   // rows per group
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wsub = wave % WPR;
     const int t = wsub * WAVE + lane;
     const bool active = t < p.ntasks;
     const int tt = active ? t : 0;
-    typename T::act x;
-    if (p.pro) prologue_act<T>(p, tt, lane, blockIdx.x == 0 && wave < WPR && active, x);
-    else T::load(p.A, tt, x);
-    if (p.post_add && blockIdx.x == 0) {
-        for (int64_t i = threadIdx.x; i < p.post_n; i += 256) p.post_add[i] = __fadd_rn(p.post_add[i], p.post_b[i]);
-    }
-
     auto locate = [&](int64_t g, int & mi, int64_t & row0) {
         mi = 0;
 #pragma unroll
@@ -587,12 +605,49 @@ __global__ __launch_bounds__(256) void k_gemv_pipe(const gemv_args p, const int6
         for (int r = 0; r < R; ++r) T::fetch(p.W[mi] + min(row0 + r, M - 1) * p.nb01[mi], tt, w[r]);
     };
 
+    // the first group's weight loads leave before anything else, so the activation prologue,
+    // the rope table and the activation loads below overlap that HBM latency
     typename T::raw cur[R], nxt[R];
     int64_t g = blockIdx.x;
     if (g < ngroups) fetch(g, cur);
-    __shared__ float red[2][4][R];
-    int par = 0;
-    for (; g < ngroups; g += gridDim.x, par ^= 1) {
+    // cos/sin of every rope pair at this token's position, one pair per thread (rope_cs, the
+    // same arithmetic the stand-alone ROPE kernel uses), instead of per output row in the
+    // epilogue's few active lanes
+    typename T::act x;
+    if constexpr (MODE != 2) T::load(p.A, tt, x);   // in flight with the first weight loads
+    __shared__ float2 rtab[MODE ? GEMV_ROPE_MAXPAIRS : 1];
+    // KV-cache destinations of the f16 epilogues, read from the dynamic-pointer table now
+    // rather than as a dependent load in the epilogue
+    __shared__ uint16_t * f16p[2 * GEMV_MAXMAT];
+    if (MODE) {
+        if (threadIdx.x < 2 * GEMV_MAXMAT) {
+            const int mi = threadIdx.x >> 1;
+            uint16_t * const * slot = (threadIdx.x & 1) ? p.rope_f16[mi] : p.f16out[mi];
+            f16p[threadIdx.x] = slot ? *slot : nullptr;
+        }
+        if (p.need_pairs) {
+            for (int ip = threadIdx.x; ip < p.rp.n_dims / 2; ip += NT) {
+                float c, sn;
+                rope_cs(p.rp, (float) p.rope_pos[0], ip, p.rope_ff, c, sn);
+                rtab[ip] = make_float2(c, sn);
+            }
+        }
+        __syncthreads();
+    }
+    if constexpr (MODE == 2) {
+        extern __shared__ __attribute__((aligned(16))) uint8_t pro_lds[];
+        const gemv_act A = prologue_wg<NWV>(p, pro_lds);
+        T::load(A, tt, x);
+    }
+    if (MODE && p.post_add && blockIdx.x == 0) {
+        for (int64_t i = threadIdx.x; i < p.post_n; i += NT) p.post_add[i] = __fadd_rn(p.post_add[i], p.post_b[i]);
+    }
+    __shared__ float red[2][NWV][R];
+    // MODE >= 1: row sums are parked in LDS and the epilogues run after the loop on all 256
+    // threads (not on the R lanes holding the sums, with the next group's loads live)
+    __shared__ float res[MODE ? GEMV_MAXG * RPG : 1];
+    int par = 0, kg = 0;
+    for (; g < ngroups; g += gridDim.x, par ^= 1, ++kg) {
         const int64_t gn = g + gridDim.x;
         if (gn < ngroups) fetch(gn, nxt);
         float acc[R];
@@ -617,20 +672,32 @@ __global__ __launch_bounds__(256) void k_gemv_pipe(const gemv_args p, const int6
             }
         }
         if (wsub == 0 && lane < R) {
-            int mi;
-            int64_t row0;
-            locate(g, mi, row0);
-            const int64_t M = p.M[mi];
-            float v = acc[0], vp = acc[R > 1 ? 1 : 0];
+            float v = acc[0];
 #pragma unroll
             for (int r = 1; r < R; ++r) v = lane == r ? acc[r] : v;
-#pragma unroll
-            for (int r = 0; r < R; ++r) vp = (lane ^ 1) == r ? acc[r] : vp;
-            const int64_t row = row0 + lane;
-            if (row < M) gemv_store(p, mi, M, row, v, vp);
+            if constexpr (MODE == 0) {
+                int mi;
+                int64_t row0;
+                locate(g, mi, row0);
+                if (row0 + lane < p.M[mi]) p.dst[mi][row0 + lane] = v;
+            } else {
+                res[kg * RPG + (wave / WPR) * R + lane] = v;
+            }
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) cur[r] = nxt[r];
+    }
+    if constexpr (MODE >= 1) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < kg * RPG; i += NT) {
+            const int64_t gg = blockIdx.x + (int64_t) (i / RPG) * gridDim.x;
+            int mi = 0;
+#pragma unroll
+            for (int k = 1; k < GEMV_MAXMAT; ++k) mi += gg >= p.blk0[k] ? 1 : 0;
+            const int64_t row = (gg - p.blk0[mi]) * RPG + i % RPG;
+            // rope partner row ^ 1 lies in the same group (RPG is even whenever rope is fused)
+            if (row < p.M[mi]) gemv_store(p, mi, p.M[mi], row, res[i], res[RPG > 1 ? i ^ 1 : i], rtab, f16p);
+        }
     }
 }
 
@@ -667,33 +734,75 @@ static void launch_g(hipStream_t st, gemv_args & a, int nmat) {
     }
 }
 
+template <class T> struct is_kq_t { static constexpr bool value = false; };
+template <> struct is_kq_t<g_q4_K> { static constexpr bool value = true; };
+template <> struct is_kq_t<g_q5_K> { static constexpr bool value = true; };
+template <> struct is_kq_t<g_q6_K> { static constexpr bool value = true; };
+
 static int g_gemv_pipe = -1;   // GGML_MI355X_GEMV_PIPE: 0 disables the pipelined kernel
 static int g_gemv_wgs = -1;    // GGML_MI355X_GEMV_WGS: persistent grid size
 
-template <class T, int R, int WPR>
-static void launch_pipe(hipStream_t st, gemv_args & a, int nmat) {
-    constexpr int RPG = (4 / WPR) * R;
+static int g_num_cu = 0;
+
+template <class T, int R, int WPR, int MODE>
+static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
+    // the prologue is computed once per workgroup: 16-wave workgroups, one per CU
+    constexpr int NWV = MODE == 2 ? 16 : 4;
+    constexpr int RPG = (NWV / WPR) * R;
     a.blk0[0] = 0;
     for (int i = 0; i < GEMV_MAXMAT; ++i) a.blk0[i + 1] = a.blk0[i] + (i < nmat ? ceil_div(a.M[i], RPG) : 0);
     for (int i = nmat; i < GEMV_MAXMAT; ++i) a.blk0[i] = a.blk0[nmat];
     const int64_t ng = a.blk0[nmat];
-    const int64_t grid = std::min<int64_t>(ng, g_gemv_wgs);
+    if (!g_num_cu) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        MI_CHECK(hipGetDevice(&dev));
+        MI_CHECK(hipGetDeviceProperties(&prop, dev));
+        g_num_cu = prop.multiProcessorCount;
+    }
+    int64_t grid = std::min<int64_t>(ng, MODE == 2 ? g_num_cu : g_gemv_wgs);
+    if (MODE >= 1) grid = std::max<int64_t>(grid, ceil_div(ng, GEMV_MAXG));   // LDS-parked row sums
+    const size_t lds = MODE == 2 ? prologue_lds_bytes(a.pro, a.pk) : 0;
     if (t_ev_beg) {
-        hipExtLaunchKernelGGL((k_gemv_pipe<T, R, WPR>), dim3((unsigned) grid), dim3(256), 0, st, t_ev_beg, t_ev_end, 0, a, ng);
+        hipExtLaunchKernelGGL((k_gemv_pipe<T, R, WPR, MODE, NWV>), dim3((unsigned) grid), dim3(64 * NWV), lds, st, t_ev_beg, t_ev_end, 0, a, ng);
     } else {
-        hipLaunchKernelGGL((k_gemv_pipe<T, R, WPR>), dim3((unsigned) grid), dim3(256), 0, st, a, ng);
+        hipLaunchKernelGGL((k_gemv_pipe<T, R, WPR, MODE, NWV>), dim3((unsigned) grid), dim3(64 * NWV), lds, st, a, ng);
+    }
+}
+
+template <class T, int R, int WPR>
+static void launch_pipe(hipStream_t st, gemv_args & a, int nmat) {
+    bool epi = a.post_add != nullptr || a.need_pairs;
+    for (int i = 0; i < nmat; ++i) {
+        epi = epi || !a.dst[i] || a.silu[i] || a.f16out[i] || a.rope_out[i] || a.rope_f16[i];
+    }
+    if (a.pro) {
+        if constexpr (is_kq_t<T>::value) launch_pipe_m<T, R, WPR, 2>(st, a, nmat);
+        else GGML_ABORT("mi355x: GEMV prologue on a non-K-quant");
+    } else if (epi) {
+        launch_pipe_m<T, R, WPR, 1>(st, a, nmat);
+    } else {
+        launch_pipe_m<T, R, WPR, 0>(st, a, nmat);
     }
 }
 
 template <class T>
 static bool launch_pipe_t(hipStream_t st, gemv_args & a, int nmat, int64_t Mt) {
     if (g_gemv_pipe < 0) g_gemv_pipe = getenv("GGML_MI355X_GEMV_PIPE") ? atoi(getenv("GGML_MI355X_GEMV_PIPE")) : 1;
-    if (g_gemv_wgs < 0) g_gemv_wgs = getenv("GGML_MI355X_GEMV_WGS") ? atoi(getenv("GGML_MI355X_GEMV_WGS")) : 512;
+    if (g_gemv_wgs < 0) g_gemv_wgs = getenv("GGML_MI355X_GEMV_WGS") ? atoi(getenv("GGML_MI355X_GEMV_WGS")) : 2048;
     if (!g_gemv_pipe || a.ntasks > 4 * WAVE) return false;
+    if (a.need_pairs && a.rp.n_dims > 2 * GEMV_ROPE_MAXPAIRS) return false;
     const int wpr = a.ntasks <= WAVE ? 1 : (a.ntasks <= 2 * WAVE ? 2 : 4);
-    const int64_t g4 = ceil_div(Mt * wpr, 16);   // groups with R = 4
-    int R = g4 >= 512 ? 4 : (2 * g4 >= 512 ? 2 : 1);
-    if (R == 1 && a.need_pairs) R = 2;   // the rope epilogue needs rows 2i, 2i+1 in one wave
+    // geometry measured on MI355X (tools/gemv_lab.hip, back-to-back launches over cold
+    // weights): two rows per wave and a grid of up to 2048 workgroups is the fastest or within
+    // 5 % of it on every Llama-3-8B shape; the 6-bit K-quant at K = 14336 prefers four rows;
+    // a matrix too short to give 256 workgroups at two rows per wave takes one
+    int R = 2;
+    if (std::is_same<T, g_q6_K>::value && wpr == 4) R = 4;
+    // a matrix too short to give 256 workgroups at two rows per wave takes one (the rope
+    // epilogue reads its partner row from the LDS-parked sums of the same group)
+    if (ceil_div(Mt * wpr, a.pro ? 32 : 8) < 256) R = 1;
+    if (a.pro && R > 2) R = 2;   // 16-wave workgroups: four rows per wave would spill
     switch (R * 8 + wpr) {
         case 4 * 8 + 1: launch_pipe<T, 4, 1>(st, a, nmat); break;
         case 4 * 8 + 2: launch_pipe<T, 4, 2>(st, a, nmat); break;
@@ -755,7 +864,7 @@ bool gemv_epilogue_ok(const ggml_tensor * mm) { return gemv_supported(mm); }
 bool gemv_prologue_ok(const ggml_tensor * mm) {
     if (!gemv_supported(mm) || !is_kq(mm->src[0]->type)) return false;
     const int64_t K = mm->src[0]->ne[0];
-    if (K % 256 != 0 || K / 64 > 4 * WAVE) return false;
+    if (K % 256 != 0 || K / 64 > 4 * WAVE || prologue_lds_bytes(1, K) > 48 * 1024) return false;
     static int pipe = -1;
     if (pipe < 0) pipe = getenv("GGML_MI355X_GEMV_PIPE") ? atoi(getenv("GGML_MI355X_GEMV_PIPE")) : 1;
     return pipe != 0;

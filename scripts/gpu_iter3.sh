@@ -1,0 +1,16 @@
+# quick iteration: GPU tests (subset via $TESTK), tg bench, kernel trace summary
+set -o pipefail
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$PWD}
+cd $R
+mkdir -p gpurun_out/trace
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${TESTK:+-k "$TESTK"} > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; grep -E "Error|error|assert|FAILED" gpurun_out/pytest_gpu.log | head -30; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python bench.py --pp ${PP:-0} --no-cpu-baseline --roofline-steps 8 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench rc=$?"; tail -20 gpurun_out/bench.err; exit 1; }
+python3 -c "import json;d=json.load(open('gpurun_out/bench.json'));print('tg', d['value'], 'ms', d['ms_per_step'], 'pp', d['pp_tok_s'], 'gemv', d['roofline']['achieved'], d['roofline']['avg_launch_us'], 'fa', d['roofline']['fattn_avg_us'])"
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/trace/t -o run -- python3 $R/bench.py --steps 16 --warmup 4 --pp 0 --no-cpu-baseline --roofline-steps 0 > $R/gpurun_out/trace/bench.json 2> $R/gpurun_out/trace/bench.err || { tail $R/gpurun_out/trace/bench.err; exit 1; }
+cd $R
+python3 scripts/trace_summary.py $(find gpurun_out/trace/t -name '*kernel_trace.csv' | head -1) 4 > gpurun_out/trace/summary.txt
+rm -rf gpurun_out/trace/t
+head -30 gpurun_out/trace/summary.txt

@@ -5,8 +5,11 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-# decode tokens: each llama_decode starts with one k_get_rows (token embedding)
-starts = [i for i, r in enumerate(rows) if 'k_get_rows' in r['Kernel_Name']]
+# decode tokens: each llama_decode ends with one output-projection GEMV, the longest single
+# kernel of a decode step; segment the trace at those launches
+dur = lambda r: int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+longest = max(rows, key=dur)['Kernel_Name']
+starts = [i for i, r in enumerate(rows) if r['Kernel_Name'] == longest and dur(r) > 0.5 * dur(max(rows, key=dur))]
 skip = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 toks = list(zip(starts[skip:-1], starts[skip + 1:]))
 agg = collections.defaultdict(lambda: [0, 0.0])
@@ -17,7 +20,7 @@ for a, b in toks:
     for r in seg:
         d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
         busy += d
-        n = r['Kernel_Name'].split('(')[0][:64]
+        n = r['Kernel_Name'].split('(')[0].replace('void mi355x::', '')[:56] + f" g{int(r.get('Grid_Size_X', r.get('Grid_Size', 0))) // int(r.get('Workgroup_Size_X', r.get('Workgroup_Size', 1)) or 1)}"
         agg[n][0] += 1
         agg[n][1] += d
 nt = len(toks)
