@@ -78,6 +78,14 @@ int mi355x_soft_max(const float * x, int64_t nc, int64_t nr, const float * mask,
                     void * stream);
 // UNARY SILU (ops.cpp:2902, vec.cpp:233)
 int mi355x_silu(const float * x, int64_t ne0, int64_t nrows, float * y, void * stream);
+// MUL_MAT_ID (ggml-cpu/ggml-cpu.c:1466, the MoE expert mat-mul): as [n_as][M][K] rows of wtype,
+// ids [T][ids_row] int32 (first n_used per token used), x [T][ne11][K] f32, y [T][n_used][M]
+int mi355x_mul_mat_id(int wtype, const void * as, int64_t K, int64_t M, int64_t n_as, const int32_t * ids, int64_t ids_row,
+                      int64_t n_used, const float * x, int64_t ne11, int64_t T, float * y, void * stream);
+// ARGSORT (ops.cpp:6956-6993, ggml_top_k): order 0 ascending, 1 descending; out [nrows][ne0] int32
+int mi355x_argsort(const float * x, int64_t ne0, int64_t nrows, int order, int32_t * out, void * stream);
+// SUM_ROWS (ops.cpp:1956-1986): y [nrows]
+int mi355x_sum_rows(const float * x, int64_t ne0, int64_t nrows, float * y, void * stream);
 // FLASH_ATTN_EXT (ops.cpp:7015-7232): q [n_q][H][D] f32, k/v [n_kv][Hkv][D] f16 (1) or q8_0 (8),
 // mask [n_q][n_kv] f16 or NULL, out [n_q][H][D]
 // test hook: phase-1 scores of the CPU-exact flash attention (q [128] f32, k [n][128] f16)

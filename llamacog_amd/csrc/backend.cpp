@@ -440,13 +440,75 @@ static void mi_backend_synchronize(ggml_backend_t backend) {
     ctx->ex.collect_timing();
 }
 
+// ---- Infinity-Cache warm planner (warm.h) ----------------------------------------------------
+// GGML_MI355X_WARM="norm,fa,mulq" = MiB each latency-bound kernel kind may warm ahead (0 = off);
+// GGML_MI355X_WARM_WG="norm,fa,mulq" = warm workgroups it carries
+static struct warm_cfg {
+    int64_t budget[WARM_NKIND] = {0, 0, 0};
+    int     nwg[WARM_NKIND] = {32, 96, 256};
+    warm_cfg() {
+        int64_t mb[WARM_NKIND] = {0, 0, 0};
+        if (const char * e = getenv("GGML_MI355X_WARM")) {
+            long a = 0, b = 0, c = 0;
+            const int n = sscanf(e, "%ld,%ld,%ld", &a, &b, &c);
+            mb[0] = n >= 1 ? a : 0; mb[1] = n >= 2 ? b : 0; mb[2] = n >= 3 ? c : 0;
+        }
+        for (int k = 0; k < WARM_NKIND; ++k) budget[k] = mb[k] << 20;
+        if (const char * e = getenv("GGML_MI355X_WARM_WG")) {
+            int a = 0, b = 0, c = 0;
+            if (sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) { nwg[0] = a; nwg[1] = b; nwg[2] = c; }
+        }
+    }
+} g_warm;
+
+void exec_ctx::warm_plan(ggml_cgraph * g) {
+    warm_list.clear();
+    warm_cur = 0;
+    warm_off = 0;
+    const int n = ggml_graph_n_nodes(g);
+    for (int i = 0; i < n; ++i) {
+        const ggml_tensor * t = ggml_graph_node(g, i);
+        if (t->op == GGML_OP_MUL_MAT && gemv_supported(t)) {
+            warm_list.push_back({i, (const uint8_t *) t->src[0]->data, (int64_t) ggml_nbytes(t->src[0])});
+        }
+    }
+}
+
+warm_spec exec_ctx::warm_take(int kind) {
+    warm_spec s;
+    s.nseg = 0;
+    s.nwg = 0;
+    const int64_t budget = g_warm.budget[kind];
+    if (budget < 1024 || warm_list.empty() || !fusion_enabled()) return s;
+    // mat-vecs at or before the current node have run (or are running): never warm them
+    while (warm_cur < warm_list.size() && warm_list[warm_cur].node <= cur_node) { ++warm_cur; warm_off = 0; }
+    int64_t left = budget;
+    while (left >= 1024 && warm_cur < warm_list.size() && s.nseg < WARM_MAXSEG) {
+        const warm_seg & g = warm_list[warm_cur];
+        const int64_t take = std::min(g.n - warm_off, left) & ~(int64_t) 1023;
+        if (take > 0) {
+            s.p[s.nseg] = g.p + warm_off;
+            s.n[s.nseg] = take;
+            ++s.nseg;
+            left -= take;
+            warm_off += take;
+        }
+        if (g.n - warm_off < 1024) { ++warm_cur; warm_off = 0; }
+    }
+    s.nwg = s.nseg ? g_warm.nwg[kind] : 0;
+    return s;
+}
+
 static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.qcache_clear();
+    ex.rt_table = nullptr;
+    ex.warm_plan(cgraph);
     ex.done.clear();
     ex.pend = exec_ctx::pending_pro();
     ex.post_add = nullptr;
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) {
+        ex.cur_node = i;
         i += op_compute(ex, cgraph, i);
     }
     if (ex.post_add) {   // a deferred in-place ADD with no later launch to carry it

@@ -92,6 +92,57 @@ GGML_BACKEND_API int mi355x_mul_mat(int wtype, const void * w, int64_t K, int64_
     return 0;
 }
 
+// ---- MUL_MAT_ID (ggml-cpu/ggml-cpu.c:1466): as [n_as][M][K] rows of wtype; ids [T][ids_row]
+// int32 of which the first n_used per token are used (a view, as test-backend-ops builds it);
+// x [T][ne11][K] f32 (ne11 = 1 broadcasts one row to every slot); y [T][n_used][M]
+GGML_BACKEND_API int mi355x_mul_mat_id(int wtype, const void * as, int64_t K, int64_t M, int64_t n_as, const int32_t * ids,
+                                       int64_t ids_row, int64_t n_used, const float * x, int64_t ne11, int64_t T, float * y,
+                                       void * stream) {
+    ggml_tensor A, I, X, Y;
+    const int64_t nea[4] = {K, M, n_as, 1}, nei[4] = {n_used, T, 1, 1}, nex[4] = {K, ne11, T, 1}, ney[4] = {M, n_used, T, 1};
+    init_tensor(A, (ggml_type) wtype, nea, (void *) as);
+    init_tensor(I, GGML_TYPE_I32, nei, (void *) ids);
+    I.nb[1] = (size_t) ids_row * sizeof(int32_t);
+    I.nb[2] = I.nb[1] * T; I.nb[3] = I.nb[2];
+    init_tensor(X, GGML_TYPE_F32, nex, (void *) x);
+    init_tensor(Y, GGML_TYPE_F32, ney, y);
+    Y.op = GGML_OP_MUL_MAT_ID;
+    Y.src[0] = &A; Y.src[1] = &X; Y.src[2] = &I;
+    if (!op_supported(&Y)) return -1;
+    scoped_ctx sc(stream);
+    op_mul_mat_id(sc.ex, &Y);
+    return 0;
+}
+
+// ---- ARGSORT (ops.cpp:6956) of nrows rows of ne0 floats; order 0 = ascending, 1 = descending
+GGML_BACKEND_API int mi355x_argsort(const float * x, int64_t ne0, int64_t nrows, int order, int32_t * out, void * stream) {
+    ggml_tensor X, Y;
+    const int64_t ne[4] = {ne0, nrows, 1, 1};
+    init_tensor(X, GGML_TYPE_F32, ne, (void *) x);
+    init_tensor(Y, GGML_TYPE_I32, ne, out);
+    Y.op = GGML_OP_ARGSORT;
+    Y.src[0] = &X;
+    Y.op_params[0] = order;
+    if (!op_supported(&Y)) return -1;
+    scoped_ctx sc(stream);
+    op_argsort(sc.ex, &Y);
+    return 0;
+}
+
+// ---- SUM_ROWS (ops.cpp:1956): y[r] = sum of row r (ne0 floats)
+GGML_BACKEND_API int mi355x_sum_rows(const float * x, int64_t ne0, int64_t nrows, float * y, void * stream) {
+    ggml_tensor X, Y;
+    const int64_t ne[4] = {ne0, nrows, 1, 1}, ney[4] = {1, nrows, 1, 1};
+    init_tensor(X, GGML_TYPE_F32, ne, (void *) x);
+    init_tensor(Y, GGML_TYPE_F32, ney, y);
+    Y.op = GGML_OP_SUM_ROWS;
+    Y.src[0] = &X;
+    if (!op_supported(&Y)) return -1;
+    scoped_ctx sc(stream);
+    op_sum_rows(sc.ex, &Y);
+    return 0;
+}
+
 // ---- rms_norm over nrows rows (optionally fused with a weight vector w[ne0]) ---------------
 GGML_BACKEND_API int mi355x_rms_norm(const float * x, int64_t ne0, int64_t nrows, float eps, const float * w, float * y,
                                      float * y_mul, void * stream) {

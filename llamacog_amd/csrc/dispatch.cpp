@@ -18,6 +18,7 @@ bool mmq_supported(const ggml_tensor * dst);
 void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst);
 
 bool fattn_supported(const ggml_tensor * op);
+bool mul_mat_id_supported(const ggml_tensor * op);
 
 static bool is_f32(const ggml_tensor * t) { return t && t->type == GGML_TYPE_F32; }
 
@@ -120,6 +121,13 @@ bool op_supported(const ggml_tensor * op) {
         }
         case GGML_OP_FLASH_ATTN_EXT:
             return fattn_supported(op);
+        case GGML_OP_MUL_MAT_ID:
+            return mul_mat_id_supported(op);
+        case GGML_OP_ARGSORT:
+            // the CPU's exchange order on one lane per row: router-sized rows (n_expert)
+            return is_f32(op->src[0]) && op->type == GGML_TYPE_I32 && op->src[0]->nb[0] == 4 && op->src[0]->ne[0] <= 1024;
+        case GGML_OP_SUM_ROWS:
+            return is_f32(op->src[0]) && is_f32(op) && op->src[0]->nb[0] == 4;
         default:
             return false;
     }
@@ -392,7 +400,12 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     // epilogues of matrix m (node position pm): silu, or rope (+ its cache store), or a cache store
     auto add_epilogues = [&](int m, int pm) {
         ggml_tensor * mm = mms[m];
-        if (ggml_tensor * sl = silu_after(g, pm, n)) {
+        // SiLU of the gate projection: by default left to the FFN-product kernel (op_compute,
+        // GGML_OP_UNARY), which forms silu(gate)*up in one pass — the epilogue parks the row
+        // sums and costs the 66 MB gate/up launch ~2 us (scripts/probe_mall.py);
+        // GGML_MI355X_SILU_EPI=1 keeps it in the GEMV
+        static const bool silu_epi = getenv("GGML_MI355X_SILU_EPI") && atoi(getenv("GGML_MI355X_SILU_EPI")) != 0;
+        if (ggml_tensor * sl = silu_epi ? silu_after(g, pm, n) : nullptr) {
             const ggml_tensor * o[1] = {sl};
             if (!overlaps_any(sl, outs, mm) && (pm == i || can_hoist(g, i, pm + 1, o, 1, absorbed))) {
                 epi.silu[m] = sl;
@@ -677,6 +690,30 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             op_scale(ctx, node);
             return 1;
         case GGML_OP_UNARY:
+            // gated FFN: SILU(gate) -> MUL(., up) -> MUL_MAT down in one pass that also quantizes
+            // the down projection's input (src/llama-graph.cpp:555-616 LLM_FFN_SILU + PAR)
+            // (graph order is gate, SILU, up, MUL: the up projection ran in the gate's grouped
+            // launch, so the MUL is hoisted over it when nothing in between is touched)
+            if (fusion_enabled() && ggml_get_unary_op(node) == GGML_UNARY_OP_SILU) {
+                for (int j = i + 1; j < n && j <= i + 4; ++j) {
+                    ggml_tensor * c = ggml_graph_node(cgraph, j);
+                    if (c->op == GGML_OP_MUL && c->src[0] == node && c->src[1] != node) {
+                        const ggml_tensor * o[1] = {c};
+                        const std::vector<const ggml_tensor *> skip(ctx.done.begin(), ctx.done.end());
+                        if (!computed_before(ctx, cgraph, c->src[1], i) || !can_hoist(cgraph, i, j, o, 1, skip)) break;
+                        ggml_tensor * mm = at(cgraph, j + 1, n);
+                        const bool ssilu = !dead_after(cgraph, n, i + 1, node, {c});
+                        const bool smul = !(mm && mm->op == GGML_OP_MUL_MAT && dead_after(cgraph, n, j + 1, c, {mm}));
+                        if (fused_silu_mul_quant(ctx, node, c, mm, ssilu, smul)) {
+                            if (j == i + 1) return 2;
+                            ctx.done.push_back(c);
+                            return 1;
+                        }
+                        break;
+                    }
+                    if (!is_view_op(c) && std::find(ctx.done.begin(), ctx.done.end(), c) == ctx.done.end()) break;
+                }
+            }
             op_unary(ctx, node);
             return 1;
         case GGML_OP_CPY:
@@ -692,6 +729,15 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             return 1;
         case GGML_OP_SOFT_MAX:
             op_soft_max(ctx, node);
+            return 1;
+        case GGML_OP_MUL_MAT_ID:
+            op_mul_mat_id(ctx, node);
+            return 1;
+        case GGML_OP_ARGSORT:
+            op_argsort(ctx, node);
+            return 1;
+        case GGML_OP_SUM_ROWS:
+            op_sum_rows(ctx, node);
             return 1;
         case GGML_OP_FLASH_ATTN_EXT: {
             // attention output -> reshape -> output projection: quantize in the FA epilogue

@@ -622,4 +622,73 @@ void op_soft_max(exec_ctx & ctx, ggml_tensor * dst) {
                        mask && mask->type == GGML_TYPE_F16 ? 1 : 0, scale, max_bias, m0, m1, n_head_log2);
 }
 
+// ------------------------------------------------------------------------------------------
+// ARGSORT (ops.cpp:6956-6993; ggml_top_k of the MoE router, src/llama-graph.cpp:694): the
+// CPU's exchange sort restated per row — for j, every later k whose value orders before
+// position j's swaps with it — so ties resolve exactly as on the CPU.  One workgroup per
+// row, the row and its index permutation in LDS, the exchange loop on one lane (router
+// rows are n_expert long; supports_op caps ne0).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_argsort(const char * __restrict__ x, t4 tx, char * __restrict__ d, t4 td, int order) {
+    extern __shared__ __attribute__((aligned(16))) char sm[];
+    const int n = (int) tx.ne[0];
+    float * v = (float *) sm;
+    int * ix = (int *) (v + n);
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % tx.ne[1], i2 = (r / tx.ne[1]) % tx.ne[2], i3 = r / (tx.ne[1] * tx.ne[2]);
+    const char * xr = x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3];
+    char * dr = d + i1 * td.nb[1] + i2 * td.nb[2] + i3 * td.nb[3];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        v[i] = *(const float *) (xr + i * tx.nb[0]);
+        ix[i] = i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int j = 0; j < n; ++j) {
+            for (int k = j + 1; k < n; ++k) {
+                const float a = v[ix[j]], b = v[ix[k]];
+                if ((order == GGML_SORT_ORDER_ASC && a > b) || (order == GGML_SORT_ORDER_DESC && a < b)) {
+                    const int tmp = ix[j];
+                    ix[j] = ix[k];
+                    ix[k] = tmp;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) *(int32_t *) (dr + i * td.nb[0]) = ix[i];
+}
+
+void op_argsort(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * src = dst->src[0];
+    const int64_t nrows = ggml_nrows(src);
+    if (nrows == 0 || src->ne[0] == 0) return;
+    const int order = dst->op_params[0];
+    const size_t lds = (size_t) src->ne[0] * (sizeof(float) + sizeof(int));
+    hipLaunchKernelGGL(k_argsort, dim3((unsigned) nrows), dim3(64), lds, ctx.stream, (const char *) src->data, mk(src),
+                       (char *) dst->data, mk(dst), order);
+}
+
+// ------------------------------------------------------------------------------------------
+// SUM_ROWS (ops.cpp:1956-1986 with ggml_vec_sum_f32, vec.h:908: sequential double sum,
+// rounded once): one lane per row, the CPU's order
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_sum_rows(const char * __restrict__ x, t4 tx, char * __restrict__ d, t4 td, int64_t nrows) {
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrows) return;
+    const int64_t i1 = r % tx.ne[1], i2 = (r / tx.ne[1]) % tx.ne[2], i3 = r / (tx.ne[1] * tx.ne[2]);
+    const char * xr = x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3];
+    double s = 0.0;
+    for (int64_t i = 0; i < tx.ne[0]; ++i) s += (double) *(const float *) (xr + i * tx.nb[0]);
+    *(float *) (d + i1 * td.nb[1] + i2 * td.nb[2] + i3 * td.nb[3]) = (float) s;
+}
+
+void op_sum_rows(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * src = dst->src[0];
+    const int64_t nrows = ggml_nrows(src);
+    if (nrows == 0) return;
+    hipLaunchKernelGGL(k_sum_rows, dim3((unsigned) ceil_div(nrows, 64)), dim3(64), 0, ctx.stream, (const char *) src->data,
+                       mk(src), (char *) dst->data, mk(dst), nrows);
+}
+
 }  // namespace mi355x

@@ -133,6 +133,10 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
     __shared__ uint32_t wflag[4];    // per wave: batches needing the general step (mask / max update)
     __shared__ int wlast[4];
     __shared__ float wmax[4];
+    if (blockIdx.y >= a.warm_y0) {   // a warm workgroup: stream the next weights during attention
+        warm_run(a.warm, (int) ((blockIdx.y - a.warm_y0) * gridDim.x + blockIdx.x), (uint8_t *) vl, 4);
+        return;
+    }
 
     // q of this head, f16-rounded, in the quad layout of dot_f16_avx512_q4
     float qf[NM][4];
@@ -276,15 +280,20 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
             // coefficients are read from LDS while batch n computes
             // (a prefetch past the chunk end reads other LDS arrays or past the allocation, which
             // reads as 0 — never used: batches at or past nrun do not run)
-            auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
+            // batch n+1's V values and coefficients (vs, ms, mask) come from LDS while batch n
+            // computes; the general step selects instead of branching, so it never waits on an
+            // LDS value to decide (a readfirstlane per position cost ~140 ns in phase 3)
+            auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U], float (&ms)[U], float (&mv)[U]) {
                 const uint16_t * vp = vl + j * D + d;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     vv[u] = vp[u * D];
                     vs[u] = sc[j + u];
+                    ms[u] = cm[j + u];
+                    mv[u] = mk[j + u];
                 }
             };
-            auto run = [&](int j, const uint32_t (&vv)[U], const float (&vs)[U]) {
+            auto run = [&](int j, const uint32_t (&vv)[U], const float (&vs)[U], const float (&ms)[U], const float (&mv)[U]) {
                 if (((bmask >> (j / U)) & 1u) == 0) {
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -293,30 +302,32 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
                     }
                     return;
                 }
+                // masked / padded position: the state is kept (-0 must survive); a running-max
+                // update (ms != 1): y = f16(y*ms), S = S*ms before the add — the CPU's
+                // vec_scale_f16 / S*ms (ops.cpp:7120-7160); otherwise y*1 and S*1 are skipped
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (__builtin_amdgcn_readfirstlane(__float_as_uint(mk[j + u])) == 0xff800000u) continue;
-                    const uint32_t msb = __builtin_amdgcn_readfirstlane(__float_as_uint(cm[j + u]));
-                    if (msb != 0x3f800000u) {
-                        const float ms = __uint_as_float(msb);
-                        float t = __fmul_rn(h2f((uint16_t) yb), ms);
-                        asm("" : "+v"(t));   // two roundings, as f16r
-                        yb = f2h(t);
-                        S = __fmul_rn(S, ms);
-                    }
-                    yb = f16_mad(vv[u], vs[u], yb);
-                    S = __fadd_rn(S, vs[u]);
+                    const bool live = __float_as_uint(mv[u]) != 0xff800000u;
+                    const bool upd = __float_as_uint(ms[u]) != 0x3f800000u;
+                    float t = __fmul_rn(h2f((uint16_t) yb), ms[u]);
+                    asm("" : "+v"(t));   // two roundings, as f16r
+                    const uint32_t ys = upd ? (uint32_t) f2h(t) : yb;
+                    const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
+                    const uint32_t yn = f16_mad(vv[u], vs[u], ys);
+                    const float Sn = __fadd_rn(Ss, vs[u]);
+                    yb = live ? yn : yb;
+                    S = live ? Sn : S;
                 }
             };
             uint32_t va[U], vb[U];
-            float sa[U], sb[U];
-            ldb(0, va, sa);
+            float sa[U], sb[U], ma[U], mb[U], ka[U], kb[U];
+            ldb(0, va, sa, ma, ka);
             for (int j = 0; j < nrun; j += 2 * U) {
-                ldb(j + U, vb, sb);
-                run(j, va, sa);
+                ldb(j + U, vb, sb, mb, kb);
+                run(j, va, sa, ma, ka);
                 if (j + U >= nrun) break;
-                ldb(j + 2 * U, va, sa);
-                run(j + U, vb, sb);
+                ldb(j + 2 * U, va, sa, ma, ka);
+                run(j + U, vb, sb, mb, kb);
             }
         }
         __syncthreads();
@@ -374,9 +385,13 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
     }
 }
 
-void launch_fattn_exact(hipStream_t st, const fa_args & a, int64_t nq3) {
-    GGML_ASSERT(a.H % a.Hkv == 0);
-    const dim3 grid((unsigned) a.n_q, (unsigned) (a.H * nq3));
+void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
+    GGML_ASSERT(a0.H % a0.Hkv == 0);
+    fa_args a = a0;
+    a.warm_y0 = a.H * nq3;
+    const int64_t wy = a.warm.nwg ? ceil_div(a.warm.nwg, a.n_q) : 0;
+    a.warm.nwg = (int) (wy * a.n_q);
+    const dim3 grid((unsigned) a.n_q, (unsigned) (a.H * nq3 + wy));
     switch (a.D) {
         case 64:  hipLaunchKernelGGL(k_fattn_exact<64>, grid, dim3(256), 0, st, a); break;
         case 128: hipLaunchKernelGGL(k_fattn_exact<128>, grid, dim3(256), 0, st, a); break;

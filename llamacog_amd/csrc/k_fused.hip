@@ -26,6 +26,8 @@ struct norm_fused_args {
     float eps;
     int qmode;                          // 0 none, 1 Q8_K, 2 Q8_0 (of yw if w else y)
     int8_t * qs; float * qd; int16_t * qsum;
+    int64_t nrows;
+    warm_spec warm;                     // Infinity-Cache warm of the next weights (warm.h)
 };
 
 // one workgroup of BT = min(ne0/4, 1024) threads per row; thread t owns the float4s at
@@ -41,7 +43,16 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
     const int64_t ro = row * p.ne0;
     __shared__ double qp[NV * 16][64];
     __shared__ double tot;
-    float4 v[NV];
+    if (row >= p.nrows) {   // a warm workgroup: stream the next weights while the rows reduce
+        warm_run(p.warm, (int) (row - p.nrows), (uint8_t *) qp, 8 * NV);
+        return;
+    }
+    float4 v[NV], wv[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        // the norm weight is loaded with the row, not after the reduction
+        if (p.w) wv[k] = *(const float4 *) (p.w + 4 * (tid + BT * k));
+    }
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int64_t e = 4 * (tid + BT * k);
@@ -79,7 +90,7 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
         y.z = __fmul_rn(v[k].z, scale); y.w = __fmul_rn(v[k].w, scale);
         *(float4 *) (p.y + ro + e) = y;
         if (p.w) {
-            const float4 ww = *(const float4 *) (p.w + e);
+            const float4 ww = wv[k];
             y.x = __fmul_rn(y.x, ww.x); y.y = __fmul_rn(y.y, ww.y);
             y.z = __fmul_rn(y.z, ww.z); y.w = __fmul_rn(y.w, ww.w);
             *(float4 *) (p.yw + ro + e) = y;
@@ -94,29 +105,51 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
     }
 }
 
-// dst = a*b (same shape, contiguous) and its quantization; one wave per 256 elements
-template <int QMODE>
+// dst = a*b (same shape, contiguous) and its quantization; one wave per 256 elements.
+// SILU: a is the gate projection and the kernel first forms s = silu(a) — the UNARY node
+// before the MUL, ggml_vec_silu_f32's arithmetic (vec.cpp:233: AVX-512 ggml_v_silu on
+// 16-element chunks of the row, x/(1+expf(-x)) on the tail) — storing it only when a later
+// node reads it (sdst != nullptr).  dst == nullptr: the product is read by nothing but the
+// quantized activation (QMODE 0 keeps no quantization and always stores).
+template <int QMODE, bool SILU>
 __global__ __launch_bounds__(64) void k_mul_quant(const float * __restrict__ a, const float * __restrict__ b,
                                                   float * __restrict__ dst, int64_t K,
                                                   int8_t * __restrict__ qs, float * __restrict__ qd,
-                                                  int16_t * __restrict__ qsum) {
+                                                  int16_t * __restrict__ qsum, float * __restrict__ sdst,
+                                                  const warm_spec warm) {
     const int lane = threadIdx.x;
     const int64_t row = blockIdx.y;
+    const int64_t nblk = (K + 255) / 256;
+    if (blockIdx.x >= nblk) {   // a warm workgroup (decode): stream the down projection's weights
+        __shared__ __attribute__((aligned(16))) uint8_t wl[1024];
+        warm_run(warm, (int) (blockIdx.x - nblk), wl, 1);
+        return;
+    }
     const int64_t c0 = (int64_t) blockIdx.x * 256;
     const int64_t e0 = c0 + 4 * lane;
     const bool valid = e0 < K;
     float q[4] = {0.f, 0.f, 0.f, 0.f};
     if (valid) {
-        const float4 x = *(const float4 *) (a + row * K + e0);
+        float4 x = *(const float4 *) (a + row * K + e0);
         const float4 y = *(const float4 *) (b + row * K + e0);
+        if constexpr (SILU) {
+            const int64_t nvec = (K / 16) * 16;
+            float v[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                v[c] = e0 + c < nvec ? v[c] / (1.0f + v_expf_avx512(-v[c])) : v[c] / (1.0f + expf_cr(-v[c]));
+            }
+            x = make_float4(v[0], v[1], v[2], v[3]);
+            if (sdst) *(float4 *) (sdst + row * K + e0) = x;
+        }
         float4 r;
         r.x = __fmul_rn(x.x, y.x); r.y = __fmul_rn(x.y, y.y); r.z = __fmul_rn(x.z, y.z); r.w = __fmul_rn(x.w, y.w);
-        *(float4 *) (dst + row * K + e0) = r;
+        if (dst) *(float4 *) (dst + row * K + e0) = r;
         q[0] = r.x; q[1] = r.y; q[2] = r.z; q[3] = r.w;
     }
     if constexpr (QMODE == 1) {
         q8K_wave(q, lane, qs + row * K + c0, qsum + row * (K / 16) + c0 / 16, qd + row * (K / 256) + c0 / 256);
-    } else {
+    } else if constexpr (QMODE == 2) {
         q8_0_wave(q, lane, valid, qs + row * K + c0, qd + row * (K / 32) + c0 / 32, qsum + row * (K / 32) + c0 / 32);
     }
 }
@@ -170,34 +203,55 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     }
     const int nv = ne0 <= 4096 ? 1 : (int) (ne0 / 4096);
     const dim3 block((unsigned) (ne0 / (4 * nv)));
+    p.nrows = nrows;
+    p.warm.nseg = 0; p.warm.nwg = 0;
+    if (nrows == 1 && block.x >= 256) p.warm = ctx.warm_take(WARM_NORM);   // decode only
+    const dim3 grid((unsigned) (nrows + p.warm.nwg));
     switch (nv) {
-        case 1: hipLaunchKernelGGL(k_norm_fused<1>, dim3((unsigned) nrows), block, 0, ctx.stream, p); break;
-        case 2: hipLaunchKernelGGL(k_norm_fused<2>, dim3((unsigned) nrows), block, 0, ctx.stream, p); break;
-        case 3: hipLaunchKernelGGL(k_norm_fused<3>, dim3((unsigned) nrows), block, 0, ctx.stream, p); break;
-        default: hipLaunchKernelGGL(k_norm_fused<4>, dim3((unsigned) nrows), block, 0, ctx.stream, p); break;
+        case 1: hipLaunchKernelGGL(k_norm_fused<1>, grid, block, 0, ctx.stream, p); break;
+        case 2: hipLaunchKernelGGL(k_norm_fused<2>, grid, block, 0, ctx.stream, p); break;
+        case 3: hipLaunchKernelGGL(k_norm_fused<3>, grid, block, 0, ctx.stream, p); break;
+        default: hipLaunchKernelGGL(k_norm_fused<4>, grid, block, 0, ctx.stream, p); break;
     }
     if (qmode) ctx.qcache_put(out, qmode == 1, act);
     return true;
 }
 
 bool fused_mul_quant(exec_ctx & ctx, ggml_tensor * mul, const ggml_tensor * mm) {
+    return fused_silu_mul_quant(ctx, nullptr, mul, mm, true);
+}
+
+// [SILU ->] MUL (a * b) -> quantized activation of the consuming MUL_MAT.  silu: the UNARY SILU
+// node that is mul's src[0] (nullptr: mul alone); store_silu / store_mul: whether those outputs
+// are read by any later node (dispatch.cpp dead_after), else only the quantization is kept.
+bool fused_silu_mul_quant(exec_ctx & ctx, ggml_tensor * silu, ggml_tensor * mul, const ggml_tensor * mm, bool store_silu,
+                          bool store_mul) {
     if (!f32_contig(mul) || !f32_contig(mul->src[0]) || !f32_contig(mul->src[1])) return false;
     if (!ggml_are_same_shape(mul->src[0], mul->src[1]) || !ggml_are_same_shape(mul, mul->src[0])) return false;
+    if (silu && (mul->src[0] != silu || !f32_contig(silu->src[0]) || !ggml_are_same_shape(silu, silu->src[0]))) return false;
     const int qmode = consumer_qmode(mm, mul);
-    if (!qmode || mul->ne[0] % 4 != 0) return false;
+    if (mul->ne[0] % 4 != 0 || (!qmode && !silu)) return false;
+    if (!qmode) store_mul = true;
     const int64_t K = mul->ne[0], nrows = ggml_nrows(mul);
     const bool kq = qmode == 1;
-    q8_act act;
-    carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(K, nrows, kq)), K, nrows, kq);
-    const dim3 grid((unsigned) ceil_div(K, 256), (unsigned) nrows);
-    if (kq) {
-        hipLaunchKernelGGL(k_mul_quant<1>, grid, dim3(64), 0, ctx.stream, (const float *) mul->src[0]->data,
-                           (const float *) mul->src[1]->data, (float *) mul->data, K, act.qs, act.d, act.s);
+    q8_act act = {};
+    if (qmode) carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(K, nrows, kq)), K, nrows, kq);
+    warm_spec warm;
+    warm.nseg = 0; warm.nwg = 0;
+    if (nrows == 1) warm = ctx.warm_take(WARM_MULQ);
+    const dim3 grid((unsigned) (ceil_div(K, 256) + warm.nwg), (unsigned) nrows);
+    const float * a = (const float *) (silu ? silu->src[0]->data : mul->src[0]->data);
+    const float * b = (const float *) mul->src[1]->data;
+    float * d = store_mul ? (float *) mul->data : nullptr;
+    float * sd = silu && store_silu ? (float *) silu->data : nullptr;
+#define MQ_LAUNCH(Q, S) hipLaunchKernelGGL((k_mul_quant<Q, S>), grid, dim3(64), 0, ctx.stream, a, b, d, K, act.qs, act.d, act.s, sd, warm)
+    if (silu) {
+        if (qmode == 1) MQ_LAUNCH(1, true); else if (qmode == 2) MQ_LAUNCH(2, true); else MQ_LAUNCH(0, true);
     } else {
-        hipLaunchKernelGGL(k_mul_quant<2>, grid, dim3(64), 0, ctx.stream, (const float *) mul->src[0]->data,
-                           (const float *) mul->src[1]->data, (float *) mul->data, K, act.qs, act.d, act.s);
+        if (qmode == 1) MQ_LAUNCH(1, false); else MQ_LAUNCH(2, false);
     }
-    ctx.qcache_put(mul, kq, act);
+#undef MQ_LAUNCH
+    if (qmode) ctx.qcache_put(mul, kq, act);
     return true;
 }
 

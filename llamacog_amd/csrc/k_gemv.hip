@@ -341,6 +341,7 @@ struct gemv_args {
     rope_params rp;
     const int32_t * rope_pos; const float * rope_ff; int64_t rope_d;
     int need_pairs;
+    const float2 * rtab_g;                // the graph's cos/sin table of the position (rope_table)
     // activation prologue (instead of a separate producer kernel), K-quant weights, one wave
     // covering a row's tasks per WPR group:
     //   pro 1: x = pa (+ pb); y = rms_norm(x) (eps); yw = y * pw; act = Q8_K(yw)
@@ -627,9 +628,13 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const
         }
         if (p.need_pairs) {
             for (int ip = threadIdx.x; ip < p.rp.n_dims / 2; ip += NT) {
-                float c, sn;
-                rope_cs(p.rp, (float) p.rope_pos[0], ip, p.rope_ff, c, sn);
-                rtab[ip] = make_float2(c, sn);
+                if (p.rtab_g) {
+                    rtab[ip] = p.rtab_g[ip];
+                } else {
+                    float c, sn;
+                    rope_cs(p.rp, (float) p.rope_pos[0], ip, p.rope_ff, c, sn);
+                    rtab[ip] = make_float2(c, sn);
+                }
             }
         }
         __syncthreads();
@@ -699,6 +704,37 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const
             if (row < p.M[mi]) gemv_store(p, mi, p.M[mi], row, res[i], res[RPG > 1 ? i ^ 1 : i], rtab, f16p);
         }
     }
+}
+
+// cos/sin of every rope pair at the token's position (one token), once per graph: rope_cs,
+// the arithmetic of the stand-alone ROPE kernel, so the fused epilogue's bits do not change.
+// Built per pair by a chain of up to n_dims/2 dependent multiplies (theta *= theta_scale, as
+// ggml_rope_cache_init) plus double-precision cos/sin — ~4 us of latency that every
+// workgroup of every Q/K projection paid before the table was shared.
+__global__ __launch_bounds__(256) void k_rope_table(const rope_params rp, const int32_t * __restrict__ pos,
+                                                    const float * __restrict__ ff, float2 * __restrict__ tab) {
+    for (int ip = threadIdx.x; ip < rp.n_dims / 2; ip += blockDim.x) {
+        float c, sn;
+        rope_cs(rp, (float) pos[0], ip, ff, c, sn);
+        tab[ip] = make_float2(c, sn);
+    }
+}
+
+// the table for a ROPE node's parameters and position tensor, launched on first use in the
+// graph (run_nodes clears the key: positions change every graph, the capture replays the
+// launch); slot 3 of the scratch arena holds it
+static const float2 * rope_table(exec_ctx & ctx, const ggml_tensor * r, const rope_params & rp, const int32_t * pos,
+                                 const float * ff) {
+    if (ctx.rt_table && ctx.rt_pos == pos && ctx.rt_ff == ff && memcmp(ctx.rt_params, r->op_params, sizeof(ctx.rt_params)) == 0) {
+        return ctx.rt_table;
+    }
+    float2 * tab = (float2 *) ctx.scratch(3, sizeof(float2) * GEMV_ROPE_MAXPAIRS);
+    hipLaunchKernelGGL(k_rope_table, dim3(1), dim3(256), 0, ctx.stream, rp, pos, ff, tab);
+    ctx.rt_table = tab;
+    ctx.rt_pos = pos;
+    ctx.rt_ff = ff;
+    memcpy(ctx.rt_params, r->op_params, sizeof(ctx.rt_params));
+    return tab;
 }
 
 // ---- host ----------------------------------------------------------------------------------------
@@ -927,6 +963,15 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
             a.rope_ff = r->src[2] ? (const float *) r->src[2]->data : nullptr;
             a.rope_d = r->src[0]->ne[0];
             a.need_pairs = 1;
+        }
+    }
+    a.rtab_g = nullptr;
+    if (a.need_pairs && a.rp.n_dims <= 2 * GEMV_ROPE_MAXPAIRS) {
+        static const bool shared_tab = !getenv("GGML_MI355X_ROPE_TABLE") || atoi(getenv("GGML_MI355X_ROPE_TABLE")) != 0;
+        if (shared_tab) {
+            for (int i = 0; i < nmat; ++i) {
+                if (epi && epi->rope[i]) { a.rtab_g = rope_table(ctx, epi->rope[i], a.rp, a.rope_pos, a.rope_ff); break; }
+            }
         }
     }
     a.A = {act.qs, act.d, act.s};

@@ -19,6 +19,8 @@
 #include "ops.h"
 #include "quant_act.h"
 
+#include <algorithm>
+
 namespace mi355x {
 
 // ------------------------------------------------------------------------------------------
@@ -647,6 +649,272 @@ void mul_mat_vec(exec_ctx & ctx, ggml_tensor * dst, const q8_act * pre) {
             if (src0->type == GGML_TYPE_F16) hipLaunchKernelGGL(k_mmv_f_exact<uint16_t>, grid, dim3(256), 0, ctx.stream, a);
             else hipLaunchKernelGGL(k_mmv_f_exact<float>, grid, dim3(256), 0, ctx.stream, a);
         }
+    }
+    if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
+}
+
+// ------------------------------------------------------------------------------------------
+// MUL_MAT_ID (ggml-cpu/ggml-cpu.c:1466 ggml_compute_forward_mul_mat_id; graph use in
+// build_moe_ffn, src/llama-graph.cpp:727-758): for token t and slot e < n_used,
+//   dst[:, e, t] = as[ids[e, t]] . b[:, e % ne11, t]
+// with the per-row arithmetic of the mat-vec above (same quantized activation, same tasks).
+// The routing never leaves the device (the reference's CUDA path copies ids to the host,
+// ggml-cuda.cu:2061-2084):
+//   * few (slot, token) pairs (decode): one mat-vec per pair, the expert read from ids by
+//     the kernel (k_mmv_q_id);
+//   * many pairs (prefill): a one-workgroup counting sort groups the pairs by expert
+//     (k_moe_sort), the activations are quantized straight into that order
+//     (k_quant_gather), and each expert's rows are streamed once per 8 of its pairs
+//     (k_mmv_q_idg); workgroups past an expert's pair count exit at once.
+// ------------------------------------------------------------------------------------------
+struct mmv_id_args {
+    const uint8_t * W; int64_t nb01, nb02; int64_t M; int64_t nblk; int64_t n_as;
+    act_view A;
+    const char * ids; int64_t ids_nb0, ids_nb1; int64_t n_used; int64_t ne11;
+    float * dst; int64_t nb1, nb2;   // bytes
+    const int32_t * cnt; const int32_t * off; const int32_t * list;   // grouped mode
+};
+
+template <template <int> class TASK, int WPR>
+__global__ __launch_bounds__(256) void k_mmv_q_id(const mmv_id_args p) {
+    using T = TASK<1>;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int RPB = 4 / WPR;
+    const int64_t row = (int64_t) blockIdx.x * RPB + wave / WPR;
+    const int wsub = wave % WPR;
+    const int64_t e = blockIdx.y % p.n_used, t = blockIdx.y / p.n_used;
+    const int32_t ex = *(const int32_t *) (p.ids + e * p.ids_nb0 + t * p.ids_nb1);
+    const bool ok = row < p.M && ex >= 0 && ex < p.n_as;
+    float acc[1] = {0.0f};
+    if (ok) {
+        const uint8_t * wrow = p.W + (int64_t) ex * p.nb02 + row * p.nb01;
+        const int64_t col = e % p.ne11 + p.ne11 * t;
+        act_view A = p.A;
+        A.qs += col * A.qs_st; A.d += col * A.d_st; A.s += col * A.s_st;
+        const int ntasks = (int) (p.nblk * T::per_block);
+        for (int tk = wsub * WAVE + lane; tk < ntasks; tk += WAVE * WPR) T::run(wrow, tk, A, 1, acc);
+    }
+    acc[0] = wave_sum(acc[0]);
+    if constexpr (WPR > 1) {
+        __shared__ float red[4];
+        if (lane == 0) red[wave] = acc[0];
+        __syncthreads();
+        if (wsub == 0 && lane == 0) {
+            float s = red[wave];
+#pragma unroll
+            for (int w = 1; w < WPR; ++w) s += red[wave + w];
+            acc[0] = s;
+        }
+    }
+    if (ok && wsub == 0 && lane == 0) *(float *) ((char *) p.dst + e * p.nb1 + t * p.nb2 + row * 4) = acc[0];
+}
+
+template <template <int> class TASK, int NC, int WPR>
+__global__ __launch_bounds__(256) void k_mmv_q_idg(const mmv_id_args p) {
+    using T = TASK<NC>;
+    const int ex = blockIdx.z;
+    const int n = p.cnt[ex];
+    const int c0 = blockIdx.y * NC;
+    if (c0 >= n) return;   // uniform over the workgroup, before any barrier
+    const int nc = min(NC, n - c0);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr int RPB = 4 / WPR;
+    const int64_t row = (int64_t) blockIdx.x * RPB + wave / WPR;
+    const int wsub = wave % WPR;
+    const int64_t pos0 = p.off[ex] + c0;   // first expert-ordered activation column
+    float acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.0f;
+    if (row < p.M) {
+        const uint8_t * wrow = p.W + (int64_t) ex * p.nb02 + row * p.nb01;
+        act_view A = p.A;
+        A.qs += pos0 * A.qs_st; A.d += pos0 * A.d_st; A.s += pos0 * A.s_st;
+        const int ntasks = (int) (p.nblk * T::per_block);
+        for (int tk = wsub * WAVE + lane; tk < ntasks; tk += WAVE * WPR) T::run(wrow, tk, A, nc, acc);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = wave_sum(acc[c]);
+    if constexpr (WPR > 1) {
+        __shared__ float red[4][NC];
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) red[wave][c] = acc[c];
+        }
+        __syncthreads();
+        if (wsub == 0 && lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                float s = red[wave][c];
+#pragma unroll
+                for (int w = 1; w < WPR; ++w) s += red[wave + w][c];
+                acc[c] = s;
+            }
+        }
+    }
+    if (row < p.M && wsub == 0 && lane == 0) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (c >= nc) break;
+            const int pair = p.list[pos0 + c];
+            const int64_t e = pair % p.n_used, t = pair / p.n_used;
+            *(float *) ((char *) p.dst + e * p.nb1 + t * p.nb2 + row * 4) = acc[c];
+        }
+    }
+}
+
+// counting sort of the (slot, token) pairs by expert, one workgroup: cnt[x] pairs routed to
+// expert x, off[x] their first position (exclusive prefix), list[off[x] + k] = pair index
+// e + n_used * t.  The order inside an expert is immaterial: every pair's output depends
+// only on its own activation column.  Out-of-range ids (the CPU asserts on them) route nowhere.
+__global__ __launch_bounds__(256) void k_moe_sort(const char * __restrict__ ids, int64_t nb0, int64_t nb1, int64_t n_used,
+                                                  int64_t n_pairs, int n_as, int32_t * __restrict__ cnt,
+                                                  int32_t * __restrict__ off, int32_t * __restrict__ list) {
+    extern __shared__ int cur[];   // [n_as]
+    for (int x = threadIdx.x; x < n_as; x += blockDim.x) cur[x] = 0;
+    __syncthreads();
+    for (int64_t q = threadIdx.x; q < n_pairs; q += blockDim.x) {
+        const int32_t ex = *(const int32_t *) (ids + (q % n_used) * nb0 + (q / n_used) * nb1);
+        if (ex >= 0 && ex < n_as) atomicAdd(&cur[ex], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int x = 0; x < n_as; ++x) {
+            const int c = cur[x];
+            cnt[x] = c;
+            off[x] = acc;
+            cur[x] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (int64_t q = threadIdx.x; q < n_pairs; q += blockDim.x) {
+        const int32_t ex = *(const int32_t *) (ids + (q % n_used) * nb0 + (q / n_used) * nb1);
+        if (ex >= 0 && ex < n_as) list[atomicAdd(&cur[ex], 1)] = (int32_t) q;
+    }
+}
+
+// quantization of the activation column of each sorted pair into position order (the
+// quantizers of quant_act.h, so the bytes equal the unsorted quantization's)
+template <int QMODE>
+__global__ __launch_bounds__(64) void k_quant_gather(const char * __restrict__ x, int64_t K, int64_t nb11, int64_t nb12,
+                                                     int64_t ne11, int64_t n_used, const int32_t * __restrict__ list,
+                                                     const int32_t * __restrict__ cnt, const int32_t * __restrict__ off,
+                                                     int n_as, int8_t * __restrict__ qs, float * __restrict__ qd,
+                                                     int16_t * __restrict__ qsum) {
+    const int lane = threadIdx.x;
+    const int64_t j = blockIdx.y;
+    if (j >= off[n_as - 1] + cnt[n_as - 1]) return;
+    const int pair = list[j];
+    const int64_t e = pair % n_used, t = pair / n_used;
+    const float * row = (const float *) (x + (e % ne11) * nb11 + t * nb12);
+    const int64_t c0 = (int64_t) blockIdx.x * 256, e0 = c0 + 4 * lane;
+    const bool valid = e0 < K;
+    float q[4] = {0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+        const uint4 v = ld16(row + e0);
+        q[0] = __uint_as_float(v.x); q[1] = __uint_as_float(v.y); q[2] = __uint_as_float(v.z); q[3] = __uint_as_float(v.w);
+    }
+    if constexpr (QMODE == 1) {
+        q8K_wave(q, lane, qs + j * K + c0, qsum + j * (K / 16) + c0 / 16, qd + j * (K / 256) + c0 / 256);
+    } else {
+        q8_0_wave(q, lane, valid, qs + j * K + c0, qd + j * (K / 32) + c0 / 32, qsum + j * (K / 32) + c0 / 32);
+    }
+}
+
+bool mul_mat_id_supported(const ggml_tensor * op) {
+    const ggml_tensor * as = op->src[0];
+    const ggml_tensor * b = op->src[1];
+    const ggml_tensor * ids = op->src[2];
+    if (!as || !b || !ids) return false;
+    if (!mmv_q_supported_type(as->type) || as->nb[0] != ggml_type_size(as->type)) return false;
+    if (b->type != GGML_TYPE_F32 || b->nb[0] != sizeof(float) || op->type != GGML_TYPE_F32 || op->nb[0] != sizeof(float)) return false;
+    if (ids->type != GGML_TYPE_I32) return false;
+    if (as->ne[0] % (is_k_quant(as->type) ? 256 : 32) != 0 || b->ne[0] != as->ne[0]) return false;
+    if (as->ne[3] != 1 || b->ne[3] != 1 || ids->ne[2] != 1 || ids->ne[3] != 1) return false;
+    return b->ne[2] == ids->ne[1] && op->ne[1] == ids->ne[0] && op->ne[2] == ids->ne[1] && as->ne[2] <= 4096;
+}
+
+template <template <int> class TASK>
+static void launch_mmv_id(hipStream_t st, const mmv_id_args & a, int64_t n_pairs, bool grouped) {
+    const int64_t waves = a.M * (grouped ? ceil_div(n_pairs, 8 * a.n_as) : n_pairs);
+    const int wpr = waves >= 8192 ? 1 : (waves >= 2048 ? 2 : 4);
+    const unsigned rb = (unsigned) ceil_div(a.M, 4 / wpr);
+    if (!grouped) {
+        const dim3 grid(rb, (unsigned) n_pairs);
+        if (wpr == 1) hipLaunchKernelGGL((k_mmv_q_id<TASK, 1>), grid, dim3(256), 0, st, a);
+        else if (wpr == 2) hipLaunchKernelGGL((k_mmv_q_id<TASK, 2>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_mmv_q_id<TASK, 4>), grid, dim3(256), 0, st, a);
+        return;
+    }
+    const dim3 grid(rb, (unsigned) ceil_div(n_pairs, 8), (unsigned) a.n_as);
+    if (wpr == 1) hipLaunchKernelGGL((k_mmv_q_idg<TASK, 8, 1>), grid, dim3(256), 0, st, a);
+    else if (wpr == 2) hipLaunchKernelGGL((k_mmv_q_idg<TASK, 8, 2>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_mmv_q_idg<TASK, 8, 4>), grid, dim3(256), 0, st, a);
+}
+
+void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst) {
+    const ggml_tensor * as = dst->src[0];
+    const ggml_tensor * b = dst->src[1];
+    const ggml_tensor * ids = dst->src[2];
+    const bool kq = is_k_quant(as->type);
+    const int64_t K = as->ne[0];
+    const int64_t n_used = ids->ne[0], T = ids->ne[1], n_pairs = n_used * T;
+    const int n_as = (int) as->ne[2];
+    if (n_pairs == 0) return;
+
+    hipEvent_t ev_beg = nullptr;
+    // algorithmic bytes: one pass over the rows of every routed expert (at most n_pairs of them)
+    const double bytes = (double) as->nb[2] * (double) std::min<int64_t>(n_pairs, n_as) +
+                         (double) ggml_nelements(b) * (kq ? 1.14 : 1.0) + (double) ggml_nbytes(dst);
+    if (ctx.timing) ctx.time_begin(TK_MMV, bytes, ev_beg);
+
+    mmv_id_args a;
+    a.W = (const uint8_t *) as->data;
+    a.nb01 = as->nb[1]; a.nb02 = as->nb[2];
+    a.M = as->ne[1];
+    a.nblk = K / ggml_blck_size(as->type);
+    a.n_as = n_as;
+    a.ids = (const char *) ids->data; a.ids_nb0 = ids->nb[0]; a.ids_nb1 = ids->nb[1];
+    a.n_used = n_used; a.ne11 = b->ne[1];
+    a.dst = (float *) dst->data; a.nb1 = dst->nb[1]; a.nb2 = dst->nb[2];
+    a.cnt = a.off = a.list = nullptr;
+
+    const bool grouped = n_pairs > 8;
+    q8_act act;
+    if (!grouped) {
+        if (!ctx.qcache_get(b, kq, act)) {
+            quantize_act(ctx, b, kq, act, exec_ctx::QSLOT);
+            ctx.qcache_put(b, kq, act);
+        }
+    } else {
+        auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
+        const size_t ib = al(sizeof(int32_t) * (size_t) (2 * n_as + n_pairs));
+        char * base = (char *) ctx.scratch(2, ib + q8_act::bytes(K, n_pairs, kq));
+        int32_t * cnt = (int32_t *) base;
+        int32_t * off = cnt + n_as;
+        int32_t * list = off + n_as;
+        carve_act(act, base + ib, K, n_pairs, kq);
+        hipLaunchKernelGGL(k_moe_sort, dim3(1), dim3(256), sizeof(int) * n_as, ctx.stream, (const char *) ids->data,
+                           (int64_t) ids->nb[0], (int64_t) ids->nb[1], n_used, n_pairs, n_as, cnt, off, list);
+        const dim3 qg((unsigned) ceil_div(K, 256), (unsigned) n_pairs);
+        if (kq) {
+            hipLaunchKernelGGL(k_quant_gather<1>, qg, dim3(64), 0, ctx.stream, (const char *) b->data, K, (int64_t) b->nb[1],
+                               (int64_t) b->nb[2], (int64_t) b->ne[1], n_used, list, cnt, off, n_as, act.qs, act.d, act.s);
+        } else {
+            hipLaunchKernelGGL(k_quant_gather<2>, qg, dim3(64), 0, ctx.stream, (const char *) b->data, K, (int64_t) b->nb[1],
+                               (int64_t) b->nb[2], (int64_t) b->ne[1], n_used, list, cnt, off, n_as, act.qs, act.d, act.s);
+        }
+        a.cnt = cnt; a.off = off; a.list = list;
+    }
+    a.A = {act.qs, act.d, act.s, act.qs_stride(), act.d_stride(), act.s_stride()};
+    switch (as->type) {
+        case GGML_TYPE_Q4_K: launch_mmv_id<task_q4_K>(ctx.stream, a, n_pairs, grouped); break;
+        case GGML_TYPE_Q5_K: launch_mmv_id<task_q5_K>(ctx.stream, a, n_pairs, grouped); break;
+        case GGML_TYPE_Q6_K: launch_mmv_id<task_q6_K>(ctx.stream, a, n_pairs, grouped); break;
+        case GGML_TYPE_Q8_0: launch_mmv_id<task_q8_0>(ctx.stream, a, n_pairs, grouped); break;
+        case GGML_TYPE_Q4_0: launch_mmv_id<task_q4_0>(ctx.stream, a, n_pairs, grouped); break;
+        default: GGML_ABORT("mi355x: unsupported mul_mat_id type");
     }
     if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
 }

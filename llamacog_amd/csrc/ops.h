@@ -4,6 +4,7 @@
 #pragma once
 
 #include "common.h"
+#include "warm.h"
 
 #include <vector>
 
@@ -53,6 +54,23 @@ struct exec_ctx {
     bool                qc_kquant = false;
     q8_act              qc_act;
     void qcache_clear() { qc_tensor = nullptr; qc_data = nullptr; }
+
+    // per-graph RoPE cos/sin table (k_gemv.hip rope_table): every layer's fused Q/K rope
+    // epilogue reads the same table of the token's position, built once per graph
+    const float2 *  rt_table = nullptr;
+    const void *    rt_pos = nullptr;
+    const void *    rt_ff = nullptr;
+    int32_t         rt_params[15] = {};
+
+    // Infinity-Cache warming (warm.h): the decode mat-vec weights of the current graph in
+    // node order and the cursor up to which latency-bound kernels have already warmed them
+    struct warm_seg { int node; const uint8_t * p; int64_t n; };
+    std::vector<warm_seg> warm_list;
+    size_t  warm_cur = 0;
+    int64_t warm_off = 0;
+    int     cur_node = 0;              // graph position being dispatched (run_nodes)
+    void      warm_plan(ggml_cgraph * g);   // backend.cpp
+    warm_spec warm_take(int kind);          // the next bytes after cur_node for a kernel of `kind`
 
     // nodes already computed ahead of their position by a grouped launch (dispatch.cpp)
     std::vector<const ggml_tensor *> done;
@@ -171,6 +189,8 @@ void carve_act(q8_act & act, void * base, int64_t K, int64_t ncols, bool k_quant
 // fused producers (k_fused.hip); false = pattern not applicable, nothing launched
 bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm);
 bool fused_mul_quant(exec_ctx & ctx, ggml_tensor * mul, const ggml_tensor * mm);
+bool fused_silu_mul_quant(exec_ctx & ctx, ggml_tensor * silu, ggml_tensor * mul, const ggml_tensor * mm, bool store_silu,
+                          bool store_mul = true);
 
 void quantize_act_raw(hipStream_t stream, const float * x, int64_t K, int64_t ncols, int64_t row_stride_elems,
                       bool k_quant, q8_act & act);

@@ -78,6 +78,9 @@ CONFIGS = {
     # small fast model with every weight type exercised (CPU tests)
     "tiny-q4km": ModelConfig("tiny-synthetic", 512, 4, 8, 2, 1024, 4096, "q4_k_m", n_ctx_train=2048),
     "tiny-q8_0": ModelConfig("tiny-q8-synthetic", 512, 4, 8, 2, 1024, 4096, "q8_0", n_ctx_train=2048),
+    # small Mixtral-style MoE (4 experts, top-2), Q5_K_M
+    "tiny-moe-q5km": ModelConfig("tiny-moe-synthetic", 512, 4, 8, 2, 1024, 4096, "q5_k_m", n_ctx_train=2048,
+                                 n_expert=4, n_expert_used=2),
 }
 
 

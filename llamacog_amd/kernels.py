@@ -40,6 +40,9 @@ def lib():
         L.mi355x_soft_max.argtypes = [P, I64, I64, P, I64, F, P, P]
         L.mi355x_silu.argtypes = [P, I64, I64, P, P]
         L.mi355x_flash_attn.argtypes = [P, P, P, P, ctypes.c_int, I64, I64, I64, I64, I64, F, F, P, P]
+        L.mi355x_mul_mat_id.argtypes = [ctypes.c_int, P, I64, I64, I64, P, I64, I64, P, I64, I64, P, P]
+        L.mi355x_argsort.argtypes = [P, I64, I64, ctypes.c_int, P, P]
+        L.mi355x_sum_rows.argtypes = [P, I64, I64, P, P]
         _lib = L
     return _lib
 
@@ -149,3 +152,31 @@ def flash_attn(q, k, v, mask_u16, kv_type, D, H, Hkv, n_kv, scale, softcap=0.0):
     _chk(lib().mi355x_flash_attn(dq.ptr, dk.ptr, dv.ptr, dm.ptr if dm else None, kv_type, D, n_q, H, n_kv, Hkv, scale,
                                  softcap, do.ptr, None), "flash_attn")
     return do.get(np.float32, (n_q, H, D))
+
+
+def mul_mat_id(wtype: int, wq: np.ndarray, K: int, M: int, n_as: int, ids: np.ndarray, n_used: int, x: np.ndarray):
+    """MUL_MAT_ID: wq [n_as*M][row bytes], ids [T][ids_row] int32 (first n_used used), x [T][ne11][K].
+    Returns y [T][n_used][M]."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    T, ne11 = x.shape[0], x.shape[1]
+    dw, di, dx, dy = Dev(wq), Dev(ids), Dev(x), Dev(nbytes=T * n_used * M * 4)
+    _chk(lib().mi355x_mul_mat_id(wtype, dw.ptr, K, M, n_as, di.ptr, ids.shape[1], n_used, dx.ptr, ne11, T, dy.ptr, None),
+         "mul_mat_id")
+    return dy.get(np.float32, (T, n_used, M))
+
+
+def argsort(x: np.ndarray, order: int) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n, ne0 = x.shape
+    dx, do = Dev(x), Dev(nbytes=x.nbytes)
+    _chk(lib().mi355x_argsort(dx.ptr, ne0, n, order, do.ptr, None), "argsort")
+    return do.get(np.int32, x.shape)
+
+
+def sum_rows(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n, ne0 = x.shape
+    dx, dy = Dev(x), Dev(nbytes=n * 4)
+    _chk(lib().mi355x_sum_rows(dx.ptr, ne0, n, dy.ptr, None), "sum_rows")
+    return dy.get(np.float32, (n,))

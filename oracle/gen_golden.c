@@ -63,6 +63,43 @@ void gg_mul_mat(int type, const void * W, int64_t K, int64_t M, const float * X,
     ggml_free(ctx);
 }
 
+/* Y[T][n_used][M] = mul_mat_id(As [n_as][M][K], X [T][ne11][K], ids [T][n_used]) on the CPU backend */
+void gg_mul_mat_id(int type, const void * As, int64_t K, int64_t M, int64_t n_as, const int32_t * ids, int64_t n_used,
+                   const float * X, int64_t ne11, int64_t T, float * Y, int nth) {
+    struct ggml_context * ctx = mk_ctx(64 + (size_t) ((K * M * n_as * 4 + K * ne11 * T * 4 + M * n_used * T * 4) >> 20) * 2);
+    struct ggml_tensor * as = ggml_new_tensor_3d(ctx, (enum ggml_type) type, K, M, n_as);
+    struct ggml_tensor * id = ggml_new_tensor_2d(ctx, GGML_TYPE_I32, n_used, T);
+    struct ggml_tensor * x = ggml_new_tensor_3d(ctx, GGML_TYPE_F32, K, ne11, T);
+    memcpy(as->data, As, ggml_nbytes(as));
+    memcpy(id->data, ids, ggml_nbytes(id));
+    memcpy(x->data, X, ggml_nbytes(x));
+    struct ggml_tensor * y = ggml_mul_mat_id(ctx, as, x, id);
+    run(ctx, y, nth);
+    memcpy(Y, y->data, ggml_nbytes(y));
+    ggml_free(ctx);
+}
+
+/* argsort of nrows rows of ne0 floats (order 0 asc, 1 desc) on the CPU backend */
+void gg_argsort(const float * x, int64_t ne0, int64_t nrows, int order, int32_t * out) {
+    struct ggml_context * ctx = mk_ctx(16 + (size_t) ((ne0 * nrows * 8) >> 20));
+    struct ggml_tensor * a = ggml_new_tensor_2d(ctx, GGML_TYPE_F32, ne0, nrows);
+    memcpy(a->data, x, ggml_nbytes(a));
+    struct ggml_tensor * o = ggml_argsort(ctx, a, (enum ggml_sort_order) order);
+    run(ctx, o, 1);
+    memcpy(out, o->data, ggml_nbytes(o));
+    ggml_free(ctx);
+}
+
+void gg_sum_rows(const float * x, int64_t ne0, int64_t nrows, float * y) {
+    struct ggml_context * ctx = mk_ctx(16 + (size_t) ((ne0 * nrows * 8) >> 20));
+    struct ggml_tensor * a = ggml_new_tensor_2d(ctx, GGML_TYPE_F32, ne0, nrows);
+    memcpy(a->data, x, ggml_nbytes(a));
+    struct ggml_tensor * o = ggml_sum_rows(ctx, a);
+    run(ctx, o, 1);
+    memcpy(y, o->data, ggml_nbytes(o));
+    ggml_free(ctx);
+}
+
 void gg_rms_norm(const float * x, int64_t ne0, int64_t nrows, float eps, float * y) {
     struct ggml_context * ctx = mk_ctx(16 + (size_t) ((ne0 * nrows * 8) >> 20));
     struct ggml_tensor * a = ggml_new_tensor_2d(ctx, GGML_TYPE_F32, ne0, nrows);

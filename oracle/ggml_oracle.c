@@ -397,6 +397,52 @@ void orc_mul_mat(int type, const void * W, int64_t K, int64_t M, const float * X
     free(xq);
 }
 
+/* ggml_compute_forward_mul_mat_id (ggml-cpu/ggml-cpu.c:1466-1600): for token t and slot e,
+ * Y[t][e][:] = mul_mat(As[ids[t][e]], X[t][e % ne11]) with the mat-vec's per-row arithmetic
+ * (the activation row quantized to the vec_dot_type, vec_dot per weight row).  As: n_as
+ * matrices of M rows; ids: T rows of ids_row int32 (first n_used used); X: [T][ne11][K]. */
+void orc_mul_mat_id(int type, const void * As, int64_t K, int64_t M, int64_t n_as, const int32_t * ids, int64_t ids_row,
+                    int64_t n_used, const float * X, int64_t ne11, int64_t T, float * Y) {
+    const size_t wmat = (size_t) (K / orc_block_size(type)) * orc_type_size(type) * (size_t) M;
+    for (int64_t t = 0; t < T; ++t) {
+        for (int64_t e = 0; e < n_used; ++e) {
+            const int32_t ex = ids[t * ids_row + e];
+            if (ex < 0 || ex >= n_as) continue;
+            orc_mul_mat(type, (const char *) As + (size_t) ex * wmat, K, M, X + (t * ne11 + e % ne11) * K, 1,
+                        Y + (t * n_used + e) * M);
+        }
+    }
+}
+
+/* ggml_compute_forward_argsort_f32 (ggml-cpu/ops.cpp:6956-6993): the exchange sort per row;
+ * order 0 ascending, 1 descending */
+void orc_argsort(const float * x, int64_t ne0, int64_t nrows, int order, int32_t * dst) {
+    for (int64_t r = 0; r < nrows; ++r) {
+        const float * s = x + r * ne0;
+        int32_t * d = dst + r * ne0;
+        for (int64_t j = 0; j < ne0; ++j) d[j] = (int32_t) j;
+        for (int64_t j = 0; j < ne0; ++j) {
+            for (int64_t k = j + 1; k < ne0; ++k) {
+                if ((order == 0 && s[d[j]] > s[d[k]]) || (order == 1 && s[d[j]] < s[d[k]])) {
+                    const int32_t tmp = d[j];
+                    d[j] = d[k];
+                    d[k] = tmp;
+                }
+            }
+        }
+    }
+}
+
+/* ggml_compute_forward_sum_rows_f32 (ggml-cpu/ops.cpp:1956-1986) with ggml_vec_sum_f32
+ * (ggml-cpu/vec.h:908-918): sequential double sum, rounded once */
+void orc_sum_rows(const float * x, int64_t ne0, int64_t nrows, float * y) {
+    for (int64_t r = 0; r < nrows; ++r) {
+        double s = 0.0;
+        for (int64_t i = 0; i < ne0; ++i) s += (double) x[r * ne0 + i];
+        y[r] = (float) s;
+    }
+}
+
 /* ggml_compute_forward_rms_norm_f32, ggml-cpu/ops.cpp:3270-3316 (sum in double) */
 void orc_rms_norm(const float * x, int64_t ne0, int64_t nrows, float eps, float * y) {
     for (int64_t r = 0; r < nrows; ++r) {

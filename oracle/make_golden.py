@@ -50,6 +50,9 @@ def load():
     lib.gg_soft_max.argtypes = [P, I64, I64, P, I64, ctypes.c_float, P]
     lib.gg_flash_attn.argtypes = [P, P, P, P, ctypes.c_int, I64, I64, I64, I64, I64, ctypes.c_float, ctypes.c_float, P,
                                   ctypes.c_int]
+    lib.gg_mul_mat_id.argtypes = [ctypes.c_int, P, I64, I64, I64, P, I64, P, I64, I64, P, ctypes.c_int]
+    lib.gg_argsort.argtypes = [P, I64, I64, ctypes.c_int, P]
+    lib.gg_sum_rows.argtypes = [P, I64, I64, P]
     lib.gg_init()
     return lib
 
@@ -101,9 +104,57 @@ def act_cases(k, rng):
     return np.stack(rows)
 
 
+def moe(lib):
+    """MoE routing ops (build_moe_ffn, src/llama-graph.cpp:642-787): MUL_MAT_ID per expert type
+    (decode T = 1 and a batch with repeated experts, ne11 = 1 broadcast and ne11 = n_used),
+    ARGSORT with ties (ggml_top_k), SUM_ROWS."""
+    rng = np.random.default_rng(4321)
+    g = {}
+    n_as, M, K, n_used = 4, 64, 512, 2
+    for t, name in ((Q4_K, "q4_K"), (Q5_K, "q5_K"), (Q6_K, "q6_K"), (Q8_0, "q8_0"), (Q4_0, "q4_0")):
+        w = (rng.standard_normal((n_as * M, K)) * 0.05).astype(np.float32)
+        wq = quantize(lib, t, w)
+        g[f"wq_{name}"] = wq
+        for T, ne11 in ((1, 1), (1, n_used), (9, 1), (9, n_used)):
+            ids = np.stack([rng.permutation(n_as)[:n_used] for _ in range(T)]).astype(np.int32)
+            if T > 1:
+                ids[1] = ids[0]            # repeated routing across tokens
+            x = np.concatenate([act_cases(K, rng)[:2], rng.standard_normal((T * ne11, K)).astype(np.float32)])[:T * ne11]
+            x = x.reshape(T, ne11, K)
+            y = np.zeros((T, n_used, M), dtype=np.float32)
+            lib.gg_mul_mat_id(t, fptr(wq), K, M, n_as, fptr(ids), n_used, fptr(x), ne11, T, fptr(y), 1)
+            g[f"ids_{name}_{T}_{ne11}"] = ids
+            g[f"x_{name}_{T}_{ne11}"] = x
+            g[f"y_{name}_{T}_{ne11}"] = y
+    # router-like rows with ties (equal probabilities must order as the CPU's exchange sort)
+    xs = rng.standard_normal((12, 8)).astype(np.float32)
+    xs[0] = [0.5, 0.1, 0.5, 0.3, 0.5, 0.1, 0.2, 0.5]
+    xs[1] = 0.25
+    xs[2, ::2] = xs[2, 1::2]
+    xl = rng.integers(-4, 4, (3, 60)).astype(np.float32)   # wide rows, many ties
+    for nm, arr in (("s", xs), ("l", xl)):
+        for order in (0, 1):
+            out = np.zeros(arr.shape, dtype=np.int32)
+            lib.gg_argsort(fptr(arr), arr.shape[1], arr.shape[0], order, fptr(out))
+            g[f"argsort_{nm}_{order}"] = out
+        g[f"argsort_{nm}_x"] = arr
+    xr = np.concatenate([rng.standard_normal((5, 2)), rng.standard_normal((5, 2)) * 1e6,
+                         rng.standard_normal((2, 2)) * 1e-8]).astype(np.float32)
+    xr2 = (rng.standard_normal((4, 1000)) * 100).astype(np.float32)
+    for nm, arr in (("a", xr), ("b", xr2)):
+        y = np.zeros(arr.shape[0], dtype=np.float32)
+        lib.gg_sum_rows(fptr(arr), arr.shape[1], arr.shape[0], fptr(y))
+        g[f"sum_rows_{nm}_x"] = arr
+        g[f"sum_rows_{nm}_y"] = y
+    np.savez_compressed(os.path.join(OUT, "moe.npz"), n_as=n_as, M=M, K=K, n_used=n_used, **g)
+    print(f"moe.npz {os.path.getsize(os.path.join(OUT, 'moe.npz'))} B")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     lib = load()
+    if "moe" in sys.argv[1:]:   # only the MoE fixture (the others stay as committed)
+        return moe(lib)
     rng = np.random.default_rng(1234)
 
     # ---- activation quantizers ------------------------------------------------------------
@@ -192,6 +243,7 @@ def main():
             fa[f"mask_{n_q}"] = m.view(np.uint16)
             fa[f"out_{kvname}_{n_q}"] = out
     np.savez_compressed(os.path.join(OUT, "flash_attn.npz"), D=D, H=H, Hkv=Hkv, n_kv=n_kv, **fa)
+    moe(lib)
     for f in sorted(os.listdir(OUT)):
         print(f"{f:28s} {os.path.getsize(os.path.join(OUT, f)):9d} B")
 

@@ -42,6 +42,9 @@ def lib():
                                ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, P, P]
         L.orc_soft_max.argtypes = [P, I64, I64, P, I64, ctypes.c_float, P]
         L.orc_flash_attn.argtypes = [P, P, P, P, ctypes.c_int, I64, I64, I64, I64, I64, ctypes.c_float, ctypes.c_float, P]
+        L.orc_mul_mat_id.argtypes = [ctypes.c_int, P, I64, I64, I64, P, I64, I64, P, I64, I64, P]
+        L.orc_argsort.argtypes = [P, I64, I64, ctypes.c_int, P]
+        L.orc_sum_rows.argtypes = [P, I64, I64, P]
         _lib = L
     return _lib
 
@@ -153,3 +156,28 @@ def split_q8(t, blocks, k):
     qs = b[:, :, 2:34].copy().view(np.int8).reshape(n, k)
     s = qs.reshape(n, k // 32, 32).astype(np.int32).sum(axis=2).astype(np.int16)
     return qs, d16.astype(np.float32), s
+
+
+def mul_mat_id(t, wq, K, M, n_as, ids, n_used, x):
+    """MUL_MAT_ID: wq [n_as*M] rows, ids [T][ids_row] (first n_used used), x [T][ne11][K] -> [T][n_used][M]."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    T, ne11 = x.shape[0], x.shape[1]
+    y = np.zeros((T, n_used, M), dtype=np.float32)
+    lib().orc_mul_mat_id(t, ptr(np.ascontiguousarray(wq)), K, M, n_as, ptr(ids), ids.shape[1], n_used, ptr(x), ne11, T,
+                         ptr(y))
+    return y
+
+
+def argsort(x, order):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.zeros(x.shape, dtype=np.int32)
+    lib().orc_argsort(ptr(x), x.shape[1], x.shape[0], order, ptr(out))
+    return out
+
+
+def sum_rows(x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.zeros(x.shape[0], dtype=np.float32)
+    lib().orc_sum_rows(ptr(x), x.shape[1], x.shape[0], ptr(y))
+    return y

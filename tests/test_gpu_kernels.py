@@ -179,3 +179,52 @@ def test_mul_mat_prefill_mfma_vs_oracle(K, name, Kd, M):
         ref = O.mul_mat(t, wq, Kd, M, x)
         err = np.abs(y - ref).max() / np.abs(ref).max()
         assert err < 2e-6, (name, T, err)
+
+
+MOE_TYPES = {"q4_K": O.Q4_K, "q5_K": O.Q5_K, "q6_K": O.Q6_K, "q8_0": O.Q8_0, "q4_0": O.Q4_0}
+
+
+@pytest.mark.parametrize("name", sorted(MOE_TYPES))
+def test_mul_mat_id_golden(K, golden_dir, name):
+    """MUL_MAT_ID vs the reference CPU backend: decode (one GEMV per routed pair, experts read
+    on the device) and T = 9 (the expert-sorted path); integer sums exact, fp32 combination
+    order differs -> 2e-6 of the range, like mul_mat."""
+    g = load(golden_dir, "moe.npz")
+    n_as, M, Kd, n_used = (int(g[k]) for k in ("n_as", "M", "K", "n_used"))
+    for T, ne11 in ((1, 1), (1, n_used), (9, 1), (9, n_used)):
+        key = f"{name}_{T}_{ne11}"
+        y = K.mul_mat_id(MOE_TYPES[name], g[f"wq_{name}"], Kd, M, n_as, g[f"ids_{key}"], n_used, g[f"x_{key}"])
+        ref = g[f"y_{key}"]
+        err = np.abs(y - ref).max() / np.abs(ref).max()
+        assert err < 2e-6, (key, err)
+
+
+@pytest.mark.parametrize("name,Kd,M,n_as,n_used,T", [("q5_K", 4096, 1024, 8, 2, 1), ("q6_K", 14336, 256, 8, 2, 1),
+                                                     ("q5_K", 4096, 512, 8, 2, 64), ("q8_0", 4096, 256, 4, 1, 33),
+                                                     ("q4_K", 1024, 128, 32, 4, 129)])
+def test_mul_mat_id_mixtral_shapes_vs_oracle(K, name, Kd, M, n_as, n_used, T):
+    """Mixtral-like expert shapes (K 4096 / 14336, 8 experts, top-2) and batch routing with a
+    view of a wider ids row (test-backend-ops builds ids as [n_mats, n] viewed to n_used)."""
+    from llamacog_amd import gguf_synth as gs
+    t = MOE_TYPES[name]
+    rng = np.random.default_rng(21)
+    blk, bs = gs.BLOCK[t]
+    wq = gs.make_blocks(t, n_as * M * Kd // blk, rng).reshape(n_as * M, -1)
+    ids = np.stack([rng.permutation(n_as) for _ in range(T)]).astype(np.int32)   # row of n_as, first n_used used
+    for ne11 in (1, n_used):
+        x = rng.standard_normal((T, ne11, Kd)).astype(np.float32)
+        y = K.mul_mat_id(t, wq, Kd, M, n_as, ids, n_used, x)
+        ref = O.mul_mat_id(t, wq, Kd, M, n_as, ids, n_used, x)
+        err = np.abs(y - ref).max() / np.abs(ref).max()
+        assert err < 2e-6, (name, T, ne11, err)
+
+
+def test_argsort_and_sum_rows_golden(K, golden_dir):
+    """ARGSORT (ggml_top_k of the router): the CPU's exchange order, ties included, bit-exact;
+    SUM_ROWS: the CPU's sequential double sum, bit-exact."""
+    g = load(golden_dir, "moe.npz")
+    for nm in ("s", "l"):
+        for order in (0, 1):
+            assert (K.argsort(g[f"argsort_{nm}_x"], order) == g[f"argsort_{nm}_{order}"]).all(), (nm, order)
+    for nm in ("a", "b"):
+        assert (K.sum_rows(g[f"sum_rows_{nm}_x"]).view(np.uint32) == g[f"sum_rows_{nm}_y"].view(np.uint32)).all()

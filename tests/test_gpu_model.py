@@ -23,7 +23,7 @@ import llamacog_amd as la
 from llamacog_amd import gguf_synth as gs
 
 OPS = ["MUL_MAT", "FLASH_ATTN_EXT", "RMS_NORM", "ROPE", "SOFT_MAX", "CPY", "GET_ROWS", "ADD", "MUL", "SCALE", "SILU",
-       "CONT", "DUP", "SUB", "DIV", "NORM", "GELU"]
+       "CONT", "DUP", "SUB", "DIV", "NORM", "GELU", "MUL_MAT_ID", "ARGSORT", "SUM_ROWS"]
 
 
 @pytest.mark.parametrize("op", OPS)
@@ -72,6 +72,14 @@ def test_greedy_tiny_q8_0():
     _check(_greedy("tiny-q8_0", 16, 16, True), 3e-2)
 
 
+def test_greedy_tiny_moe_q5km():
+    """Mixtral-style MoE FFN (router soft_max -> top-k ARGSORT -> GET_ROWS -> SUM_ROWS/DIV ->
+    MUL_MAT_ID up/gate/down -> weighted sum) entirely on MI355X, vs the CPU backend; prompt
+    decode exercises the expert-sorted batch path, generation the per-pair decode path."""
+    rel = _check(_greedy("tiny-moe-q5km", 16, 16, True), 3e-2)
+    print("tiny-moe-q5km max rel logit err", max(rel))
+
+
 def test_greedy_llama3_8b_2layer_q4km():
     rel = _check(_greedy("llama3-8b-2l-q4km", 32, 16, True), 5e-2)
     print("llama3-8b-2l max rel logit err", max(rel))
@@ -104,8 +112,9 @@ def test_fused_and_graph_replay_bit_identical(cfg):
     assert (la_.view(np.uint32) == lb.view(np.uint32)).all(), np.abs(la_ - lb).max()
 
 
-def test_graph_runs_on_mi355x():
-    path = gs.ensure("tiny-q4km")
+@pytest.mark.parametrize("cfg", ["tiny-q4km", "tiny-moe-q5km"])
+def test_graph_runs_on_mi355x(cfg):
+    path = gs.ensure(cfg)
     lib = la.llb()
     m = la.Model(path, gpu=True, n_ctx=256)
     m.greedy([1, 2, 3], 2)

@@ -123,3 +123,34 @@ def test_flash_attn(golden_dir, n_q, kv):
     err = np.abs(out - ref).max() / np.abs(ref).max()
     # f16 VKQ accumulation is restated rounding-for-rounding; only exp/dot-order ulps remain
     assert err < (2e-3 if kv == "f16" else 2e-6), err
+
+
+MOE_TYPES = {"q4_K": O.Q4_K, "q5_K": O.Q5_K, "q6_K": O.Q6_K, "q8_0": O.Q8_0, "q4_0": O.Q4_0}
+
+
+@pytest.mark.parametrize("name", sorted(MOE_TYPES))
+def test_mul_mat_id_restatement(golden_dir, name):
+    """MUL_MAT_ID (ggml-cpu.c:1466) per routed (slot, token): decode and a batch with repeated
+    experts, the activation broadcast (ne11 = 1) or per slot (ne11 = n_used).  Same per-row
+    arithmetic as mul_mat, so the same bound."""
+    g = load(golden_dir, "moe.npz")
+    n_as, M, K, n_used = (int(g[k]) for k in ("n_as", "M", "K", "n_used"))
+    for T, ne11 in ((1, 1), (1, n_used), (9, 1), (9, n_used)):
+        key = f"{name}_{T}_{ne11}"
+        y = O.mul_mat_id(MOE_TYPES[name], g[f"wq_{name}"], K, M, n_as, g[f"ids_{key}"], n_used, g[f"x_{key}"])
+        ref = g[f"y_{key}"]
+        assert np.abs(y - ref).max() <= 1e-5 * np.abs(ref).max(), (key, np.abs(y - ref).max())
+
+
+def test_argsort_restatement_bit_exact(golden_dir):
+    """ARGSORT (ops.cpp:6956): the exchange sort, ties included (router rows of equal probability)."""
+    g = load(golden_dir, "moe.npz")
+    for nm in ("s", "l"):
+        for order in (0, 1):
+            assert (O.argsort(g[f"argsort_{nm}_x"], order) == g[f"argsort_{nm}_{order}"]).all(), (nm, order)
+
+
+def test_sum_rows_restatement_bit_exact(golden_dir):
+    g = load(golden_dir, "moe.npz")
+    for nm in ("a", "b"):
+        assert (O.sum_rows(g[f"sum_rows_{nm}_x"]).view(np.uint32) == g[f"sum_rows_{nm}_y"].view(np.uint32)).all()
