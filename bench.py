@@ -155,6 +155,12 @@ def main():
     t = dist.max(t_local)
     value = ws * a.steps / t
 
+    # where a step's wall time goes: host work inside llama_decode (libllama graph build,
+    # scheduling, input upload, our graph_compute and launch) vs waiting in llama_synchronize
+    m.clear()
+    m.time_gen(4)
+    t_sp, t_dec, t_syn = m.time_gen_split(a.steps)
+
     # roofline pass: HIP events around every mat-vec launch on the plugin stream
     m.clear()
     m.time_gen(4)
@@ -232,6 +238,8 @@ def main():
                 "fattn_avg_us": round(1e3 * fa_ms / fa_n, 3) if fa_n else None,
                 "timed_pass_tok_s": round(a.roofline_steps / t_rf, 2),
             },
+            "step_split_ms": {"wall": round(1e3 * t_sp / a.steps, 4), "llama_decode_host": round(1e3 * t_dec / a.steps, 4),
+                              "llama_synchronize": round(1e3 * t_syn / a.steps, 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

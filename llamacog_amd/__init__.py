@@ -96,6 +96,9 @@ def llb(echo_log: bool = False, with_plugin: bool = True) -> ctypes.CDLL:
     lib.llb_time_prompt.restype = ctypes.c_double
     lib.llb_time_gen.argtypes = [ctypes.c_void_p, ctypes.c_int]
     lib.llb_time_gen.restype = ctypes.c_double
+    lib.llb_time_gen_split.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_double)]
+    lib.llb_time_gen_split.restype = ctypes.c_double
     lib.llb_greedy.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_int,
                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float)]
     lib.llb_log.argtypes = [ctypes.c_char_p, ctypes.c_int]
@@ -166,6 +169,14 @@ class Model:
         if t < 0:
             raise RuntimeError("llama_decode failed")
         return t
+
+    def time_gen_split(self, n: int) -> tuple[float, float, float]:
+        """test_gen with the host time split: (wall, inside llama_decode, inside llama_synchronize)."""
+        td, ts = ctypes.c_double(), ctypes.c_double()
+        t = self.lib.llb_time_gen_split(self.h, n, ctypes.byref(td), ctypes.byref(ts))
+        if t < 0:
+            raise RuntimeError("llama_decode failed")
+        return t, td.value, ts.value
 
     def time_prompt(self, n: int) -> float:
         t = self.lib.llb_time_prompt(self.h, n)

@@ -112,7 +112,7 @@ template <int D> struct fax_cfg {
     static constexpr int CH = D <= 128 ? 256 : 128;   // positions per chunk (V chunk <= 64 KiB)
     static constexpr int NP = CH / 64;                // score passes per chunk (64 positions each)
     static constexpr int RPP = 512 / D;               // V rows per 1 KiB global_load_lds piece
-    static constexpr int U = 16;                      // phase-3 positions per batch
+    static constexpr int U = 8;                       // phase-3 positions per batch
 };
 
 template <int D>
@@ -127,9 +127,9 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
     const int64_t hk = h / (a.H / a.Hkv);
 
     __shared__ __attribute__((aligned(16))) uint16_t vl[CH * D];   // V chunk, [pos][D] f16
-    __shared__ float sc[CH + 3 * U];    // scores -> vs coefficient (0 where masked)
-    __shared__ float cm[CH + 3 * U];    // ms coefficient (1 where masked)
-    __shared__ float mk[CH + 3 * U];    // mask values of the chunk (-inf = skipped)
+    __shared__ __attribute__((aligned(16))) float sc[CH + 6 * U];    // scores -> vs coefficient (0 where masked)
+    __shared__ __attribute__((aligned(16))) float cm[CH + 6 * U];    // ms coefficient (1 where masked)
+    __shared__ __attribute__((aligned(16))) float mk[CH + 6 * U];    // mask values of the chunk (-inf = skipped)
     __shared__ uint32_t wflag[4];    // per wave: batches needing the general step (mask / max update)
     __shared__ int wlast[4];
     __shared__ float wmax[4];
@@ -268,10 +268,11 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         mark(4);
-        uint32_t bmask = 0;   // bit n: batch n takes the general step (uniform)
+        uint64_t bmask = 0;   // bit n: batch n takes the general step (uniform)
 #pragma unroll
-        for (int w = 0; w < 4; ++w) bmask |= wflag[w] << ((64 / U) * w);
-        bmask = __builtin_amdgcn_readfirstlane(bmask);
+        for (int w = 0; w < 4; ++w) bmask |= (uint64_t) wflag[w] << ((64 / U) * w);
+        bmask = ((uint64_t) __builtin_amdgcn_readfirstlane((uint32_t) (bmask >> 32)) << 32) |
+                __builtin_amdgcn_readfirstlane((uint32_t) bmask);
         // ---- phase 3: sequential f16 recurrence (V from LDS) --------------------------------
         // y = f16(y*ms) and S*ms only where the running max moved (ms != 1: y*1 and S*1 are
         // identities); masked / padded positions keep the state (-0 must survive)
@@ -280,20 +281,24 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
             // coefficients are read from LDS while batch n computes
             // (a prefetch past the chunk end reads other LDS arrays or past the allocation, which
             // reads as 0 — never used: batches at or past nrun do not run)
-            // batch n+1's V values and coefficients (vs, ms, mask) come from LDS while batch n
-            // computes; the general step selects instead of branching, so it never waits on an
-            // LDS value to decide (a readfirstlane per position cost ~140 ns in phase 3)
-            auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U], float (&ms)[U], float (&mv)[U]) {
-                const uint16_t * vp = vl + j * D + d;
+            // batch n+1's V values and vs coefficients come from LDS while batch n computes: U
+            // u16 reads of the thread's V column plus U/4 broadcast b128 reads of vs, few enough
+            // to stay under the 15-deep LDS counter, so the prefetch really overlaps (U = 16
+            // with scalar coefficient reads saturated it: ~66 cycles per position)
+            auto ld4 = [&](const float * p, float (&o)[U]) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    vv[u] = vp[u * D];
-                    vs[u] = sc[j + u];
-                    ms[u] = cm[j + u];
-                    mv[u] = mk[j + u];
+                for (int u = 0; u < U; u += 4) {
+                    const float4 t = *(const float4 *) (p + u);
+                    o[u] = t.x; o[u + 1] = t.y; o[u + 2] = t.z; o[u + 3] = t.w;
                 }
             };
-            auto run = [&](int j, const uint32_t (&vv)[U], const float (&vs)[U], const float (&ms)[U], const float (&mv)[U]) {
+            auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
+                const uint16_t * vp = vl + j * D + d;
+#pragma unroll
+                for (int u = 0; u < U; ++u) vv[u] = vp[u * D];
+                ld4(sc + j, vs);
+            };
+            auto run = [&](int j, const uint32_t (&vv)[U], const float (&vs)[U]) {
                 if (((bmask >> (j / U)) & 1u) == 0) {
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -304,7 +309,11 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
                 }
                 // masked / padded position: the state is kept (-0 must survive); a running-max
                 // update (ms != 1): y = f16(y*ms), S = S*ms before the add — the CPU's
-                // vec_scale_f16 / S*ms (ops.cpp:7120-7160); otherwise y*1 and S*1 are skipped
+                // vec_scale_f16 / S*ms (ops.cpp:7120-7160); otherwise y*1 and S*1 are skipped.
+                // Selects, not branches on LDS values.
+                float ms[U], mv[U];
+                ld4(cm + j, ms);
+                ld4(mk + j, mv);
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const bool live = __float_as_uint(mv[u]) != 0xff800000u;
@@ -320,14 +329,14 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
                 }
             };
             uint32_t va[U], vb[U];
-            float sa[U], sb[U], ma[U], mb[U], ka[U], kb[U];
-            ldb(0, va, sa, ma, ka);
+            float sa[U], sb[U];
+            ldb(0, va, sa);
             for (int j = 0; j < nrun; j += 2 * U) {
-                ldb(j + U, vb, sb, mb, kb);
-                run(j, va, sa, ma, ka);
+                ldb(j + U, vb, sb);
+                run(j, va, sa);
                 if (j + U >= nrun) break;
-                ldb(j + 2 * U, va, sa, ma, ka);
-                run(j + U, vb, sb, mb, kb);
+                ldb(j + 2 * U, va, sa);
+                run(j + U, vb, sb);
             }
         }
         __syncthreads();
