@@ -159,7 +159,12 @@ def main():
     # scheduling, input upload, our graph_compute and launch) vs waiting in llama_synchronize
     m.clear()
     m.time_gen(4)
+    plugin.ggml_backend_mi355x_reset_timing()
+    plugin.ggml_backend_mi355x_set_graph_timing(1)
     t_sp, t_dec, t_syn = m.time_gen_split(a.steps)
+    plugin.ggml_backend_mi355x_set_graph_timing(0)
+    g_ms, _, g_n = la.kernel_timing(plugin, 5)    # device time of each graph_compute (events around it)
+    gh_ms, _, gh_n = la.kernel_timing(plugin, 6)  # host time inside graph_compute
 
     # roofline pass: HIP events around every mat-vec launch on the plugin stream
     m.clear()
@@ -238,8 +243,15 @@ def main():
                 "fattn_avg_us": round(1e3 * fa_ms / fa_n, 3) if fa_n else None,
                 "timed_pass_tok_s": round(a.roofline_steps / t_rf, 2),
             },
-            "step_split_ms": {"wall": round(1e3 * t_sp / a.steps, 4), "llama_decode_host": round(1e3 * t_dec / a.steps, 4),
-                              "llama_synchronize": round(1e3 * t_syn / a.steps, 4)},
+            # wall = one llama_decode + llama_synchronize; device_graph = GPU time of the graph
+            # (events before/after graph_compute's launches); graph_compute_host = host time in
+            # our graph_compute (signature, KV-slot table upload, hipGraph launch); the rest of the
+            # wall is libllama's host work (graph build, scheduling, input upload, logits copy)
+            "step_split_ms": {"wall": round(1e3 * t_sp / a.steps, 4),
+                              "device_graph": round(g_ms / g_n, 4) if g_n else None,
+                              "graph_compute_host": round(gh_ms / gh_n, 4) if gh_n else None,
+                              "llama_decode_call": round(1e3 * t_dec / a.steps, 4),
+                              "llama_synchronize_call": round(1e3 * t_syn / a.steps, 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
