@@ -601,6 +601,27 @@ static int op_rope_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     return 1;
 }
 
+// which outputs of a fused [ADD] -> RMS_NORM -> [MUL] chain feeding mat-vec `mm` must be stored:
+// the norm output when something other than the MUL reads it; the last output when something
+// other than the decode mat-vecs that consume it through the quantized-activation cache reads it
+static void norm_stores(ggml_cgraph * g, int n, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm,
+                        bool & store_norm, bool & store_mul) {
+    store_norm = store_mul = true;
+    const int pn = node_index(g, norm);
+    const ggml_tensor * last = mul ? mul : norm;
+    if (mul) store_norm = !dead_after(g, n, pn + 1, norm, {mul});
+    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != last || !gemv_supported(mm)) return;
+    std::vector<const ggml_tensor *> readers;
+    const int pm = node_index(g, mm);
+    for (int k = pm; k < n && k <= pm + 12; ++k) {
+        const ggml_tensor * c = ggml_graph_node(g, k);
+        if (c->op == GGML_OP_MUL_MAT && c->src[1] == last && gemv_supported(c) &&
+            c->src[0]->type == mm->src[0]->type && c->src[0]->ne[0] == mm->src[0]->ne[0]) readers.push_back(c);
+    }
+    const bool dead = dead_after(g, n, node_index(g, last) + 1, last, readers);
+    if (mul) store_mul = !dead; else store_norm = !dead;
+}
+
 int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
     ggml_tensor * node = ggml_graph_node(cgraph, i);
     if (ctx.pend.kind && ctx.pend.consumer != node) {
@@ -652,8 +673,11 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             if (fusion_enabled() && defer_to_prologue(ctx, cgraph, n, 1, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
                 return mul ? 2 : 1;
             }
-            if (fusion_enabled() && fused_norm(ctx, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
-                return mul ? 2 : 1;
+            if (fusion_enabled()) {
+                ggml_tensor * mm = at(cgraph, i + (mul ? 2 : 1), n);
+                bool sn, sm;
+                norm_stores(cgraph, n, node, mul, mm, sn, sm);
+                if (fused_norm(ctx, nullptr, node, mul, mm, sn, sm)) return mul ? 2 : 1;
             }
             op_rms_norm(ctx, node, mul ? mul->src[1] : nullptr, mul);
             return mul ? 2 : 1;
@@ -669,7 +693,10 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                     ggml_tensor * mul = norm_weight_mul(cgraph, i + 1, n);
                     const int used = mul ? 3 : 2;
                     if (defer_to_prologue(ctx, cgraph, n, 1, node, nx, mul, at(cgraph, i + used, n))) return used;
-                    if (fused_norm(ctx, node, nx, mul, at(cgraph, i + used, n))) return used;
+                    ggml_tensor * mm = at(cgraph, i + used, n);
+                    bool sn, sm;
+                    norm_stores(cgraph, n, nx, mul, mm, sn, sm);
+                    if (fused_norm(ctx, node, nx, mul, mm, sn, sm)) return used;
                 }
             }
             op_binary(ctx, node);

@@ -88,12 +88,12 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
         float4 y;
         y.x = __fmul_rn(v[k].x, scale); y.y = __fmul_rn(v[k].y, scale);
         y.z = __fmul_rn(v[k].z, scale); y.w = __fmul_rn(v[k].w, scale);
-        *(float4 *) (p.y + ro + e) = y;
+        if (p.y) *(float4 *) (p.y + ro + e) = y;
         if (p.w) {
             const float4 ww = wv[k];
             y.x = __fmul_rn(y.x, ww.x); y.y = __fmul_rn(y.y, ww.y);
             y.z = __fmul_rn(y.z, ww.z); y.w = __fmul_rn(y.w, ww.w);
-            *(float4 *) (p.yw + ro + e) = y;
+            if (p.yw) *(float4 *) (p.yw + ro + e) = y;
         }
         const float q[4] = {y.x, y.y, y.z, y.w};
         const int64_t c0 = 4 * (int64_t) BT * k + 256 * wave;
@@ -170,7 +170,8 @@ static int consumer_qmode(const ggml_tensor * mm, const ggml_tensor * x) {
     return kq ? 1 : 2;
 }
 
-bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm) {
+bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm,
+                bool store_norm, bool store_mul) {
     const int64_t ne0 = norm->ne[0];
     // ne0 <= 4096: one float4 per thread; above: whole 4096-element slices per 1024 threads
     if (ne0 % 256 != 0 || (ne0 > 4096 && ne0 % 4096 != 0) || ne0 > 16384) return false;
@@ -186,9 +187,11 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     p.a = add ? (const float *) add->src[0]->data : (const float *) norm->src[0]->data;
     p.b = add ? (const float *) add->src[1]->data : nullptr;
     p.xsum = add ? (float *) add->data : nullptr;
-    p.y = (float *) norm->data;
     p.w = mul ? (const float *) mul->src[1]->data : nullptr;
-    p.yw = mul ? (float *) mul->data : nullptr;
+    // an output nothing reads is not stored; the last one is kept unless it is quantized here
+    const bool last_needed = !qmode || (mul ? store_mul : store_norm);
+    p.y = (mul ? store_norm : last_needed) ? (float *) norm->data : nullptr;
+    p.yw = mul && last_needed ? (float *) mul->data : nullptr;
     p.ne0 = ne0;
     memcpy(&p.eps, norm->op_params, sizeof(float));
     p.qmode = qmode;

@@ -354,6 +354,9 @@ struct gemv_args {
     int8_t * cq; float * cd; int16_t * cs;
     // a deferred in-place ADD stored by workgroup 0 (x[i] = x[i] + y[i], n elements)
     float * post_add; const float * post_b; int64_t post_n;
+    // MUL_MAT_ID decode (gemv_mul_mat_id): matrix m is expert ids[ids_e[m]] of the stack at
+    // W[0] (stride nb02), read on the device so routing needs no host round trip
+    const int32_t * ids; int64_t nb02; int64_t ids_e[GEMV_MAXMAT];
 };
 
 // the activation prologue, once per workgroup (4 waves): wave w owns the Q8_K blocks
@@ -582,7 +585,7 @@ __global__ __launch_bounds__(256) void k_gemv(const gemv_args p) {
 // MODE: 0 = plain stores (no prologue, no epilogue), 1 = epilogues, 2 = activation prologue +
 // epilogues.  The lean modes keep the register footprint (and so the number of resident
 // workgroups) of the plain mat-vec: 90 VGPRs at R = 2 against 134 with the prologue compiled in.
-template <class T, int R, int WPR, int MODE, int NWV>
+template <class T, int R, int WPR, int MODE, int NWV, bool ID = false>
 __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const int64_t ngroups) {
     constexpr int NT = 64 * NWV;
     constexpr int RPG = (NWV / WPR) * R;   // rows per group
@@ -597,13 +600,26 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const
         for (int k = 1; k < GEMV_MAXMAT; ++k) mi += g >= p.blk0[k] ? 1 : 0;
         row0 = (g - p.blk0[mi]) * RPG + (wave / WPR) * R;
     };
+    // ID: matrix k is the expert ids[ids_e[k]] of the stack at W[0] (MUL_MAT_ID decode), its
+    // base read once per workgroup
+    const uint8_t * Wb[GEMV_MAXMAT];
+    if constexpr (ID) {
+#pragma unroll
+        for (int k = 0; k < GEMV_MAXMAT; ++k) Wb[k] = p.W[0] + (int64_t) p.ids[p.ids_e[k]] * p.nb02;
+    }
     auto fetch = [&](int64_t g, typename T::raw (&w)[R]) {
         int mi;
         int64_t row0;
         locate(g, mi, row0);
         const int64_t M = p.M[mi];
+        const uint8_t * Wm = p.W[mi];
+        if constexpr (ID) {
+            Wm = Wb[0];
 #pragma unroll
-        for (int r = 0; r < R; ++r) T::fetch(p.W[mi] + min(row0 + r, M - 1) * p.nb01[mi], tt, w[r]);
+            for (int k = 1; k < GEMV_MAXMAT; ++k) Wm = mi == k ? Wb[k] : Wm;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) T::fetch(Wm + min(row0 + r, M - 1) * p.nb01[mi], tt, w[r]);
     };
 
     // the first group's weight loads leave before anything else, so the activation prologue,
@@ -799,7 +815,9 @@ static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
     int64_t grid = std::min<int64_t>(ng, MODE == 2 ? g_num_cu : g_gemv_wgs);
     if (MODE >= 1) grid = std::max<int64_t>(grid, ceil_div(ng, GEMV_MAXG));   // LDS-parked row sums
     const size_t lds = MODE == 2 ? prologue_lds_bytes(a.pro, a.pk) : 0;
-    if (t_ev_beg) {
+    if (MODE == 0 && a.ids) {
+        hipLaunchKernelGGL((k_gemv_pipe<T, R, WPR, 0, NWV, true>), dim3((unsigned) grid), dim3(64 * NWV), lds, st, a, ng);
+    } else if (t_ev_beg) {
         hipExtLaunchKernelGGL((k_gemv_pipe<T, R, WPR, MODE, NWV>), dim3((unsigned) grid), dim3(64 * NWV), lds, st, t_ev_beg, t_ev_end, 0, a, ng);
     } else {
         hipLaunchKernelGGL((k_gemv_pipe<T, R, WPR, MODE, NWV>), dim3((unsigned) grid), dim3(64 * NWV), lds, st, a, ng);
@@ -1001,6 +1019,58 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         ctx.pending.push_back({t_ev_beg, t_ev_end, bytes, TK_MMV});
         t_ev_beg = t_ev_end = nullptr;
     }
+}
+
+// MUL_MAT_ID of one token (decode) on the pipelined mat-vec: the routed experts are the
+// matrices of a grouped launch, their bases read from ids on the device.  A shared activation
+// (b->ne[1] == 1: up / gate) makes one launch over the n_used experts; per-slot activations
+// (down) one launch per slot.  Returns false when the pipelined kernel does not apply.
+bool gemv_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act) {
+    const ggml_tensor * as = dst->src[0];
+    const ggml_tensor * b = dst->src[1];
+    const ggml_tensor * ids = dst->src[2];
+    const ggml_type wt = as->type;
+    const int64_t n_used = ids->ne[0], K = as->ne[0];
+    if (ids->ne[1] != 1 || n_used > GEMV_MAXMAT || (b->ne[1] != 1 && b->ne[1] != n_used)) return false;
+    if (wt != GGML_TYPE_Q4_K && wt != GGML_TYPE_Q5_K && wt != GGML_TYPE_Q6_K && wt != GGML_TYPE_Q8_0 && wt != GGML_TYPE_Q4_0) return false;
+    if (ids->nb[0] % sizeof(int32_t) != 0) return false;
+    const int64_t nblk = K / ggml_blck_size(wt);
+    const int per = (wt == GGML_TYPE_Q8_0 || wt == GGML_TYPE_Q4_0) ? 1 : 4;
+    if (nblk * per > 4 * WAVE) return false;   // the pipelined kernel covers K in one pass per wave
+    const bool shared = b->ne[1] == 1;
+    const int nlaunch = shared ? 1 : (int) n_used;
+    for (int l = 0; l < nlaunch; ++l) {
+        gemv_args a = {};
+        const int nmat = shared ? (int) n_used : 1;
+        a.ids = (const int32_t *) ids->data;
+        a.nb02 = as->nb[2];
+        for (int m = 0; m < nmat; ++m) {
+            const int e = shared ? m : l;
+            a.W[m] = (const uint8_t *) as->data;
+            a.nb01[m] = as->nb[1];
+            a.M[m] = as->ne[1];
+            a.dst[m] = (float *) ((char *) dst->data + e * dst->nb[1]);
+            a.ids_e[m] = e * (int64_t) (ids->nb[0] / sizeof(int32_t));
+        }
+        for (int m = nmat; m < GEMV_MAXMAT; ++m) a.ids_e[m] = a.ids_e[0];
+        const int64_t col = shared ? 0 : l;
+        a.A = {act.qs + col * act.qs_stride(), act.d + col * act.d_stride(), act.s + col * act.s_stride()};
+        a.ntasks = (int) (nblk * per);
+        int64_t Mt = a.M[0] * nmat;
+        bool ok = false;
+        switch (wt) {
+            case GGML_TYPE_Q4_K: ok = launch_pipe_t<g_q4_K>(ctx.stream, a, nmat, Mt); break;
+            case GGML_TYPE_Q5_K: ok = launch_pipe_t<g_q5_K>(ctx.stream, a, nmat, Mt); break;
+            case GGML_TYPE_Q6_K: ok = launch_pipe_t<g_q6_K>(ctx.stream, a, nmat, Mt); break;
+            case GGML_TYPE_Q8_0: ok = launch_pipe_t<g_q8_0>(ctx.stream, a, nmat, Mt); break;
+            default:             ok = launch_pipe_t<g_q4_0>(ctx.stream, a, nmat, Mt); break;
+        }
+        if (!ok) {
+            GGML_ASSERT(l == 0 && "mi355x: pipelined MUL_MAT_ID launch refused after the first slot");
+            return false;
+        }
+    }
+    return true;
 }
 
 }  // namespace mi355x

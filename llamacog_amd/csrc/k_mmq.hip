@@ -88,6 +88,10 @@ struct mmq_args {
     const int8_t * xq; const float * xd; const int16_t * xs;   // Q8_K SoA: [T][K], [T][K/256], [T][K/16]
     int64_t T;
     float * dst; int64_t nb1;   // dst[t * nb1 + m*4]
+    // MUL_MAT_ID (expert-sorted, k_mmv.hip k_moe_sort): blockIdx.z = expert, its cnt[z] tokens are
+    // activation columns off[z] .. off[z] + cnt[z] - 1, column j is pair list[j] = e + n_used * t and
+    // lands at dst + e * nb1 + t * nb2; nullptr cnt = a plain MUL_MAT
+    const int32_t * cnt; const int32_t * off; const int32_t * list; int64_t n_used; int64_t nb02; int64_t nb2;
 };
 
 template <class W>
@@ -105,6 +109,15 @@ __global__ __launch_bounds__(256) void k_mmq(const mmq_args p) {
     const int64_t row0 = (int64_t) blockIdx.x * MQ_BM;
     const int64_t tok0 = (int64_t) blockIdx.y * MQ_BN;
     const int h = lane >> 4, c16 = lane & 15;
+    // MUL_MAT_ID: this workgroup's expert, its token count and first activation column
+    const uint8_t * Wb = p.W;
+    int64_t T = p.T, col0 = 0;
+    if (p.cnt) {
+        T = p.cnt[blockIdx.z];
+        if (tok0 >= T) return;   // uniform: no barrier passed yet
+        col0 = p.off[blockIdx.z];
+        Wb = p.W + (int64_t) blockIdx.z * p.nb02;
+    }
 
     float acc[4][4];
 #pragma unroll
@@ -120,13 +133,13 @@ __global__ __launch_bounds__(256) void k_mmq(const mmq_args p) {
         for (int c = tid; c < MQ_BM * RC; c += 256) {
             const int r = c / RC, k = c % RC;
             const int64_t row = min(row0 + r, p.M - 1);
-            const uint4 v = ld16(p.W + row * p.nb01 + b * W::BLK + 16 * k);
+            const uint4 v = ld16(Wb + row * p.nb01 + b * W::BLK + 16 * k);
             *(uint4 *) (wq + r * RS + 16 * k) = v;
         }
         for (int c0 = wave * 64; c0 < MQ_BN * 16; c0 += 256) {
             const int c = c0 + lane;
             const int t = c >> 4, part = c & 15;
-            const int64_t tok = min(tok0 + t, p.T - 1);
+            const int64_t tok = col0 + min(tok0 + t, T - 1);
             const int8_t * src = p.xq + tok * p.K + b * 256 + 16 * part;
             __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (xq + 16 * c0), 16, 0, 0);
         }
@@ -144,7 +157,7 @@ __global__ __launch_bounds__(256) void k_mmq(const mmq_args p) {
             wd[tid] = d; wdm[tid] = dmin;
         } else if (tid < MQ_BM + MQ_BN) {
             const int t = tid - MQ_BM;
-            const int64_t tok = min(tok0 + t, p.T - 1);
+            const int64_t tok = col0 + min(tok0 + t, T - 1);
             xd[t] = p.xd[tok * (p.K / 256) + b];
             const int16_t * s16 = p.xs + tok * (p.K / 16) + b * 16;
 #pragma unroll
@@ -218,11 +231,16 @@ __global__ __launch_bounds__(256) void k_mmq(const mmq_args p) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
         const int64_t t = tok0 + 16 * n + c16;
-        if (t >= p.T) continue;
+        if (t >= T) continue;
+        char * drow = (char *) p.dst + t * p.nb1;
+        if (p.cnt) {
+            const int pair = p.list[col0 + t];
+            drow = (char *) p.dst + (pair % p.n_used) * p.nb1 + (pair / p.n_used) * p.nb2;
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t m = row0 + 16 * wave + 4 * h + i;
-            if (m < p.M) *(float *) ((char *) p.dst + t * p.nb1 + m * 4) = acc[n][i];
+            if (m < p.M) *(float *) (drow + m * 4) = acc[n][i];
         }
     }
 }
@@ -257,6 +275,7 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
     p.xq = act.qs; p.xd = act.d; p.xs = act.s;
     p.T = x->ne[1];
     p.dst = (float *) dst->data; p.nb1 = dst->nb[1];
+    p.cnt = p.off = p.list = nullptr; p.n_used = 1; p.nb02 = 0; p.nb2 = 0;
     const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(p.T, MQ_BN));
     switch (w->type) {
         case GGML_TYPE_Q4_K: hipLaunchKernelGGL(k_mmq<mq_q4_K>, grid, dim3(256), 0, ctx.stream, p); break;
@@ -265,6 +284,34 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
         default: GGML_ABORT("mi355x: mmq type");
     }
     if (ctx.timing) ctx.time_end(TK_MMQ, flops, ev);
+}
+
+// MUL_MAT_ID prefill on the MFMA tile: the pairs sorted by expert (cnt/off/list) and their
+// activations quantized in that order (k_mmv.hip op_mul_mat_id); grid z = expert, workgroups past
+// an expert's token count exit at once
+bool mmq_id_supported(const ggml_tensor * dst) {
+    static const bool off = getenv("GGML_MI355X_NO_MMQ") && atoi(getenv("GGML_MI355X_NO_MMQ")) != 0;
+    const ggml_type t = dst->src[0]->type;
+    return !off && (t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K);
+}
+
+void mul_mat_q_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, const int32_t * cnt, const int32_t * off,
+                  const int32_t * list, int64_t n_pairs) {
+    const ggml_tensor * w = dst->src[0];
+    const ggml_tensor * ids = dst->src[2];
+    mmq_args p;
+    p.W = (const uint8_t *) w->data; p.nb01 = w->nb[1]; p.M = w->ne[1]; p.K = w->ne[0]; p.nblk = w->ne[0] / 256;
+    p.xq = act.qs; p.xd = act.d; p.xs = act.s;
+    p.T = n_pairs;
+    p.dst = (float *) dst->data; p.nb1 = dst->nb[1];
+    p.cnt = cnt; p.off = off; p.list = list; p.n_used = ids->ne[0]; p.nb02 = w->nb[2]; p.nb2 = dst->nb[2];
+    const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(n_pairs, MQ_BN), (unsigned) w->ne[2]);
+    switch (w->type) {
+        case GGML_TYPE_Q4_K: hipLaunchKernelGGL(k_mmq<mq_q4_K>, grid, dim3(256), 0, ctx.stream, p); break;
+        case GGML_TYPE_Q5_K: hipLaunchKernelGGL(k_mmq<mq_q5_K>, grid, dim3(256), 0, ctx.stream, p); break;
+        case GGML_TYPE_Q6_K: hipLaunchKernelGGL(k_mmq<mq_q6_K>, grid, dim3(256), 0, ctx.stream, p); break;
+        default: GGML_ABORT("mi355x: mmq id type");
+    }
 }
 
 }  // namespace mi355x

@@ -853,6 +853,11 @@ static void launch_mmv_id(hipStream_t st, const mmv_id_args & a, int64_t n_pairs
     else hipLaunchKernelGGL((k_mmv_q_idg<TASK, 8, 4>), grid, dim3(256), 0, st, a);
 }
 
+bool gemv_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act);
+bool mmq_id_supported(const ggml_tensor * dst);
+void mul_mat_q_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, const int32_t * cnt, const int32_t * off,
+                  const int32_t * list, int64_t n_pairs);
+
 void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst) {
     const ggml_tensor * as = dst->src[0];
     const ggml_tensor * b = dst->src[1];
@@ -887,6 +892,12 @@ void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst) {
             quantize_act(ctx, b, kq, act, exec_ctx::QSLOT);
             ctx.qcache_put(b, kq, act);
         }
+        // one token: the routed experts on the pipelined decode mat-vec (k_gemv.hip)
+        static const bool pipe_id = !getenv("GGML_MI355X_MMID_PIPE") || atoi(getenv("GGML_MI355X_MMID_PIPE")) != 0;
+        if (pipe_id && T == 1 && gemv_mul_mat_id(ctx, dst, act)) {
+            if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
+            return;
+        }
     } else {
         auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
         const size_t ib = al(sizeof(int32_t) * (size_t) (2 * n_as + n_pairs));
@@ -906,6 +917,12 @@ void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst) {
                                (int64_t) b->nb[2], (int64_t) b->ne[1], n_used, list, cnt, off, n_as, act.qs, act.d, act.s);
         }
         a.cnt = cnt; a.off = off; a.list = list;
+        // enough tokens per expert for the 64-token MFMA tile
+        if (n_pairs >= 64 && mmq_id_supported(dst)) {
+            mul_mat_q_id(ctx, dst, act, cnt, off, list, n_pairs);
+            if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
+            return;
+        }
     }
     a.A = {act.qs, act.d, act.s, act.qs_stride(), act.d_stride(), act.s_stride()};
     switch (as->type) {
