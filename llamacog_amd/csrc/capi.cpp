@@ -16,6 +16,7 @@ using namespace mi355x;
 
 namespace mi355x {
 bool mmv_q_supported_type(ggml_type t);
+void mul_mat_vec(exec_ctx & ctx, ggml_tensor * dst, const q8_act * pre);
 void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int64_t n, float * s);
 }
 
@@ -319,6 +320,61 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int6
         mms[m] = &Y[m];
     }
     if (!gemv_supported(mms[0])) return -1.0;
+    if (epi_kind == 7) {
+        // the general mat-vec (k_mmv_q, one weight row per wave) on matrix 0 only
+        hipEvent_t f0, f1;
+        MI_CHECK(hipEventCreate(&f0));
+        MI_CHECK(hipEventCreate(&f1));
+        auto run7 = [&](int it) { W[0].data = pool[(size_t) (it % copies) * nmat]; mul_mat_vec(sc.ex, mms[0], nullptr); };
+        for (int i = 0; i < 4; ++i) run7(i);
+        MI_CHECK(hipEventRecord(f0, sc.ex.stream));
+        for (int i = 0; i < iters; ++i) run7(i);
+        MI_CHECK(hipEventRecord(f1, sc.ex.stream));
+        MI_CHECK(hipEventSynchronize(f1));
+        float ms = 0;
+        MI_CHECK(hipEventElapsedTime(&ms, f0, f1));
+        for (auto p : pool) MI_CHECK(hipFree(p));
+        MI_CHECK(hipFree(x)); MI_CHECK(hipFree(y));
+        return ms * 1000.0 / iters;
+    }
+    if (epi_kind == 6) {
+        // MUL_MAT_ID decode: nmat = n_used experts routed out of a stack of 8 (ids 1, 5, 6),
+        // one shared activation row; the stacks rotate over `copies` copies
+        const int64_t n_as = 8;
+        std::vector<char *> stacks((size_t) copies);
+        for (auto & p : stacks) {
+            MI_CHECK(hipMalloc(&p, mat * n_as));
+            MI_CHECK(hipMemset(p, 0x11, mat * n_as));
+        }
+        int32_t * ids;
+        const int32_t hid[3] = {1, 5, 6};
+        MI_CHECK(hipMalloc(&ids, sizeof(hid)));
+        MI_CHECK(hipMemcpy(ids, hid, sizeof(hid), hipMemcpyHostToDevice));
+        float * yid;
+        MI_CHECK(hipMalloc(&yid, M * 4 * nmat));
+        ggml_tensor As, Id, Yid;
+        const int64_t nea[4] = {K, M, n_as, 1}, nei[4] = {nmat, 1, 1, 1}, ney2[4] = {M, nmat, 1, 1};
+        init_tensor(As, t, nea, stacks[0]);
+        init_tensor(Id, GGML_TYPE_I32, nei, ids);
+        init_tensor(Yid, GGML_TYPE_F32, ney2, yid);
+        Yid.op = GGML_OP_MUL_MAT_ID;
+        Yid.src[0] = &As; Yid.src[1] = &X; Yid.src[2] = &Id;
+        hipEvent_t f0, f1;
+        MI_CHECK(hipEventCreate(&f0));
+        MI_CHECK(hipEventCreate(&f1));
+        auto run_id = [&](int it) { As.data = stacks[(size_t) (it % copies)]; op_mul_mat_id(sc.ex, &Yid); };
+        for (int i = 0; i < 4; ++i) run_id(i);
+        MI_CHECK(hipEventRecord(f0, sc.ex.stream));
+        for (int i = 0; i < iters; ++i) run_id(i);
+        MI_CHECK(hipEventRecord(f1, sc.ex.stream));
+        MI_CHECK(hipEventSynchronize(f1));
+        float ms = 0;
+        MI_CHECK(hipEventElapsedTime(&ms, f0, f1));
+        for (auto p : stacks) MI_CHECK(hipFree(p));
+        for (auto p : pool) MI_CHECK(hipFree(p));
+        MI_CHECK(hipFree(ids)); MI_CHECK(hipFree(yid)); MI_CHECK(hipFree(x)); MI_CHECK(hipFree(y));
+        return ms * 1000.0 / iters;
+    }
     // epilogue / prologue operands
     gemv_epi epi;
     ggml_tensor S, Rt, P, A0, A1, Wn, Add, Nrm, Mul;

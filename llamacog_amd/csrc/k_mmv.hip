@@ -492,11 +492,16 @@ __global__ __launch_bounds__(256) void k_mmv_f(const mmv_f_args p) {
 // ------------------------------------------------------------------------------------------
 template <typename WT>
 __global__ __launch_bounds__(256) void k_mmv_f_exact(const mmv_f_args p) {
-    const int64_t row = (int64_t) blockIdx.x * 256 + threadIdx.x;
+    // one wave per row: lane s keeps the AVX-512 partial acc[s] of ggml_vec_dot_f32 (4
+    // accumulators x 16 lanes, FMA'd over the row in steps of 64), so the loads are coalesced
+    // 256-B rows and the sum order is the CPU's; lane 0 then forms REDUCE + the
+    // _mm512_reduce_add_ps tree and the scalar tail in double
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row = (int64_t) blockIdx.x * 4 + wave;
     const int64_t c = blockIdx.y;
     const int64_t i12 = blockIdx.z % p.ne12, i13 = blockIdx.z / p.ne12;
-    if (row >= p.M) return;
-    const char * wrow = p.W + (i12 / p.r2) * p.nb02 + (i13 / p.r3) * p.nb03 + row * p.nb01;
+    const bool ok = row < p.M;
+    const char * wrow = p.W + (i12 / p.r2) * p.nb02 + (i13 / p.r3) * p.nb03 + (ok ? row : 0) * p.nb01;
     const float * x = (const float *) (p.X + i12 * p.nb12 + i13 * p.nb13 + c * p.nb11);
     auto wv = [&](int64_t k) -> float {
         if constexpr (sizeof(WT) == 2) return h2f(ld2(wrow + 2 * k));
@@ -507,19 +512,21 @@ __global__ __launch_bounds__(256) void k_mmv_f_exact(const mmv_f_args p) {
         else return x[k];
     };
     const int64_t np = p.K & ~int64_t(63);
-    float acc[64];
+    float acc = 0.0f;
+#pragma unroll 8
+    for (int64_t i = 0; i < np; i += 64) acc = fmaf(wv(i + lane), xv(i + lane), acc);
+    __shared__ float part[4][64];
+    part[wave][lane] = acc;
+    __syncthreads();
+    if (ok && lane == 0) {
+        const float * a = part[wave];
+        float w[16];
 #pragma unroll
-    for (int s = 0; s < 64; ++s) acc[s] = 0.0f;
-    for (int64_t i = 0; i < np; i += 64) {
-#pragma unroll
-        for (int s = 0; s < 64; ++s) acc[s] = fmaf(wv(i + s), xv(i + s), acc[s]);
+        for (int l = 0; l < 16; ++l) w[l] = __fadd_rn(__fadd_rn(a[l], a[32 + l]), __fadd_rn(a[16 + l], a[48 + l]));
+        double sumf = (double) reduce16_avx512(w);
+        for (int64_t k = np; k < p.K; ++k) sumf += (double) __fmul_rn(wv(k), xv(k));
+        *(float *) ((char *) p.dst + i12 * p.nb2 + i13 * p.nb3 + c * p.nb1 + row * 4) = (float) sumf;
     }
-    float w[16];
-#pragma unroll
-    for (int l = 0; l < 16; ++l) w[l] = __fadd_rn(__fadd_rn(acc[l], acc[32 + l]), __fadd_rn(acc[16 + l], acc[48 + l]));
-    double sumf = (double) reduce16_avx512(w);
-    for (int64_t k = np; k < p.K; ++k) sumf += (double) __fmul_rn(wv(k), xv(k));
-    *(float *) ((char *) p.dst + i12 * p.nb2 + i13 * p.nb3 + c * p.nb1 + row * 4) = (float) sumf;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -645,7 +652,7 @@ void mul_mat_vec(exec_ctx & ctx, ggml_tensor * dst, const q8_act * pre) {
             if (src0->type == GGML_TYPE_F16) launch_mmv_f<uint16_t>(ctx.stream, a, a.ne11, nbatch);
             else launch_mmv_f<float>(ctx.stream, a, a.ne11, nbatch);
         } else {
-            dim3 grid((unsigned) ceil_div(a.M, 256), (unsigned) a.ne11, (unsigned) nbatch);
+            dim3 grid((unsigned) ceil_div(a.M, 4), (unsigned) a.ne11, (unsigned) nbatch);
             if (src0->type == GGML_TYPE_F16) hipLaunchKernelGGL(k_mmv_f_exact<uint16_t>, grid, dim3(256), 0, ctx.stream, a);
             else hipLaunchKernelGGL(k_mmv_f_exact<float>, grid, dim3(256), 0, ctx.stream, a);
         }
@@ -892,8 +899,10 @@ void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst) {
             quantize_act(ctx, b, kq, act, exec_ctx::QSLOT);
             ctx.qcache_put(b, kq, act);
         }
-        // one token: the routed experts on the pipelined decode mat-vec (k_gemv.hip)
-        static const bool pipe_id = !getenv("GGML_MI355X_MMID_PIPE") || atoi(getenv("GGML_MI355X_MMID_PIPE")) != 0;
+        // GGML_MI355X_MMID_PIPE=1: the routed experts on the pipelined decode mat-vec (k_gemv.hip).
+        // Off by default: one row per wave (k_mmv_q_id) measured faster on the Mixtral shapes —
+        // up/gate 2 x 40 MB Q5_K 23.4 vs 31.6 us, down 40 MB 11.4 vs 24.4 us (scripts/probe_mmid.py)
+        static const bool pipe_id = getenv("GGML_MI355X_MMID_PIPE") && atoi(getenv("GGML_MI355X_MMID_PIPE")) != 0;
         if (pipe_id && T == 1 && gemv_mul_mat_id(ctx, dst, act)) {
             if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
             return;

@@ -5,11 +5,13 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-# decode tokens: each llama_decode ends with one output-projection GEMV, the longest single
-# kernel of a decode step; segment the trace at those launches
+# decode tokens: every decode graph launches the RoPE table kernel once (before its first
+# Q/K projection); segment the trace there (fallback: the longest kernel, the output projection)
 dur = lambda r: int(r['End_Timestamp']) - int(r['Start_Timestamp'])
-longest = max(rows, key=dur)['Kernel_Name']
-starts = [i for i, r in enumerate(rows) if r['Kernel_Name'] == longest and dur(r) > 0.5 * dur(max(rows, key=dur))]
+starts = [i for i, r in enumerate(rows) if 'k_rope_table' in r['Kernel_Name']]
+if len(starts) < 3:
+    longest = max(rows, key=dur)['Kernel_Name']
+    starts = [i for i, r in enumerate(rows) if r['Kernel_Name'] == longest and dur(r) > 0.5 * dur(max(rows, key=dur))]
 skip = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 toks = list(zip(starts[skip:-1], starts[skip + 1:]))
 agg = collections.defaultdict(lambda: [0, 0.0])
@@ -23,7 +25,7 @@ for a, b in toks:
         n = r['Kernel_Name'].split('(')[0].replace('void mi355x::', '')[:56] + f" g{int(r.get('Grid_Size_X', r.get('Grid_Size', 0))) // int(r.get('Workgroup_Size_X', r.get('Workgroup_Size', 1)) or 1)}"
         agg[n][0] += 1
         agg[n][1] += d
-nt = len(toks)
+nt = max(len(toks), 1)
 print(f"tokens {nt}: wall {wall / nt:.1f} us/token, kernel busy {busy / nt:.1f} us/token, "
       f"launches {sum(v[0] for v in agg.values()) / nt:.1f}/token")
 for n, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1]):
