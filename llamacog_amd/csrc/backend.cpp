@@ -506,10 +506,15 @@ static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.done.clear();
     ex.pend = exec_ctx::pending_pro();
     ex.post_add = nullptr;
+    ex.silu_defer = ex.silu_mul = nullptr;
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) {
         ex.cur_node = i;
         i += op_compute(ex, cgraph, i);
+    }
+    if (ex.silu_defer) {   // a deferred SILU whose MUL never came
+        op_unary(ex, ex.silu_defer);
+        ex.silu_defer = ex.silu_mul = nullptr;
     }
     if (ex.post_add) {   // a deferred in-place ADD with no later launch to carry it
         op_binary(ex, ex.post_add);

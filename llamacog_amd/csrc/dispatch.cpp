@@ -622,8 +622,56 @@ static void norm_stores(ggml_cgraph * g, int n, ggml_tensor * norm, ggml_tensor 
     if (mul) store_mul = !dead; else store_norm = !dead;
 }
 
+// The MoE router (build_moe_ffn, src/llama-graph.cpp:661-712) in two launches instead of five.
+// At the SOFT_MAX: the ARGSORT (DESC, ggml_top_k) of its output follows after views only.  At the
+// GET_ROWS of the probabilities by the top-k view: SUM_ROWS and the DIV follow after views only
+// (the expert mat-muls lie between the two halves in graph order).
+static bool try_moe_sort(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * sm = ggml_graph_node(g, i);
+    float max_bias = 0.0f;
+    memcpy(&max_bias, (const float *) sm->op_params + 1, sizeof(float));
+    if (sm->src[1] || sm->src[2] || max_bias != 0.0f || !f32c(sm) || !f32c(sm->src[0])) return false;
+    for (int j = i + 1; j < n && j <= i + 4; ++j) {
+        ggml_tensor * c = ggml_graph_node(g, j);
+        if (is_view_op(c)) continue;
+        if (c->op == GGML_OP_ARGSORT && c->src[0] == sm && c->op_params[0] == GGML_SORT_ORDER_DESC &&
+            c->type == GGML_TYPE_I32 && moe_route_sort(ctx, sm, c)) {
+            ctx.done.push_back(c);
+            return true;
+        }
+        return false;
+    }
+    return false;
+}
+
+static bool try_moe_weights(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * gr = ggml_graph_node(g, i);
+    const ggml_tensor * pb = base_of(gr->src[0]), * ib = base_of(gr->src[1]);
+    if (!pb || !ib || pb->op != GGML_OP_SOFT_MAX || ib->op != GGML_OP_ARGSORT || gr->type != GGML_TYPE_F32) return false;
+    ggml_tensor * sr = nullptr, * dv = nullptr;
+    for (int j = i + 1; j < n && j <= i + 6; ++j) {
+        ggml_tensor * c = ggml_graph_node(g, j);
+        if (is_view_op(c)) continue;
+        if (!sr && c->op == GGML_OP_SUM_ROWS && base_of(c->src[0]) == gr && c->type == GGML_TYPE_F32) { sr = c; continue; }
+        if (sr && c->op == GGML_OP_DIV && base_of(c->src[0]) == gr && c->src[1] == sr && c->type == GGML_TYPE_F32) dv = c;
+        break;
+    }
+    if (!sr || !dv || !moe_route_weights(ctx, gr, sr, dv)) return false;
+    ctx.done.push_back(sr);
+    ctx.done.push_back(dv);
+    return true;
+}
+
 int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
     ggml_tensor * node = ggml_graph_node(cgraph, i);
+    if (ctx.silu_defer && node != ctx.silu_mul && !is_view_op(node)) {
+        bool reads = false;
+        for (int k = 0; k < GGML_MAX_SRC; ++k) reads = reads || (node->src[k] && overlaps(node->src[k], ctx.silu_defer));
+        if (reads || overlaps(node, ctx.silu_defer) || overlaps(node, ctx.silu_defer->src[0])) {
+            op_unary(ctx, ctx.silu_defer);   // something else needs it now: run it stand-alone
+            ctx.silu_defer = ctx.silu_mul = nullptr;
+        }
+    }
     if (ctx.pend.kind && ctx.pend.consumer != node) {
         // the deferred producer chain must run before anything else: do it stand-alone
         const auto pd = ctx.pend;
@@ -663,6 +711,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             op_mul_mat(ctx, node);
             return 1;
         case GGML_OP_GET_ROWS:
+            if (fusion_enabled() && try_moe_weights(ctx, cgraph, i, n)) return 1;
             op_get_rows(ctx, node);
             return 1;
         case GGML_OP_RMS_NORM: {
@@ -702,6 +751,16 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             op_binary(ctx, node);
             return 1;
         case GGML_OP_MUL:
+            if (ctx.silu_defer && node == ctx.silu_mul) {
+                ggml_tensor * sl = ctx.silu_defer;
+                ctx.silu_defer = ctx.silu_mul = nullptr;
+                ggml_tensor * mm = at(cgraph, i + 1, n);
+                const bool smul = !(mm && mm->op == GGML_OP_MUL_MAT && dead_after(cgraph, n, i + 1, node, {mm}));
+                if (fused_silu_mul_quant(ctx, sl, node, mm, false, smul)) return 1;
+                op_unary(ctx, sl);
+                op_binary(ctx, node);
+                return 1;
+            }
             // gated-FFN product feeding the down projection: multiply + quantize in one pass
             if (fusion_enabled()) {
                 if (defer_to_prologue(ctx, cgraph, n, 2, nullptr, nullptr, node, at(cgraph, i + 1, n))) return 1;
@@ -722,9 +781,17 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             // (graph order is gate, SILU, up, MUL: the up projection ran in the gate's grouped
             // launch, so the MUL is hoisted over it when nothing in between is touched)
             if (fusion_enabled() && ggml_get_unary_op(node) == GGML_UNARY_OP_SILU) {
+                const ggml_tensor * between = nullptr;   // one node computing the MUL's other input
                 for (int j = i + 1; j < n && j <= i + 4; ++j) {
                     ggml_tensor * c = ggml_graph_node(cgraph, j);
                     if (c->op == GGML_OP_MUL && c->src[0] == node && c->src[1] != node) {
+                        if (between && base_of(c->src[1]) == between && dead_after(cgraph, n, i + 1, node, {c}) &&
+                            !overlaps(between, node) && !overlaps(between, node->src[0])) {
+                            // MoE order (gate, SILU, up, MUL): the SILU waits for the MUL
+                            ctx.silu_defer = node;
+                            ctx.silu_mul = c;
+                            return 1;
+                        }
                         const ggml_tensor * o[1] = {c};
                         const std::vector<const ggml_tensor *> skip(ctx.done.begin(), ctx.done.end());
                         if (!computed_before(ctx, cgraph, c->src[1], i) || !can_hoist(cgraph, i, j, o, 1, skip)) break;
@@ -738,7 +805,12 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                         }
                         break;
                     }
-                    if (!is_view_op(c) && std::find(ctx.done.begin(), ctx.done.end(), c) == ctx.done.end()) break;
+                    if (is_view_op(c) || std::find(ctx.done.begin(), ctx.done.end(), c) != ctx.done.end()) continue;
+                    // a projection that reads neither the SILU nor writes its input may run first
+                    bool reads = false;
+                    for (int k = 0; k < GGML_MAX_SRC; ++k) reads = reads || (c->src[k] && base_of(c->src[k]) == node);
+                    if (between || reads || (c->op != GGML_OP_MUL_MAT && c->op != GGML_OP_MUL_MAT_ID)) break;
+                    between = c;
                 }
             }
             op_unary(ctx, node);
@@ -755,6 +827,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             op_rope(ctx, node);
             return 1;
         case GGML_OP_SOFT_MAX:
+            if (fusion_enabled() && try_moe_sort(ctx, cgraph, i, n)) return 1;
             op_soft_max(ctx, node);
             return 1;
         case GGML_OP_MUL_MAT_ID:

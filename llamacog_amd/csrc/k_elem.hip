@@ -691,4 +691,122 @@ void op_sum_rows(exec_ctx & ctx, ggml_tensor * dst) {
                        mk(src), (char *) dst->data, mk(dst), nrows);
 }
 
+// ------------------------------------------------------------------------------------------
+// MoE router chain in one launch (build_moe_ffn, src/llama-graph.cpp:661-712, softmax gating
+// with norm_w): probs = SOFT_MAX(logits * scale), order = ARGSORT(probs, DESC) (ggml_top_k's
+// view keeps its first n_used), w = GET_ROWS(probs, top-k), sum = SUM_ROWS(w), wn = w / sum.
+// One lane per token; every output node is written with the arithmetic of its stand-alone
+// kernel above (k_soft_max's chunked AVX-512 exp + double sum for n >= 16, libm expf tail;
+// the exchange sort; the double row sum; the broadcast DIV), so fused and unfused graphs agree
+// bit for bit.  Replaces five small launches per MoE layer.
+// ------------------------------------------------------------------------------------------
+struct moe_route_args {
+    const char * logits; int64_t nb_l;
+    char * probs; int64_t nb_p;
+    char * order; int64_t nb_o;
+    char * w; int64_t nb_w;           // GET_ROWS output rows ([1, n_used, T]: row t at t * nb_w)
+    char * wsum; int64_t nb_s;        // SUM_ROWS output (nullable)
+    char * wn; int64_t nb_n;          // DIV output rows (nullable)
+    int n_exp, n_used;
+    int64_t T;
+    float scale;
+    int stage;                        // bit 0: SOFT_MAX + ARGSORT; bit 1: GET_ROWS [+ SUM_ROWS + DIV]
+};
+
+__global__ __launch_bounds__(64) void k_moe_route(const moe_route_args a) {
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.T) return;
+    const float * x = (const float *) (a.logits + t * a.nb_l);
+    float * p = (float *) (a.probs + t * a.nb_p);
+    int32_t * o = (int32_t *) (a.order + t * a.nb_o);
+    const int n = a.n_exp;
+    if (a.stage & 1) {
+    float mx = -INFINITY;
+    for (int i = 0; i < n; ++i) {
+        const float v = __fmul_rn(x[i], a.scale);
+        p[i] = v;
+        mx = fmaxf(mx, v);
+    }
+    const int nch = n / 16;
+    double s = 0.0;
+    for (int c = 0; c < nch; ++c) {
+        float e[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            e[k] = v_expf_avx512(__fsub_rn(p[16 * c + k], mx));
+            p[16 * c + k] = e[k];
+        }
+        s += (double) reduce16_avx512(e);
+    }
+    for (int i = 16 * nch; i < n; ++i) {
+        const float e = expf_cr(__fsub_rn(p[i], mx));
+        p[i] = e;
+        s += (double) e;
+    }
+    const float inv = (float) (1.0 / s);
+    for (int i = 0; i < n; ++i) p[i] = __fmul_rn(p[i], inv);
+    for (int j = 0; j < n; ++j) o[j] = j;
+    for (int j = 0; j < n; ++j) {
+        for (int k = j + 1; k < n; ++k) {
+            if (p[o[j]] < p[o[k]]) {   // GGML_SORT_ORDER_DESC
+                const int32_t tmp = o[j];
+                o[j] = o[k];
+                o[k] = tmp;
+            }
+        }
+    }
+    }
+    if (!(a.stage & 2)) return;
+    float * wr = (float *) (a.w + t * a.nb_w);
+    double ws = 0.0;
+    for (int k = 0; k < a.n_used; ++k) {
+        wr[k] = p[o[k]];
+        ws += (double) wr[k];
+    }
+    if (a.wsum) {
+        const float sf = (float) ws;
+        *(float *) (a.wsum + t * a.nb_s) = sf;
+        if (a.wn) {
+            float * nr = (float *) (a.wn + t * a.nb_n);
+            for (int k = 0; k < a.n_used; ++k) nr[k] = wr[k] / sf;
+        }
+    }
+}
+
+// stage 1 (at the SOFT_MAX): probabilities and their descending order; as = the ARGSORT node
+bool moe_route_sort(exec_ctx & ctx, const ggml_tensor * sm, ggml_tensor * as) {
+    const int64_t n = sm->ne[0], T = ggml_nrows(sm);
+    if (n > 256 || !ggml_is_contiguous(sm) || !ggml_is_contiguous(sm->src[0]) || !ggml_is_contiguous(as) ||
+        as->ne[0] != n || ggml_nrows(as) != T) return false;
+    moe_route_args a = {};
+    a.logits = (const char *) sm->src[0]->data; a.nb_l = sm->src[0]->nb[1];
+    a.probs = (char *) sm->data; a.nb_p = sm->nb[1];
+    a.order = (char *) as->data; a.nb_o = as->nb[1];
+    a.n_exp = (int) n; a.T = T; a.stage = 1;
+    memcpy(&a.scale, sm->op_params, sizeof(float));
+    hipLaunchKernelGGL(k_moe_route, dim3((unsigned) ceil_div(T, 64)), dim3(64), 0, ctx.stream, a);
+    return true;
+}
+
+// stage 2 (at the GET_ROWS): the routed experts' probabilities, their sum and the normalised
+// weights; probabilities and order as stage 1 (or the stand-alone kernels) stored them
+bool moe_route_weights(exec_ctx & ctx, ggml_tensor * gr, ggml_tensor * sr, ggml_tensor * dv) {
+    const ggml_tensor * pr = gr->src[0];   // [1, n_exp, T] view of the probabilities
+    const ggml_tensor * ids = gr->src[1];  // [n_used, T] view of the order
+    const int64_t n = pr->ne[1], T = pr->ne[2], n_used = ids->ne[0];
+    if (n > 256 || n_used > n || ids->ne[1] != T || pr->nb[1] != sizeof(float) || ids->nb[0] != sizeof(int32_t)) return false;
+    if (gr->ne[0] != 1 || gr->ne[1] != n_used || gr->ne[2] != T || !ggml_is_contiguous(gr)) return false;
+    if (!sr || !dv || sr->src[0]->data != gr->data || ggml_nelements(sr) != T || !ggml_is_contiguous(sr)) return false;
+    if (dv->src[1] != sr || dv->src[0]->data != gr->data || ggml_nelements(dv) != T * n_used || !ggml_is_contiguous(dv)) return false;
+    moe_route_args a = {};
+    a.probs = (char *) pr->data; a.nb_p = pr->nb[2];
+    a.order = (char *) ids->data; a.nb_o = ids->nb[1];
+    a.w = (char *) gr->data; a.nb_w = gr->nb[2];
+    a.wsum = (char *) sr->data; a.nb_s = sizeof(float);
+    a.wn = (char *) dv->data; a.nb_n = sizeof(float) * n_used;
+    a.n_exp = (int) n; a.n_used = (int) n_used; a.T = T; a.stage = 2;
+    hipLaunchKernelGGL(k_moe_route, dim3((unsigned) ceil_div(T, 64)), dim3(64), 0, ctx.stream, a);
+    return true;
+}
+
 }  // namespace mi355x

@@ -84,6 +84,10 @@ struct exec_ctx {
         bool need_elide_norm = false;      // deferral valid only if the launch elides these
         bool need_elide_mul = false;
     } pend;
+    // a SILU whose MUL partner's other input (the up projection) is computed after it (MoE:
+    // gate, SILU, up, MUL): run as one silu*mul kernel at the MUL (dispatch.cpp)
+    ggml_tensor * silu_defer = nullptr;
+    ggml_tensor * silu_mul = nullptr;
     // an in-place residual ADD whose inputs the previous GEMV prologue read: the next GEMV
     // launch stores it (workgroup 0), before any node can read it
     ggml_tensor * post_add = nullptr;
@@ -158,6 +162,9 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm = n
 void op_argsort(exec_ctx & ctx, ggml_tensor * dst);
 void op_sum_rows(exec_ctx & ctx, ggml_tensor * dst);
 void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst);
+// the MoE router chain (k_elem.hip): SOFT_MAX + ARGSORT in one launch, GET_ROWS + SUM_ROWS + DIV in another
+bool moe_route_sort(exec_ctx & ctx, const ggml_tensor * sm, ggml_tensor * as);
+bool moe_route_weights(exec_ctx & ctx, ggml_tensor * gr, ggml_tensor * sr, ggml_tensor * dv);
 
 // quantizes ncols rows of an f32 tensor (row i = (i1, i2, i3) flattened) into act
 void quantize_act(exec_ctx & ctx, const ggml_tensor * src, bool k_quant, q8_act & act, int slot);

@@ -85,7 +85,7 @@ def test_greedy_llama3_8b_2layer_q4km():
     print("llama3-8b-2l max rel logit err", max(rel))
 
 
-@pytest.mark.parametrize("cfg", ["llama3-8b-2l-q4km", "tiny-q8_0"])
+@pytest.mark.parametrize("cfg", ["llama3-8b-2l-q4km", "tiny-q8_0", "tiny-moe-q5km"])
 def test_fused_and_graph_replay_bit_identical(cfg):
     """The fused producers (k_fused.hip) and hipGraph replay change no bit of the logits:
     fused + replayed vs one-kernel-per-node eager on the same prompt."""
