@@ -644,6 +644,30 @@ static bool try_moe_sort(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     return false;
 }
 
+// The expert outputs weighted and summed (build_moe_ffn :761-777, n_used = 2): MUL(experts,
+// weights) followed, after views only, by the ADD of its two slot views.  One launch; the MUL
+// output is not stored when only that ADD reads it.
+static bool try_moe_combine(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * mul = ggml_graph_node(g, i);
+    const ggml_tensor * e = mul->src[0], * w = mul->src[1];
+    if (!f32c(mul) || !f32c(e) || !w || w->type != GGML_TYPE_F32 || mul->ne[1] != 2 || w->ne[0] != 1 || w->ne[1] != 2 ||
+        w->ne[2] != mul->ne[2] || mul->ne[3] != 1 || !ggml_are_same_shape(mul, e)) return false;
+    for (int j = i + 1; j < n && j <= i + 6; ++j) {
+        ggml_tensor * c = ggml_graph_node(g, j);
+        if (is_view_op(c)) continue;
+        if (c->op != GGML_OP_ADD || !f32c(c) || base_of(c->src[0]) != mul || base_of(c->src[1]) != mul) return false;
+        const ggml_tensor * v0 = c->src[0], * v1 = c->src[1];
+        if (v0->data != mul->data || (const char *) v1->data != (const char *) mul->data + mul->nb[1]) return false;
+        if (v0->ne[0] != mul->ne[0] || v0->ne[1] != mul->ne[2] || v0->nb[1] != mul->nb[2] || v1->nb[1] != mul->nb[2] ||
+            c->ne[0] != mul->ne[0] || c->ne[1] != mul->ne[2]) return false;
+        if (!dead_after(g, n, i + 1, mul, {c}) || overlaps(c, e) || overlaps(c, w)) return false;
+        moe_combine(ctx, mul, c);
+        ctx.done.push_back(c);
+        return true;
+    }
+    return false;
+}
+
 static bool try_moe_weights(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     ggml_tensor * gr = ggml_graph_node(g, i);
     const ggml_tensor * pb = base_of(gr->src[0]), * ib = base_of(gr->src[1]);
@@ -755,12 +779,14 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                 ggml_tensor * sl = ctx.silu_defer;
                 ctx.silu_defer = ctx.silu_mul = nullptr;
                 ggml_tensor * mm = at(cgraph, i + 1, n);
-                const bool smul = !(mm && mm->op == GGML_OP_MUL_MAT && dead_after(cgraph, n, i + 1, node, {mm}));
+                const bool smul = !(mm && (mm->op == GGML_OP_MUL_MAT || mm->op == GGML_OP_MUL_MAT_ID) &&
+                                    dead_after(cgraph, n, i + 1, node, {mm}));
                 if (fused_silu_mul_quant(ctx, sl, node, mm, false, smul)) return 1;
                 op_unary(ctx, sl);
                 op_binary(ctx, node);
                 return 1;
             }
+            if (fusion_enabled() && try_moe_combine(ctx, cgraph, i, n)) return 1;
             // gated-FFN product feeding the down projection: multiply + quantize in one pass
             if (fusion_enabled()) {
                 if (defer_to_prologue(ctx, cgraph, n, 2, nullptr, nullptr, node, at(cgraph, i + 1, n))) return 1;

@@ -809,4 +809,26 @@ bool moe_route_weights(exec_ctx & ctx, ggml_tensor * gr, ggml_tensor * sr, ggml_
     return true;
 }
 
+// MoE output: MUL(experts [ne0, 2, T], weights [1, 2, T]) then ADD of its two slot views, with
+// the unfused arithmetic (m_k = e_k * w_k rounded, then m_0 + m_1); one element per lane
+__global__ __launch_bounds__(256) void k_moe_combine(const char * __restrict__ e, int64_t nb_e1, int64_t nb_e2,
+                                                     const char * __restrict__ w, int64_t nb_w1, int64_t nb_w2,
+                                                     char * __restrict__ out, int64_t nb_o1, int64_t ne0) {
+    const int64_t t = blockIdx.y;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ne0) return;
+    const float w0 = *(const float *) (w + t * nb_w2), w1 = *(const float *) (w + nb_w1 + t * nb_w2);
+    const float m0 = __fmul_rn(((const float *) (e + t * nb_e2))[i], w0);
+    const float m1 = __fmul_rn(((const float *) (e + nb_e1 + t * nb_e2))[i], w1);
+    ((float *) (out + t * nb_o1))[i] = __fadd_rn(m0, m1);
+}
+
+void moe_combine(exec_ctx & ctx, const ggml_tensor * mul, ggml_tensor * add) {
+    const ggml_tensor * e = mul->src[0], * w = mul->src[1];
+    const dim3 grid((unsigned) ceil_div(mul->ne[0], 256), (unsigned) mul->ne[2]);
+    hipLaunchKernelGGL(k_moe_combine, grid, dim3(256), 0, ctx.stream, (const char *) e->data, (int64_t) e->nb[1],
+                       (int64_t) e->nb[2], (const char *) w->data, (int64_t) w->nb[1], (int64_t) w->nb[2], (char *) add->data,
+                       (int64_t) add->nb[1], mul->ne[0]);
+}
+
 }  // namespace mi355x

@@ -161,7 +161,8 @@ bool mmv_q_supported_type(ggml_type t);
 
 // vec_dot_type quantization wanted by a MUL_MAT consumer of `x` (0 = none / not fusable)
 static int consumer_qmode(const ggml_tensor * mm, const ggml_tensor * x) {
-    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != x) return 0;
+    // MUL_MAT_ID: the decode path (<= 8 routed pairs) takes the cached activation as well
+    if (!mm || (mm->op != GGML_OP_MUL_MAT && mm->op != GGML_OP_MUL_MAT_ID) || mm->src[1] != x) return 0;
     const ggml_type t = mm->src[0]->type;
     if (!mmv_q_supported_type(t)) return 0;
     if (mm->src[1]->ne[1] * mm->src[1]->ne[2] * mm->src[1]->ne[3] > 8) return 0;   // mat-vec path only

@@ -165,6 +165,9 @@ void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst);
 // the MoE router chain (k_elem.hip): SOFT_MAX + ARGSORT in one launch, GET_ROWS + SUM_ROWS + DIV in another
 bool moe_route_sort(exec_ctx & ctx, const ggml_tensor * sm, ggml_tensor * as);
 bool moe_route_weights(exec_ctx & ctx, ggml_tensor * gr, ggml_tensor * sr, ggml_tensor * dv);
+// out = experts[:, 0] * w0 + experts[:, 1] * w1 per token: the MUL by the routing weights and the ADD
+// of its two slot views in one launch (k_elem.hip)
+void moe_combine(exec_ctx & ctx, const ggml_tensor * mul, ggml_tensor * add);
 
 // quantizes ncols rows of an f32 tensor (row i = (i1, i2, i3) flattened) into act
 void quantize_act(exec_ctx & ctx, const ggml_tensor * src, bool k_quant, q8_act & act, int slot);
