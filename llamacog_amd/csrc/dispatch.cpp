@@ -601,6 +601,26 @@ static int op_rope_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     return 1;
 }
 
+// A MoE FFN norm feeds the f32 router first; the expert MUL_MAT_ID behind it reads a reshape of
+// the same output: quantize for that consumer instead (qkey = the reshape), so it needs no
+// quantize launch of its own
+static ggml_tensor * moe_quant_consumer(ggml_cgraph * g, int n, const ggml_tensor * out, const ggml_tensor * mm,
+                                        const ggml_tensor ** qkey) {
+    if (!mm || mm->op != GGML_OP_MUL_MAT || mmv_q_supported_type(mm->src[0]->type)) return nullptr;
+    const int p = node_index(g, mm);
+    for (int k = p + 1; k < n && k <= p + 16; ++k) {
+        ggml_tensor * c = ggml_graph_node(g, k);
+        if (c->op != GGML_OP_MUL_MAT_ID) continue;
+        const ggml_tensor * b = c->src[1];
+        if (base_of(b) == base_of(out) && b->data == out->data && ggml_is_contiguous(b) && ggml_nelements(b) == ggml_nelements(out)) {
+            *qkey = b;
+            return c;
+        }
+        return nullptr;
+    }
+    return nullptr;
+}
+
 // which outputs of a fused [ADD] -> RMS_NORM -> [MUL] chain feeding mat-vec `mm` must be stored:
 // the norm output when something other than the MUL reads it; the last output when something
 // other than the decode mat-vecs that consume it through the quantized-activation cache reads it
@@ -750,7 +770,9 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                 ggml_tensor * mm = at(cgraph, i + (mul ? 2 : 1), n);
                 bool sn, sm;
                 norm_stores(cgraph, n, node, mul, mm, sn, sm);
-                if (fused_norm(ctx, nullptr, node, mul, mm, sn, sm)) return mul ? 2 : 1;
+                const ggml_tensor * qkey = nullptr;
+                if (ggml_tensor * c = moe_quant_consumer(cgraph, n, mul ? mul : node, mm, &qkey)) mm = c;
+                if (fused_norm(ctx, nullptr, node, mul, mm, sn, sm, qkey)) return mul ? 2 : 1;
             }
             op_rms_norm(ctx, node, mul ? mul->src[1] : nullptr, mul);
             return mul ? 2 : 1;
@@ -769,7 +791,9 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                     ggml_tensor * mm = at(cgraph, i + used, n);
                     bool sn, sm;
                     norm_stores(cgraph, n, nx, mul, mm, sn, sm);
-                    if (fused_norm(ctx, node, nx, mul, mm, sn, sm)) return used;
+                    const ggml_tensor * qkey = nullptr;
+                    if (ggml_tensor * c = moe_quant_consumer(cgraph, n, mul ? mul : nx, mm, &qkey)) mm = c;
+                    if (fused_norm(ctx, node, nx, mul, mm, sn, sm, qkey)) return used;
                 }
             }
             op_binary(ctx, node);

@@ -172,7 +172,7 @@ static int consumer_qmode(const ggml_tensor * mm, const ggml_tensor * x) {
 }
 
 bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm,
-                bool store_norm, bool store_mul) {
+                bool store_norm, bool store_mul, const ggml_tensor * qkey) {
     const int64_t ne0 = norm->ne[0];
     // ne0 <= 4096: one float4 per thread; above: whole 4096-element slices per 1024 threads
     if (ne0 % 256 != 0 || (ne0 > 4096 && ne0 % 4096 != 0) || ne0 > 16384) return false;
@@ -181,7 +181,8 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
                 !ggml_are_same_shape(add, norm) || norm->src[0] != add)) return false;
     if (mul && (!f32_contig(mul) || !f32_contig(mul->src[1]) || ggml_nelements(mul->src[1]) != ne0)) return false;
     const ggml_tensor * out = mul ? mul : norm;
-    const int qmode = consumer_qmode(mm, out);
+    const ggml_tensor * key = qkey ? qkey : out;
+    const int qmode = consumer_qmode(mm, key);
     const int64_t nrows = ggml_nrows(norm);
 
     norm_fused_args p;
@@ -217,7 +218,7 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
         case 3: hipLaunchKernelGGL(k_norm_fused<3>, grid, block, 0, ctx.stream, p); break;
         default: hipLaunchKernelGGL(k_norm_fused<4>, grid, block, 0, ctx.stream, p); break;
     }
-    if (qmode) ctx.qcache_put(out, qmode == 1, act);
+    if (qmode) ctx.qcache_put(key, qmode == 1, act);
     return true;
 }
 

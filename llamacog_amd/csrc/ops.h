@@ -199,8 +199,10 @@ void carve_act(q8_act & act, void * base, int64_t K, int64_t ncols, bool k_quant
 // fused producers (k_fused.hip); false = pattern not applicable, nothing launched
 // store_norm / store_mul = false: that output is read by no later node (dispatch.cpp dead_after;
 // the consuming mat-vecs take the quantized activation from the cache), so it is not written
+// qkey: the tensor the quantized activation is cached under when the consumer `mm` reads a
+// reshape of the chain's output (a MoE MUL_MAT_ID behind the router); nullptr = the output itself
 bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm,
-                bool store_norm = true, bool store_mul = true);
+                bool store_norm = true, bool store_mul = true, const ggml_tensor * qkey = nullptr);
 bool fused_mul_quant(exec_ctx & ctx, ggml_tensor * mul, const ggml_tensor * mm);
 bool fused_silu_mul_quant(exec_ctx & ctx, ggml_tensor * silu, ggml_tensor * mul, const ggml_tensor * mm, bool store_silu,
                           bool store_mul = true);
