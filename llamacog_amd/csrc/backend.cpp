@@ -347,7 +347,9 @@ static void graph_signature(ggml_cgraph * cgraph, std::vector<int64_t> & sig) {
         const ggml_tensor * t = ggml_graph_node(cgraph, i);
         if (t->op == GGML_OP_CPY) { dyn.push_back(t); dyn.push_back(t->src[1]); }
     }
-    auto is_dyn = [&](const ggml_tensor * t) { return std::find(dyn.begin(), dyn.end(), t) != dyn.end(); };
+    // sorted: ~11 lookups per node over ~650 nodes every token (host time of graph_compute)
+    std::sort(dyn.begin(), dyn.end());
+    auto is_dyn = [&](const ggml_tensor * t) { return std::binary_search(dyn.begin(), dyn.end(), t); };
     auto put_tensor = [&](const ggml_tensor * t) {
         sig.push_back(is_dyn(t) ? 0 : (int64_t) (intptr_t) t->data);
         sig.push_back((int64_t) t->type);
