@@ -177,7 +177,7 @@ def main():
     fa_ms, fa_bytes, fa_n = la.kernel_timing(plugin, 2)
     achieved = (mv_bytes / (mv_ms * 1e-3)) / 1e9 if mv_ms > 0 else None
     # HBM bytes per GEMV launch from the PMC pass (rocprofv3 --pmc FETCH_SIZE, x2 gfx950
-    # correction), committed with its command under profiles/ (scripts/gpu_round_artifacts.sh)
+    # correction), committed with its command under profiles/ (scripts/gpu_final.sh, scripts/pmc_traffic.py)
     traffic = None
     if os.path.exists(TRAFFIC_FILE):
         try:
