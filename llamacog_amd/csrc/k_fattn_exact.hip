@@ -349,7 +349,15 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
     // ---- output and its optional quantization ------------------------------------------------
     float * drow = (float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H + h * a.nb1_dst + iq3 * a.nb2_dst);
     const float o = d < D ? __fmul_rn(h2f((uint16_t) yb), 1.0f / S) : 0.0f;
-    if (d < D) drow[d] = o;
+    // a Q8_K block spanning several heads is handed to the last of their workgroups: the
+    // outputs are stored write-through (sc1) and drained before the counter add, and read
+    // back with sc1 loads, so no L2 write-back fence is needed (MI355X_MICROARCH.md,
+    // inter-workgroup visibility, first hand-off row)
+    constexpr bool handoff = D < 256;
+    if (d < D) {
+        if (handoff && a.qmode == 1) __hip_atomic_store(drow + d, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else drow[d] = o;
+    }
     if (a.qmode == 2) {
         // Q8_0: the head's D outputs are D/32 whole blocks of the flat [H*D] row
         const int64_t K = a.H * D;
@@ -371,10 +379,10 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
         const int64_t blk = (h * D) / 256;
         __shared__ int is_last;
         if (NH > 1) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
             __syncthreads();
             if (tid == 0) {
-                const int prev = __hip_atomic_fetch_add(a.cnt + blk, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                const int prev = __hip_atomic_fetch_add(a.cnt + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 is_last = prev == NH - 1;
                 if (is_last) __hip_atomic_store(a.cnt + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }

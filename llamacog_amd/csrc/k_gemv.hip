@@ -793,6 +793,7 @@ template <> struct is_kq_t<g_q6_K> { static constexpr bool value = true; };
 
 static int g_gemv_pipe = -1;   // GGML_MI355X_GEMV_PIPE: 0 disables the pipelined kernel
 static int g_gemv_wgs = -1;    // GGML_MI355X_GEMV_WGS: persistent grid size
+static int g_gemv_bal = -1;    // GGML_MI355X_GEMV_BAL: 1 = balanced resident grid (k rounds: k + 1)
 
 static int g_num_cu = 0;
 
@@ -813,6 +814,19 @@ static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
         g_num_cu = prop.multiProcessorCount;
     }
     int64_t grid = std::min<int64_t>(ng, MODE == 2 ? g_num_cu : g_gemv_wgs);
+    if (g_gemv_bal && MODE != 2) {
+        // balanced resident grid: every workgroup resident at once and the same number of
+        // groups (+-1 only when ng does not divide) per workgroup, so no second round of
+        // workgroups and no tail of single-group waves
+        static int occ = -1;
+        if (occ < 0) {
+            MI_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(&k_gemv_pipe<T, R, WPR, MODE, NWV>), 64 * NWV, 0));
+            occ = std::max(occ, 1);
+        }
+        const int64_t cap = (int64_t) occ * g_num_cu * (g_gemv_bal >= 2 ? g_gemv_bal - 1 : 1);
+        const int64_t per = ceil_div(ng, cap);
+        grid = ceil_div(ng, per);
+    }
     if (MODE >= 1) grid = std::max<int64_t>(grid, ceil_div(ng, GEMV_MAXG));   // LDS-parked row sums
     const size_t lds = MODE == 2 ? prologue_lds_bytes(a.pro, a.pk) : 0;
     if (MODE == 0 && a.ids) {
@@ -844,6 +858,7 @@ template <class T>
 static bool launch_pipe_t(hipStream_t st, gemv_args & a, int nmat, int64_t Mt) {
     if (g_gemv_pipe < 0) g_gemv_pipe = getenv("GGML_MI355X_GEMV_PIPE") ? atoi(getenv("GGML_MI355X_GEMV_PIPE")) : 1;
     if (g_gemv_wgs < 0) g_gemv_wgs = getenv("GGML_MI355X_GEMV_WGS") ? atoi(getenv("GGML_MI355X_GEMV_WGS")) : 2048;
+    if (g_gemv_bal < 0) g_gemv_bal = getenv("GGML_MI355X_GEMV_BAL") ? atoi(getenv("GGML_MI355X_GEMV_BAL")) : 0;
     if (!g_gemv_pipe || a.ntasks > 4 * WAVE) return false;
     if (a.need_pairs && a.rp.n_dims > 2 * GEMV_ROPE_MAXPAIRS) return false;
     const int wpr = a.ntasks <= WAVE ? 1 : (a.ntasks <= 2 * WAVE ? 2 : 4);
