@@ -462,7 +462,17 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
         ggml_tensor * c = ggml_graph_node(g, j);
         if (c->op != GGML_OP_MUL_MAT || c->src[1] != mm0->src[1] || !gemv_supported(c)) continue;
         if (std::find(ctx.done.begin(), ctx.done.end(), c) != ctx.done.end()) continue;
-        if (c->src[0]->type != mm0->src[0]->type || c->src[0]->ne[0] != mm0->src[0]->ne[0]) continue;
+        if (c->src[0]->ne[0] != mm0->src[0]->ne[0]) continue;
+        if (c->src[0]->type != mm0->src[0]->type) {
+            // a second K-quant type (V beside Q/K) joins as the launch's second body, one type
+            // besides mm0's at most, and not under an activation prologue (16-wave workgroups)
+            bool ok = gemv_mixed_ok(mm0, c) && !(ctx.pend.kind && ctx.pend.consumer == mm0);
+            for (int m = 1; m < nm; ++m) {
+                const ggml_type tm = mms[m]->src[0]->type;
+                ok = ok && (tm == mm0->src[0]->type || tm == c->src[0]->type);
+            }
+            if (!ok) continue;
+        }
         const ggml_tensor * o[1] = {c};
         if (overlaps_any(c, outs) || !can_hoist(g, i, j, o, 1, absorbed)) {
             static const bool dbg = getenv("GGML_MI355X_DEBUG_FUSE") != nullptr;

@@ -585,8 +585,10 @@ __global__ __launch_bounds__(256) void k_gemv(const gemv_args p) {
 // MODE: 0 = plain stores (no prologue, no epilogue), 1 = epilogues, 2 = activation prologue +
 // epilogues.  The lean modes keep the register footprint (and so the number of resident
 // workgroups) of the plain mat-vec: 90 VGPRs at R = 2 against 134 with the prologue compiled in.
+// The body runs as workgroup wg0 of nwg over the launch's ngroups row groups, so one launch can
+// hold two bodies of different weight types (k_gemv_pipe2).
 template <class T, int R, int WPR, int MODE, int NWV, bool ID = false>
-__global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const int64_t ngroups) {
+__device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_t ngroups, const int64_t wg0, const int64_t nwg) {
     constexpr int NT = 64 * NWV;
     constexpr int RPG = (NWV / WPR) * R;   // rows per group
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -625,7 +627,7 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const
     // the first group's weight loads leave before anything else, so the activation prologue,
     // the rope table and the activation loads below overlap that HBM latency
     typename T::raw cur[R], nxt[R];
-    int64_t g = blockIdx.x;
+    int64_t g = wg0;
     if (g < ngroups) fetch(g, cur);
     // cos/sin of every rope pair at this token's position, one pair per thread (rope_cs, the
     // same arithmetic the stand-alone ROPE kernel uses), instead of per output row in the
@@ -660,7 +662,7 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const
         const gemv_act A = prologue_wg<NWV>(p, pro_lds);
         T::load(A, tt, x);
     }
-    if (MODE && p.post_add && blockIdx.x == 0) {
+    if (MODE && p.post_add && wg0 == 0) {
         for (int64_t i = threadIdx.x; i < p.post_n; i += NT) p.post_add[i] = __fadd_rn(p.post_add[i], p.post_b[i]);
     }
     __shared__ float red[2][NWV][R];
@@ -668,8 +670,8 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const
     // threads (not on the R lanes holding the sums, with the next group's loads live)
     __shared__ float res[MODE ? GEMV_MAXG * RPG : 1];
     int par = 0, kg = 0;
-    for (; g < ngroups; g += gridDim.x, par ^= 1, ++kg) {
-        const int64_t gn = g + gridDim.x;
+    for (; g < ngroups; g += nwg, par ^= 1, ++kg) {
+        const int64_t gn = g + nwg;
         if (gn < ngroups) fetch(gn, nxt);
         float acc[R];
 #pragma unroll
@@ -711,7 +713,7 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const
     if constexpr (MODE >= 1) {
         __syncthreads();
         for (int i = threadIdx.x; i < kg * RPG; i += NT) {
-            const int64_t gg = blockIdx.x + (int64_t) (i / RPG) * gridDim.x;
+            const int64_t gg = wg0 + (int64_t) (i / RPG) * nwg;
             int mi = 0;
 #pragma unroll
             for (int k = 1; k < GEMV_MAXMAT; ++k) mi += gg >= p.blk0[k] ? 1 : 0;
@@ -720,6 +722,22 @@ __global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const
             if (row < p.M[mi]) gemv_store(p, mi, p.M[mi], row, res[i], res[RPG > 1 ? i ^ 1 : i], rtab, f16p);
         }
     }
+}
+
+template <class T, int R, int WPR, int MODE, int NWV, bool ID = false>
+__global__ __launch_bounds__(64 * NWV) void k_gemv_pipe(const gemv_args p, const int64_t ngroups) {
+    gemv_pipe_body<T, R, WPR, MODE, NWV, ID>(p, ngroups, blockIdx.x, gridDim.x);
+}
+
+// Q/K of one K-quant and V of another (Llama-3 Q4_K_M: Q4_K and Q6_K on 16 of 32 layers) in
+// one launch with epilogues: workgroups [0, nwg1) run p1's matrices, the rest p2's.  Each
+// row's arithmetic is its type's own (WPR depends on K only), so the bits are those of two
+// separate launches.
+template <class T1, class T2, int R2, int WPR>
+__global__ __launch_bounds__(256) void k_gemv_pipe2(const gemv_args p1, const int64_t ng1, const int64_t nwg1,
+                                                    const gemv_args p2, const int64_t ng2) {
+    if ((int64_t) blockIdx.x < nwg1) gemv_pipe_body<T1, 2, WPR, 1, 4>(p1, ng1, blockIdx.x, nwg1);
+    else gemv_pipe_body<T2, R2, WPR, 1, 4>(p2, ng2, (int64_t) blockIdx.x - nwg1, (int64_t) gridDim.x - nwg1);
 }
 
 // cos/sin of every rope pair at the token's position (one token), once per graph: rope_cs,
@@ -886,6 +904,67 @@ static bool launch_pipe_t(hipStream_t st, gemv_args & a, int nmat, int64_t Mt) {
     return true;
 }
 
+// two weight types in one launch (k_gemv_pipe2): p1's matrices at two rows per wave, p2's at
+// R2 by the single-type rule; false when the shapes fall outside the compiled variants
+template <class T1, class T2, int R2, int WPR>
+static void launch_pipe2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2, int n2) {
+    constexpr int NWV = 4;
+    auto blocks = [](gemv_args & a, int nmat, int rpg) {
+        a.blk0[0] = 0;
+        for (int i = 0; i < GEMV_MAXMAT; ++i) a.blk0[i + 1] = a.blk0[i] + (i < nmat ? ceil_div(a.M[i], rpg) : 0);
+        for (int i = nmat; i < GEMV_MAXMAT; ++i) a.blk0[i] = a.blk0[nmat];
+        return a.blk0[nmat];
+    };
+    const int64_t ng1 = blocks(a1, n1, (NWV / WPR) * 2), ng2 = blocks(a2, n2, (NWV / WPR) * R2);
+    auto grid_of = [](int64_t ng) {
+        return std::max<int64_t>(std::min<int64_t>(ng, g_gemv_wgs), ceil_div(ng, GEMV_MAXG));   // LDS-parked row sums
+    };
+    const int64_t w1 = grid_of(ng1), w2 = grid_of(ng2);
+    if (t_ev_beg) {
+        hipExtLaunchKernelGGL((k_gemv_pipe2<T1, T2, R2, WPR>), dim3((unsigned) (w1 + w2)), dim3(64 * NWV), 0, st, t_ev_beg, t_ev_end,
+                              0, a1, ng1, w1, a2, ng2);
+    } else {
+        hipLaunchKernelGGL((k_gemv_pipe2<T1, T2, R2, WPR>), dim3((unsigned) (w1 + w2)), dim3(64 * NWV), 0, st, a1, ng1, w1, a2, ng2);
+    }
+}
+
+template <class T1, class T2>
+static bool launch_pipe2_t(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2, int n2) {
+    if (g_gemv_pipe < 0) g_gemv_pipe = getenv("GGML_MI355X_GEMV_PIPE") ? atoi(getenv("GGML_MI355X_GEMV_PIPE")) : 1;
+    if (g_gemv_wgs < 0) g_gemv_wgs = getenv("GGML_MI355X_GEMV_WGS") ? atoi(getenv("GGML_MI355X_GEMV_WGS")) : 2048;
+    if (!g_gemv_pipe || a1.ntasks != a2.ntasks || a1.ntasks > 2 * WAVE) return false;
+    if ((a1.need_pairs || a2.need_pairs) && a1.rp.n_dims > 2 * GEMV_ROPE_MAXPAIRS) return false;
+    const int wpr = a1.ntasks <= WAVE ? 1 : 2;
+    int64_t m1 = 0, m2 = 0;
+    for (int i = 0; i < n1; ++i) m1 += a1.M[i];
+    for (int i = 0; i < n2; ++i) m2 += a2.M[i];
+    // the single-type launch's rows-per-wave rule (launch_pipe_t), per part
+    if (ceil_div(m1 * wpr, 8) < 256) return false;
+    const int r2 = ceil_div(m2 * wpr, 8) < 256 ? 1 : 2;
+    switch (r2 * 8 + wpr) {
+        case 1 * 8 + 1: launch_pipe2_v<T1, T2, 1, 1>(st, a1, n1, a2, n2); break;
+        case 1 * 8 + 2: launch_pipe2_v<T1, T2, 1, 2>(st, a1, n1, a2, n2); break;
+        case 2 * 8 + 1: launch_pipe2_v<T1, T2, 2, 1>(st, a1, n1, a2, n2); break;
+        default:        launch_pipe2_v<T1, T2, 2, 2>(st, a1, n1, a2, n2); break;
+    }
+    return true;
+}
+
+// Q/K/V of two K-quant types (gemv_group); false: launch the parts separately
+static bool launch_mixed(hipStream_t st, ggml_type t1, gemv_args & a1, int n1, ggml_type t2, gemv_args & a2, int n2) {
+    if (t1 == GGML_TYPE_Q4_K && t2 == GGML_TYPE_Q6_K) return launch_pipe2_t<g_q4_K, g_q6_K>(st, a1, n1, a2, n2);
+    if (t1 == GGML_TYPE_Q4_K && t2 == GGML_TYPE_Q5_K) return launch_pipe2_t<g_q4_K, g_q5_K>(st, a1, n1, a2, n2);
+    if (t1 == GGML_TYPE_Q5_K && t2 == GGML_TYPE_Q6_K) return launch_pipe2_t<g_q5_K, g_q6_K>(st, a1, n1, a2, n2);
+    return false;
+}
+
+bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c) {
+    static const int on = getenv("GGML_MI355X_GEMV_MIXED") ? atoi(getenv("GGML_MI355X_GEMV_MIXED")) : 1;
+    const ggml_type t1 = mm0->src[0]->type, t2 = c->src[0]->type;
+    return on && ((t1 == GGML_TYPE_Q4_K && (t2 == GGML_TYPE_Q6_K || t2 == GGML_TYPE_Q5_K)) ||
+                  (t1 == GGML_TYPE_Q5_K && t2 == GGML_TYPE_Q6_K));
+}
+
 template <class T>
 static void launch_t(hipStream_t st, gemv_args & a, int nmat) {
     int64_t Mt = 0;
@@ -1021,7 +1100,48 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         t_ev_beg = ctx.get_event();
         t_ev_end = ctx.get_event();
     }
-    switch (wt) {
+    // matrices of a second K-quant type (V beside Q/K, gemv_mixed_ok): one two-body launch
+    int ia[GEMV_MAXMAT], ib[GEMV_MAXMAT], n1 = 0, n2 = 0;
+    ggml_type wt2 = wt;
+    for (int i = 0; i < nmat; ++i) {
+        const ggml_type ti = mms[i]->src[0]->type;
+        if (ti == wt) ia[n1++] = i;
+        else { GGML_ASSERT((wt2 == wt || wt2 == ti) && is_kq(ti) && kq && !pro); wt2 = ti; ib[n2++] = i; }
+    }
+    if (n2) {
+        auto part = [&](gemv_args & d, const int * idx, int cnt) {
+            d.need_pairs = 0;
+            for (int k = 0; k < GEMV_MAXMAT; ++k) {
+                const int s = idx[k < cnt ? k : 0];
+                d.W[k] = a.W[s]; d.nb01[k] = a.nb01[s]; d.M[k] = a.M[s];
+                d.dst[k] = a.dst[s]; d.silu[k] = a.silu[s]; d.f16out[k] = a.f16out[s];
+                d.rope_out[k] = a.rope_out[s]; d.rope_f16[k] = a.rope_f16[s];
+                if (k < cnt && epi && epi->rope[s]) d.need_pairs = 1;
+            }
+            d.ntasks = (int) (nblk * 4);
+        };
+        gemv_args a1 = a, a2 = a;
+        part(a1, ia, n1);
+        part(a2, ib, n2);
+        a2.post_add = nullptr;   // stored by workgroup 0 of the first body
+        if (!launch_mixed(ctx.stream, wt, a1, n1, wt2, a2, n2)) {
+            auto one = [&](ggml_type t, gemv_args & d, int cnt) {
+                switch (t) {
+                    case GGML_TYPE_Q4_K: launch_t<g_q4_K>(ctx.stream, d, cnt); break;
+                    case GGML_TYPE_Q5_K: launch_t<g_q5_K>(ctx.stream, d, cnt); break;
+                    default:             launch_t<g_q6_K>(ctx.stream, d, cnt); break;
+                }
+            };
+            one(wt, a1, n1);
+            if (ctx.timing) {   // the second launch is timed as its own mat-vec
+                ctx.pending.push_back({t_ev_beg, t_ev_end, bytes, TK_MMV});
+                t_ev_beg = ctx.get_event();
+                t_ev_end = ctx.get_event();
+                bytes = 0;
+            }
+            one(wt2, a2, n2);
+        }
+    } else switch (wt) {
         case GGML_TYPE_Q4_K: a.ntasks = (int) (nblk * 4); launch_t<g_q4_K>(ctx.stream, a, nmat); break;
         case GGML_TYPE_Q5_K: a.ntasks = (int) (nblk * 4); launch_t<g_q5_K>(ctx.stream, a, nmat); break;
         case GGML_TYPE_Q6_K: a.ntasks = (int) (nblk * 4); launch_t<g_q6_K>(ctx.stream, a, nmat); break;

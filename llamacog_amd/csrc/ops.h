@@ -192,6 +192,7 @@ bool gemv_supported(const ggml_tensor * mm);
 bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
 bool gemv_prologue_ok(const ggml_tensor * mm);   // the consumer can run an activation prologue
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi);
+bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c);   // c may join mm0's launch as a second weight type
 
 // lays out a q8_act (qs | d | s, 256-B aligned) in `base`
 void carve_act(q8_act & act, void * base, int64_t K, int64_t ncols, bool k_quant);
