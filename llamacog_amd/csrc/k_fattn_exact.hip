@@ -140,12 +140,21 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
 
     // q of this head, f16-rounded, in the quad layout of dot_f16_avx512_q4
     float qf[NM][4];
+    const char * mrow = a.mask ? a.mask + (iq1 % a.mask_ne1) * a.nbm1 : nullptr;
+    // the first chunk's mask value of this thread is loaded together with q, so the two
+    // memory latencies overlap instead of following each other
+    uint16_t mk0 = 0;
+    float4 q4[NM];
     {
         const float * qrow = (const float *) (a.q + iq1 * a.nbq1 + h * a.nbq2 + iq3 * a.nbq3);
 #pragma unroll
+        for (int m = 0; m < NM; ++m) q4[m] = *(const float4 *) (qrow + 16 * m + 4 * qd);
+        if (mrow && tid < min((int64_t) CH, a.n_kv)) mk0 = *(const uint16_t *) (mrow + 2 * tid);
+    }
+    {
+#pragma unroll
         for (int m = 0; m < NM; ++m) {
-            const float4 q4 = *(const float4 *) (qrow + 16 * m + 4 * qd);
-            qf[m][0] = f16r(q4.x); qf[m][1] = f16r(q4.y); qf[m][2] = f16r(q4.z); qf[m][3] = f16r(q4.w);
+            qf[m][0] = f16r(q4[m].x); qf[m][1] = f16r(q4[m].y); qf[m][2] = f16r(q4[m].z); qf[m][3] = f16r(q4[m].w);
         }
     }
     const float slope = a.max_bias > 0.0f
@@ -161,7 +170,6 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
 
     const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
     const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
-    const char * mrow = a.mask ? a.mask + (iq1 % a.mask_ne1) * a.nbm1 : nullptr;
 
     const bool prof = a.prof && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0;
     unsigned long long tp = prof ? __builtin_amdgcn_s_memtime() : 0, pc[6] = {0, 0, 0, 0, 0, 0};
@@ -176,7 +184,7 @@ __global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
         for (int j0 = 0; j0 < CH + U; j0 += 256) {
             const int j = j0 + tid;
             float mv = -INFINITY;
-            if (j < nch) mv = mrow ? h2f(*(const uint16_t *) (mrow + 2 * (c0 + j))) : 0.0f;
+            if (j < nch) mv = mrow ? h2f(c0 == 0 && j0 == 0 ? mk0 : *(const uint16_t *) (mrow + 2 * (c0 + j))) : 0.0f;
             if (j < CH + U) mk[j] = mv;
             const unsigned long long b = __ballot(mv != -INFINITY);
             if (b) last = j0 + 64 * wave + 63 - __clzll(b);
