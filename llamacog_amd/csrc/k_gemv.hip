@@ -832,6 +832,13 @@ static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
         g_num_cu = prop.multiProcessorCount;
     }
     int64_t grid = std::min<int64_t>(ng, MODE == 2 ? g_num_cu : g_gemv_wgs);
+    if constexpr (WPR == 4 && !std::is_same<T, g_q6_K>::value) {
+        // four waves per row (K = 14336, the FFN down projection): one resident round of
+        // workgroups (5 per CU at <= 96 VGPRs) beats 2048 single-group workgroups in two
+        // rounds (Q4_K 4096 x 14336: 12.0 -> 11.2 us, scripts/probe_geom.py)
+        static const int wgs4 = getenv("GGML_MI355X_GEMV_WGS4") ? atoi(getenv("GGML_MI355X_GEMV_WGS4")) : 5 * g_num_cu;
+        if (MODE != 2 && wgs4 > 0) grid = std::min<int64_t>(ng, wgs4);
+    }
     if (g_gemv_bal && MODE != 2) {
         // balanced resident grid: every workgroup resident at once and the same number of
         // groups (+-1 only when ng does not divide) per workgroup, so no second round of
@@ -886,6 +893,8 @@ static bool launch_pipe_t(hipStream_t st, gemv_args & a, int nmat, int64_t Mt) {
     // a matrix too short to give 256 workgroups at two rows per wave takes one
     int R = 2;
     if (std::is_same<T, g_q6_K>::value && wpr == 4) R = 4;
+    static const int r_wpr4 = getenv("GGML_MI355X_GEMV_R4W") ? atoi(getenv("GGML_MI355X_GEMV_R4W")) : 0;   // lab knob
+    if (wpr == 4 && (r_wpr4 == 1 || r_wpr4 == 2 || r_wpr4 == 4)) R = r_wpr4;
     // a matrix too short to give 256 workgroups at two rows per wave takes one (the rope
     // epilogue reads its partner row from the LDS-parked sums of the same group)
     if (ceil_div(Mt * wpr, a.pro ? 32 : 8) < 256) R = 1;

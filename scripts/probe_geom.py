@@ -1,0 +1,22 @@
+"""Decode GEMV geometry on the Llama-3-8B FFN shapes (cold weights, mi355x_bench_gemv2 kind 0):
+run once per GEMV knob setting (GGML_MI355X_GEMV_WGS / _BAL / _R4W in the environment)."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import llamacog_amd as la
+
+BB = {12: 144, 13: 176, 14: 210}
+lib = la.plugin_lib()
+g = lib.mi355x_bench_gemv2
+g.restype = ctypes.c_double
+g.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+tag = " ".join(f"{k[13:]}={v}" for k, v in os.environ.items() if k.startswith("GGML_MI355X_GEMV")) or "default"
+out = []
+for t, K, M, nm in [(12, 14336, 4096, 1), (14, 14336, 4096, 1), (12, 4096, 14336, 2), (12, 4096, 4096, 1)]:
+    mb = K // 256 * BB[t] * M * nm
+    cp = max(2, -(-(1 << 30) // mb))
+    a = g(t, K, M, nm, cp, 40, 0)
+    out.append(f"t{t} {K}x{M}x{nm} {a:6.2f}us {mb / a / 1e6:4.2f}TB/s")
+print(f"[{tag}] " + " | ".join(out), flush=True)
