@@ -245,6 +245,224 @@ __global__ __launch_bounds__(256) void k_mmq(const mmq_args p) {
     }
 }
 
+// ---- double-buffered variant ------------------------------------------------------------------
+// The same tile, arithmetic and stores as k_mmq; the loads of K block b+1 are in flight while
+// block b computes: the Q8_K token rows, their scales d and bsums go HBM -> LDS by
+// global_load_lds into the other of two stages, the weight blocks go to registers and are
+// written to that stage after the MFMA work.  One s_waitcnt + barrier per block then finds
+// the next stage landed instead of waiting a full memory latency for it.
+template <class W> struct mq_stage {
+    static constexpr int RS = (W::BLK + 15) / 16 * 16;
+    static constexpr int XQ = MQ_BM * RS;            // token rows [64][256] after the weight tile
+    static constexpr int XD = XQ + MQ_BN * 256;      // token scales [64] f32
+    static constexpr int XS = XD + MQ_BN * 4;        // token bsums [64][16] i16
+    static constexpr int BYTES = XS + MQ_BN * 32;
+    static constexpr int RC = RS / 16;               // 16-byte chunks per weight row
+    static constexpr int NWR = (MQ_BM * RC + 255) / 256;   // weight chunks per thread
+};
+
+// two workgroups per CU (two stages of 56-66 KB LDS each): at most 256 VGPRs + AGPRs per lane
+#ifndef MQ_DB_OCC
+#define MQ_DB_OCC 2
+#endif
+#ifndef MQ_DB_UNROLL
+#define MQ_DB_UNROLL 2
+#endif
+template <class W>
+__global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
+    using S = mq_stage<W>;
+    constexpr int RS = S::RS;
+    __shared__ __attribute__((aligned(16))) uint8_t st[2][S::BYTES];
+    __shared__ int wsc[MQ_BM][W::NSC];
+    __shared__ int wmn[MQ_BM][8];
+    __shared__ float wd[MQ_BM], wdm[MQ_BM];
+    __shared__ int xs[MQ_BN][8];   // Q8_K sums per 32-element chunk
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t row0 = (int64_t) blockIdx.x * MQ_BM;
+    const int64_t tok0 = (int64_t) blockIdx.y * MQ_BN;
+    const int h = lane >> 4, c16 = lane & 15;
+    const uint8_t * Wb = p.W;
+    int64_t T = p.T, col0 = 0;
+    if (p.cnt) {
+        T = p.cnt[blockIdx.z];
+        if (tok0 >= T) return;   // uniform: no barrier passed yet
+        col0 = p.off[blockIdx.z];
+        Wb = p.W + (int64_t) blockIdx.z * p.nb02;
+    }
+    const int64_t KB = p.K / 256;
+
+    // token-side loads of block b into stage s (LDS-DMA: 1 KiB, or 256 B, per wave instruction)
+    auto issue_x = [&](int64_t b, int s) {
+        uint8_t * base = st[s];
+#pragma unroll
+        for (int i = wave; i < MQ_BN * 256 / 1024; i += 4) {   // token rows: 16 instructions
+            const int c = 64 * i + lane, t = c >> 4, part = c & 15;
+            const int64_t tok = col0 + min(tok0 + t, T - 1);
+            __builtin_amdgcn_global_load_lds((const void *) (p.xq + tok * p.K + b * 256 + 16 * part),
+                                             (lds_ptr_t) (base + S::XQ + 1024 * i), 16, 0, 0);
+        }
+        if (wave == 0) {   // scales: one 4-byte load per token
+            const int64_t tok = col0 + min(tok0 + lane, T - 1);
+            __builtin_amdgcn_global_load_lds((const void *) (p.xd + tok * KB + b), (lds_ptr_t) (base + S::XD), 4, 0, 0);
+        } else if (wave <= 2) {   // bsums: 32 B per token, two instructions
+            const int i = wave - 1;
+            const int c = 64 * i + lane, t = c >> 1, half = c & 1;
+            const int64_t tok = col0 + min(tok0 + t, T - 1);
+            __builtin_amdgcn_global_load_lds((const void *) (p.xs + tok * (p.K / 16) + b * 16 + 8 * half),
+                                             (lds_ptr_t) (base + S::XS + 1024 * i), 16, 0, 0);
+        }
+    };
+    uint4 wr[S::NWR];
+    auto load_w = [&](int64_t b) {
+#pragma unroll
+        for (int j = 0; j < S::NWR; ++j) {
+            const int c = tid + 256 * j;
+            if (c < MQ_BM * S::RC) {
+                const int r = c / S::RC, k = c % S::RC;
+                const int64_t row = min(row0 + r, p.M - 1);
+                wr[j] = ld16(Wb + row * p.nb01 + b * W::BLK + 16 * k);
+            }
+        }
+    };
+    auto store_w = [&](int s) {
+#pragma unroll
+        for (int j = 0; j < S::NWR; ++j) {
+            const int c = tid + 256 * j;
+            if (c < MQ_BM * S::RC) *(uint4 *) (st[s] + c * 16) = wr[j];   // row r, chunk k at r * RS + 16 k = 16 c
+        }
+    };
+
+    float acc[4][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[n][i] = 0.0f;
+
+    issue_x(0, 0);
+    load_w(0);
+    store_w(0);
+    for (int64_t b = 0; b < p.nblk; ++b) {
+        const int s = (int) (b & 1);
+        const uint8_t * wq = st[s];
+        const int8_t * xq = (const int8_t *) (st[s] + S::XQ);
+        const float * xd = (const float *) (st[s] + S::XD);
+        // stage s has landed for every wave, and block b-1's reads of stage s^1 are done
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const bool more = b + 1 < p.nblk;
+        if (more) {
+            issue_x(b + 1, s ^ 1);
+            load_w(b + 1);
+        }
+        // ---- per-row scales and per-token chunk sums of block b ----------------------------
+        if (tid < MQ_BM) {
+            int sc[16], mn[8];
+            float d, dmin;
+            W::unpack(wq + tid * RS, sc, mn, d, dmin);
+#pragma unroll
+            for (int j = 0; j < W::NSC; ++j) wsc[tid][j] = sc[j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wmn[tid][j] = mn[j];
+            wd[tid] = d; wdm[tid] = dmin;
+        } else if (tid < MQ_BM + MQ_BN) {
+            const int t = tid - MQ_BM;
+            const int16_t * s16 = (const int16_t *) (st[s] + S::XS) + 16 * t;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xs[t][j] = s16[2 * j] + s16[2 * j + 1];
+        }
+        __syncthreads();
+        // ---- MFMA over the 8 chunks of 32 (k_mmq's arithmetic) -----------------------------
+        const int rA = 16 * wave + c16;
+        int sumi[4][4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sumi[n][i] = 0;
+#pragma unroll MQ_DB_UNROLL
+        for (int c = 0; c < 8; ++c) {
+            const long a = W::afrag(wq + rA * RS, c, h);
+            if constexpr (W::NSC == 8) {
+                int scv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) scv[i] = wsc[16 * wave + 4 * h + i][c];
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 32 * c + 8 * h);
+                    v4i r = {0, 0, 0, 0};
+                    r = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, bf, r, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sumi[n][i] += r[i] * scv[i];
+                }
+            } else {
+                const long a0 = h < 2 ? a : 0, a1 = h < 2 ? 0 : a;
+                int sc0[4], sc1[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    sc0[i] = wsc[16 * wave + 4 * h + i][2 * c];
+                    sc1[i] = wsc[16 * wave + 4 * h + i][2 * c + 1];
+                }
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 32 * c + 8 * h);
+                    v4i r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
+                    r0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, bf, r0, 0, 0, 0);
+                    r1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, bf, r1, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) sumi[n][i] += r0[i] * sc0[i] + r1[i] * sc1[i];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = 16 * wave + 4 * h + i;
+            const float dw = wd[r], dmw = wdm[r];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int t = 16 * n + c16;
+                const float dy = xd[t];
+                if constexpr (W::NSC == 8) {
+                    int summ = 0;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) summ += wmn[r][j] * xs[t][j];
+                    acc[n][i] += (dw * dy) * (float) sumi[n][i] - (dmw * dy) * (float) summ;
+                } else {
+                    acc[n][i] += (dw * dy) * (float) sumi[n][i];
+                }
+            }
+        }
+        // block b+1's weights into the other stage (its readers, block b-1, passed the barrier)
+        if (more) store_w(s ^ 1);
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int64_t t = tok0 + 16 * n + c16;
+        if (t >= T) continue;
+        char * drow = (char *) p.dst + t * p.nb1;
+        if (p.cnt) {
+            const int pair = p.list[col0 + t];
+            drow = (char *) p.dst + (pair % p.n_used) * p.nb1 + (pair / p.n_used) * p.nb2;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t m = row0 + 16 * wave + 4 * h + i;
+            if (m < p.M) *(float *) (drow + m * 4) = acc[n][i];
+        }
+    }
+}
+
+// GGML_MI355X_MMQ_DB=0 selects the single-buffered k_mmq
+static bool mmq_db_on() {
+    static const int on = getenv("GGML_MI355X_MMQ_DB") ? atoi(getenv("GGML_MI355X_MMQ_DB")) : 1;
+    return on != 0;
+}
+
+template <class W>
+static void launch_mmq(hipStream_t st, const dim3 & grid, const mmq_args & p) {
+    if (mmq_db_on()) hipLaunchKernelGGL(k_mmq_db<W>, grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(k_mmq<W>, grid, dim3(256), 0, st, p);
+}
+
 // ---- host --------------------------------------------------------------------------------------
 bool mmq_supported(const ggml_tensor * dst) {
     static const bool off = getenv("GGML_MI355X_NO_MMQ") && atoi(getenv("GGML_MI355X_NO_MMQ")) != 0;
@@ -278,9 +496,9 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
     p.cnt = p.off = p.list = nullptr; p.n_used = 1; p.nb02 = 0; p.nb2 = 0;
     const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(p.T, MQ_BN));
     switch (w->type) {
-        case GGML_TYPE_Q4_K: hipLaunchKernelGGL(k_mmq<mq_q4_K>, grid, dim3(256), 0, ctx.stream, p); break;
-        case GGML_TYPE_Q5_K: hipLaunchKernelGGL(k_mmq<mq_q5_K>, grid, dim3(256), 0, ctx.stream, p); break;
-        case GGML_TYPE_Q6_K: hipLaunchKernelGGL(k_mmq<mq_q6_K>, grid, dim3(256), 0, ctx.stream, p); break;
+        case GGML_TYPE_Q4_K: launch_mmq<mq_q4_K>(ctx.stream, grid, p); break;
+        case GGML_TYPE_Q5_K: launch_mmq<mq_q5_K>(ctx.stream, grid, p); break;
+        case GGML_TYPE_Q6_K: launch_mmq<mq_q6_K>(ctx.stream, grid, p); break;
         default: GGML_ABORT("mi355x: mmq type");
     }
     if (ctx.timing) ctx.time_end(TK_MMQ, flops, ev);
@@ -307,9 +525,9 @@ void mul_mat_q_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, const i
     p.cnt = cnt; p.off = off; p.list = list; p.n_used = ids->ne[0]; p.nb02 = w->nb[2]; p.nb2 = dst->nb[2];
     const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(n_pairs, MQ_BN), (unsigned) w->ne[2]);
     switch (w->type) {
-        case GGML_TYPE_Q4_K: hipLaunchKernelGGL(k_mmq<mq_q4_K>, grid, dim3(256), 0, ctx.stream, p); break;
-        case GGML_TYPE_Q5_K: hipLaunchKernelGGL(k_mmq<mq_q5_K>, grid, dim3(256), 0, ctx.stream, p); break;
-        case GGML_TYPE_Q6_K: hipLaunchKernelGGL(k_mmq<mq_q6_K>, grid, dim3(256), 0, ctx.stream, p); break;
+        case GGML_TYPE_Q4_K: launch_mmq<mq_q4_K>(ctx.stream, grid, p); break;
+        case GGML_TYPE_Q5_K: launch_mmq<mq_q5_K>(ctx.stream, grid, p); break;
+        case GGML_TYPE_Q6_K: launch_mmq<mq_q6_K>(ctx.stream, grid, p); break;
         default: GGML_ABORT("mi355x: mmq id type");
     }
 }
