@@ -246,6 +246,9 @@ __global__ __launch_bounds__(256) void k_mmq(const mmq_args p) {
 }
 
 // ---- double-buffered variant ------------------------------------------------------------------
+// (24-bit multiplies, full rate, for the sub-block scaling: |MFMA result| <= 32*15*127 (Q4_K),
+// 32*31*127 (Q5_K), 16*32*128 (Q6_K) < 2^23, scales and mins < 2^7, Q8_K chunk sums < 2^13,
+// so every product is exact)
 // The same tile, arithmetic and stores as k_mmq; the loads of K block b+1 are in flight while
 // block b computes: the Q8_K token rows, their scales d and bsums go HBM -> LDS by
 // global_load_lds into the other of two stages, the weight blocks go to registers and are
@@ -292,37 +295,44 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
     }
     const int64_t KB = p.K / 256;
 
+    // per-thread source pointers of block 0 (block b adds b * 256 / b / b * 16 / b * BLK)
+    const int8_t * xsrc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // token rows: instruction i = wave + 4k of 16
+        const int c = 64 * (wave + 4 * k) + lane, t = c >> 4, part = c & 15;
+        xsrc[k] = p.xq + (col0 + min(tok0 + t, T - 1)) * p.K + 16 * part;
+    }
+    const float * dsrc = p.xd + (col0 + min(tok0 + lane, T - 1)) * KB;
+    const int16_t * ssrc;
+    {
+        const int c = 64 * (wave == 2 ? 1 : 0) + lane, t = c >> 1, half = c & 1;
+        ssrc = p.xs + (col0 + min(tok0 + t, T - 1)) * (p.K / 16) + 8 * half;
+    }
+    const uint8_t * wsrc[S::NWR];
+#pragma unroll
+    for (int j = 0; j < S::NWR; ++j) {
+        const int c = min(tid + 256 * j, MQ_BM * S::RC - 1);
+        const int r = c / S::RC, k = c % S::RC;
+        wsrc[j] = Wb + min(row0 + r, p.M - 1) * p.nb01 + 16 * k;
+    }
     // token-side loads of block b into stage s (LDS-DMA: 1 KiB, or 256 B, per wave instruction)
     auto issue_x = [&](int64_t b, int s) {
         uint8_t * base = st[s];
 #pragma unroll
-        for (int i = wave; i < MQ_BN * 256 / 1024; i += 4) {   // token rows: 16 instructions
-            const int c = 64 * i + lane, t = c >> 4, part = c & 15;
-            const int64_t tok = col0 + min(tok0 + t, T - 1);
-            __builtin_amdgcn_global_load_lds((const void *) (p.xq + tok * p.K + b * 256 + 16 * part),
-                                             (lds_ptr_t) (base + S::XQ + 1024 * i), 16, 0, 0);
+        for (int k = 0; k < 4; ++k) {
+            __builtin_amdgcn_global_load_lds((const void *) (xsrc[k] + b * 256), (lds_ptr_t) (base + S::XQ + 1024 * (wave + 4 * k)), 16, 0, 0);
         }
         if (wave == 0) {   // scales: one 4-byte load per token
-            const int64_t tok = col0 + min(tok0 + lane, T - 1);
-            __builtin_amdgcn_global_load_lds((const void *) (p.xd + tok * KB + b), (lds_ptr_t) (base + S::XD), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (dsrc + b), (lds_ptr_t) (base + S::XD), 4, 0, 0);
         } else if (wave <= 2) {   // bsums: 32 B per token, two instructions
-            const int i = wave - 1;
-            const int c = 64 * i + lane, t = c >> 1, half = c & 1;
-            const int64_t tok = col0 + min(tok0 + t, T - 1);
-            __builtin_amdgcn_global_load_lds((const void *) (p.xs + tok * (p.K / 16) + b * 16 + 8 * half),
-                                             (lds_ptr_t) (base + S::XS + 1024 * i), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (ssrc + b * 16), (lds_ptr_t) (base + S::XS + 1024 * (wave - 1)), 16, 0, 0);
         }
     };
     uint4 wr[S::NWR];
     auto load_w = [&](int64_t b) {
 #pragma unroll
         for (int j = 0; j < S::NWR; ++j) {
-            const int c = tid + 256 * j;
-            if (c < MQ_BM * S::RC) {
-                const int r = c / S::RC, k = c % S::RC;
-                const int64_t row = min(row0 + r, p.M - 1);
-                wr[j] = ld16(Wb + row * p.nb01 + b * W::BLK + 16 * k);
-            }
+            if (tid + 256 * j < MQ_BM * S::RC) wr[j] = ld16(wsrc[j] + b * W::BLK);
         }
     };
     auto store_w = [&](int s) {
@@ -392,7 +402,7 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
                     v4i r = {0, 0, 0, 0};
                     r = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, bf, r, 0, 0, 0);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) sumi[n][i] += r[i] * scv[i];
+                    for (int i = 0; i < 4; ++i) sumi[n][i] += __mul24(r[i], scv[i]);
                 }
             } else {
                 const long a0 = h < 2 ? a : 0, a1 = h < 2 ? 0 : a;
@@ -409,7 +419,7 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
                     r0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, bf, r0, 0, 0, 0);
                     r1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, bf, r1, 0, 0, 0);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) sumi[n][i] += r0[i] * sc0[i] + r1[i] * sc1[i];
+                    for (int i = 0; i < 4; ++i) sumi[n][i] += __mul24(r0[i], sc0[i]) + __mul24(r1[i], sc1[i]);
                 }
             }
         }
@@ -424,7 +434,7 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
                 if constexpr (W::NSC == 8) {
                     int summ = 0;
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) summ += wmn[r][j] * xs[t][j];
+                    for (int j = 0; j < 8; ++j) summ += __mul24(wmn[r][j], xs[t][j]);
                     acc[n][i] += (dw * dy) * (float) sumi[n][i] - (dmw * dy) * (float) summ;
                 } else {
                     acc[n][i] += (dw * dy) * (float) sumi[n][i];
