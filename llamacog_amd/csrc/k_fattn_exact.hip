@@ -115,8 +115,10 @@ template <int D> struct fax_cfg {
     static constexpr int U = 8;                       // phase-3 positions per batch
 };
 
-template <int D>
-__global__ __launch_bounds__(256) void k_fattn_exact(const fa_args a) {
+// OCC = workgroups per CU the register budget allows: 1 for decode (32-64 workgroups, every
+// register for ILP), 2 for prefill (thousands of workgroups; the LDS allows two)
+template <int D, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
     using C = fax_cfg<D>;
     constexpr int CH = C::CH, U = C::U, NM = D / 16;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -417,9 +419,14 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     const int64_t wy = a.warm.nwg ? ceil_div(a.warm.nwg, a.n_q) : 0;
     a.warm.nwg = (int) (wy * a.n_q);
     const dim3 grid((unsigned) a.n_q, (unsigned) (a.H * nq3 + wy));
+    static const int pocc = getenv("GGML_MI355X_FA_PREFILL_OCC") ? atoi(getenv("GGML_MI355X_FA_PREFILL_OCC")) : 2;
+    const bool wide = a.n_q * a.H * nq3 > 256 && pocc == 2;   // prefill: more workgroups than CUs
     switch (a.D) {
         case 64:  hipLaunchKernelGGL(k_fattn_exact<64>, grid, dim3(256), 0, st, a); break;
-        case 128: hipLaunchKernelGGL(k_fattn_exact<128>, grid, dim3(256), 0, st, a); break;
+        case 128:
+            if (wide) hipLaunchKernelGGL((k_fattn_exact<128, 2>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL(k_fattn_exact<128>, grid, dim3(256), 0, st, a);
+            break;
         case 256: hipLaunchKernelGGL(k_fattn_exact<256>, grid, dim3(256), 0, st, a); break;
         default: GGML_ABORT("mi355x: FA head size %d", (int) a.D);
     }
