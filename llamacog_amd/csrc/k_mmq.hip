@@ -254,6 +254,10 @@ __global__ __launch_bounds__(256) void k_mmq(const mmq_args p) {
 // global_load_lds into the other of two stages, the weight blocks go to registers and are
 // written to that stage after the MFMA work.  One s_waitcnt + barrier per block then finds
 // the next stage landed instead of waiting a full memory latency for it.
+// The token tile is XOR-swizzled in LDS: the 16-byte chunk k of token row t sits in slot
+// k ^ (t & 15), so the 16 lanes of an MFMA B fragment (rows t = 16n + c16, same chunk) read 16
+// different bank groups instead of one (rows are 256 B = one bank period apart).  The swizzle
+// is applied on the source side of the LDS-DMA (each lane picks which chunk it fetches).
 template <class W> struct mq_stage {
     static constexpr int RS = (W::BLK + 15) / 16 * 16;
     static constexpr int XQ = MQ_BM * RS;            // token rows [64][256] after the weight tile
@@ -299,7 +303,7 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
     const int8_t * xsrc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {   // token rows: instruction i = wave + 4k of 16
-        const int c = 64 * (wave + 4 * k) + lane, t = c >> 4, part = c & 15;
+        const int c = 64 * (wave + 4 * k) + lane, t = c >> 4, part = (c & 15) ^ (t & 15);   // LDS slot (t, c & 15) holds chunk (c & 15) ^ (t & 15)
         xsrc[k] = p.xq + (col0 + min(tok0 + t, T - 1)) * p.K + 16 * part;
     }
     const float * dsrc = p.xd + (col0 + min(tok0 + lane, T - 1)) * KB;
@@ -398,7 +402,7 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
                 for (int i = 0; i < 4; ++i) scv[i] = wsc[16 * wave + 4 * h + i][c];
 #pragma unroll
                 for (int n = 0; n < 4; ++n) {
-                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 32 * c + 8 * h);
+                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 16 * ((2 * c + (h >> 1)) ^ c16) + 8 * (h & 1));
                     v4i r = {0, 0, 0, 0};
                     r = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, bf, r, 0, 0, 0);
 #pragma unroll
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
                 }
 #pragma unroll
                 for (int n = 0; n < 4; ++n) {
-                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 32 * c + 8 * h);
+                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 16 * ((2 * c + (h >> 1)) ^ c16) + 8 * (h & 1));
                     v4i r0 = {0, 0, 0, 0}, r1 = {0, 0, 0, 0};
                     r0 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a0, bf, r0, 0, 0, 0);
                     r1 = __builtin_amdgcn_mfma_i32_16x16x32_i8(a1, bf, r1, 0, 0, 0);
@@ -461,15 +465,209 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
     }
 }
 
-// GGML_MI355X_MMQ_DB=0 selects the single-buffered k_mmq
-static bool mmq_db_on() {
-    static const int on = getenv("GGML_MI355X_MMQ_DB") ? atoi(getenv("GGML_MI355X_MMQ_DB")) : 1;
-    return on != 0;
+// ---- prefetch distance 2 (16-byte-aligned weight blocks: Q4_K) ----------------------------------
+// k_mmq_db waits about one memory latency per K block whenever a block's MFMA work is shorter
+// than that latency, and the compiler, which cannot tell LDS stages apart, also waits for every
+// LDS-DMA in flight before each LDS read.  Here every load is an LDS-DMA issued from inline asm
+// (invisible to the compiler's waitcnt pass), the token side of block b+2 and the weights of
+// block b+1 leave while block b computes (three token stages, two weight stages), and every wave
+// issues the same number of DMA instructions per block (clamped duplicates at the edges), so
+// "blocks b's stages landed" is one fixed s_waitcnt vmcnt.
+__device__ __forceinline__ void dma_lds16(const void * g, const void * lds) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (lds_ptr_t) lds);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(g), "s"(m) : "memory", "m0");
+}
+__device__ __forceinline__ void dma_lds4(const void * g, const void * lds) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (lds_ptr_t) lds);
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" :: "v"(g), "s"(m) : "memory", "m0");
+}
+
+template <class W> struct mq_pipe {
+    static_assert(W::BLK % 16 == 0, "weight blocks must be whole 16-byte chunks");
+    static constexpr int RC = W::BLK / 16;                      // 16-byte chunks per weight row
+    static constexpr int WQ = MQ_BM * W::BLK;                   // a weight stage
+    static constexpr int NWI = (MQ_BM * RC / 64 + 3) / 4;       // weight DMA instructions per wave
+    static constexpr int XD = MQ_BN * 256, XS = XD + MQ_BN * 4;
+    static constexpr int XB = XS + MQ_BN * 32;                  // a token stage: rows, d, bsums
+    static constexpr int NXI = 5;                               // token DMA instructions per wave
+};
+
+template <class W>
+__global__ __launch_bounds__(256, 2) void k_mmq_p2(const mmq_args p) {
+    using S = mq_pipe<W>;
+    constexpr int RS = W::BLK;
+    __shared__ __attribute__((aligned(16))) uint8_t xst[3][S::XB];
+    __shared__ __attribute__((aligned(16))) uint8_t wst[2][S::WQ];
+    __shared__ uint8_t wsc[MQ_BM][W::NSC];
+    __shared__ uint8_t wmn[MQ_BM][8];
+    __shared__ float wd[MQ_BM], wdm[MQ_BM];
+    __shared__ int xs[MQ_BN][8];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t row0 = (int64_t) blockIdx.x * MQ_BM;
+    const int64_t tok0 = (int64_t) blockIdx.y * MQ_BN;
+    const int h = lane >> 4, c16 = lane & 15;
+    const uint8_t * Wb = p.W;
+    int64_t T = p.T, col0 = 0;
+    if (p.cnt) {
+        T = p.cnt[blockIdx.z];
+        if (tok0 >= T) return;   // uniform: no barrier passed yet
+        col0 = p.off[blockIdx.z];
+        Wb = p.W + (int64_t) blockIdx.z * p.nb02;
+    }
+    const int64_t KB = p.K / 256;
+    const int64_t nblk = p.nblk;
+
+    const int8_t * xsrc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int c = 64 * (wave + 4 * k) + lane, t = c >> 4, part = (c & 15) ^ (t & 15);   // LDS slot (t, c & 15) holds chunk (c & 15) ^ (t & 15)
+        xsrc[k] = p.xq + (col0 + min(tok0 + t, T - 1)) * p.K + 16 * part;
+    }
+    // the fifth token instruction: the scales (wave 0, and the same bytes again by wave 3) or
+    // half of the bsums (waves 1, 2)
+    const uint8_t * esrc;
+    int eoff;
+    const bool e4 = wave == 0 || wave == 3;
+    if (e4) {
+        esrc = (const uint8_t *) (p.xd + (col0 + min(tok0 + lane, T - 1)) * KB);
+        eoff = S::XD;
+    } else {
+        const int c = 64 * (wave - 1) + lane, t = c >> 1, half = c & 1;
+        esrc = (const uint8_t *) (p.xs + (col0 + min(tok0 + t, T - 1)) * (p.K / 16) + 8 * half);
+        eoff = S::XS + 1024 * (wave - 1);
+    }
+    // weight instruction i = wave + 4j covers chunks 64i .. 64i+63 (row c / RC, chunk c % RC);
+    // indices past the tile repeat the last instruction (same bytes, same LDS)
+    const uint8_t * wsrc[S::NWI];
+    int woff[S::NWI];
+#pragma unroll
+    for (int j = 0; j < S::NWI; ++j) {
+        const int i = min(wave + 4 * j, MQ_BM * S::RC / 64 - 1);
+        const int c = 64 * i + lane, r = c / S::RC, k = c % S::RC;
+        wsrc[j] = Wb + min(row0 + r, p.M - 1) * p.nb01 + 16 * k;
+        woff[j] = 1024 * i;
+    }
+    auto issue_w = [&](int64_t b, int ws_i) {
+        b = min(b, nblk - 1);
+#pragma unroll
+        for (int j = 0; j < S::NWI; ++j) dma_lds16(wsrc[j] + b * W::BLK, wst[ws_i] + woff[j]);
+    };
+    auto issue_x = [&](int64_t b, int xs_i) {
+        b = min(b, nblk - 1);
+        uint8_t * base = xst[xs_i];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dma_lds16(xsrc[k] + b * 256, base + 1024 * (wave + 4 * k));
+        if (e4) dma_lds4(esrc + 4 * b, base + eoff);
+        else dma_lds16(esrc + 32 * b, base + eoff);
+    };
+
+    float acc[4][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[n][i] = 0.0f;
+
+    // queue per wave, oldest first: X(0) | W(0) X(1) | W(1) X(2) | ... — at block b's top the
+    // newest group (W(b) X(b+1)) is in flight and only X(b+1) may stay so
+    issue_x(0, 0);
+    issue_w(0, 0);
+    issue_x(1, 1);
+    int xi = 0;
+    for (int64_t b = 0; b < nblk; ++b) {
+        const int wi = (int) (b & 1);
+        const uint8_t * wq = wst[wi];
+        const uint8_t * xb = xst[xi];
+        const int8_t * xq = (const int8_t *) xb;
+        const float * xd = (const float *) (xb + S::XD);
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(S::NXI) : "memory");
+        __syncthreads();   // block b's stages landed for every wave; block b-1's reads are done
+        issue_w(b + 1, wi ^ 1);
+        issue_x(b + 2, xi == 0 ? 2 : xi - 1);
+        if (tid < MQ_BM) {
+            int sc[16], mn[8];
+            float d, dmin;
+            W::unpack(wq + tid * RS, sc, mn, d, dmin);
+#pragma unroll
+            for (int j = 0; j < W::NSC; ++j) wsc[tid][j] = (uint8_t) sc[j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wmn[tid][j] = (uint8_t) mn[j];
+            wd[tid] = d; wdm[tid] = dmin;
+        } else if (tid < MQ_BM + MQ_BN) {
+            const int t = tid - MQ_BM;
+            const int16_t * s16 = (const int16_t *) (xb + S::XS) + 16 * t;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xs[t][j] = s16[2 * j] + s16[2 * j + 1];
+        }
+        __syncthreads();
+        const int rA = 16 * wave + c16;
+        int sumi[4][4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sumi[n][i] = 0;
+#pragma unroll 2
+        for (int c = 0; c < 8; ++c) {
+            const long a = W::afrag(wq + rA * RS, c, h);
+            int scv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) scv[i] = wsc[16 * wave + 4 * h + i][c];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 16 * ((2 * c + (h >> 1)) ^ c16) + 8 * (h & 1));
+                v4i r = {0, 0, 0, 0};
+                r = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, bf, r, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sumi[n][i] += __mul24(r[i], scv[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = 16 * wave + 4 * h + i;
+            const float dw = wd[r], dmw = wdm[r];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int t = 16 * n + c16;
+                const float dy = xd[t];
+                int summ = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) summ += __mul24((int) wmn[r][j], xs[t][j]);
+                acc[n][i] += (dw * dy) * (float) sumi[n][i] - (dmw * dy) * (float) summ;
+            }
+        }
+        xi = xi == 2 ? 0 : xi + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped tail loads land before exit
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int64_t t = tok0 + 16 * n + c16;
+        if (t >= T) continue;
+        char * drow = (char *) p.dst + t * p.nb1;
+        if (p.cnt) {
+            const int pair = p.list[col0 + t];
+            drow = (char *) p.dst + (pair % p.n_used) * p.nb1 + (pair / p.n_used) * p.nb2;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t m = row0 + 16 * wave + 4 * h + i;
+            if (m < p.M) *(float *) (drow + m * 4) = acc[n][i];
+        }
+    }
+}
+
+// GGML_MI355X_MMQ_DB: 0 = single-buffered k_mmq, 1 = k_mmq_db, 2 = k_mmq_p2
+static int mmq_db_mode() {
+    static const int m = getenv("GGML_MI355X_MMQ_DB") ? atoi(getenv("GGML_MI355X_MMQ_DB")) : 1;
+    return m;
 }
 
 template <class W>
 static void launch_mmq(hipStream_t st, const dim3 & grid, const mmq_args & p) {
-    if (mmq_db_on()) hipLaunchKernelGGL(k_mmq_db<W>, grid, dim3(256), 0, st, p);
+    const int m = mmq_db_mode();
+    if constexpr (std::is_same<W, mq_q4_K>::value) {
+        if (m == 2) { hipLaunchKernelGGL(k_mmq_p2<W>, grid, dim3(256), 0, st, p); return; }
+    }
+    if (m == 1) hipLaunchKernelGGL(k_mmq_db<W>, grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL(k_mmq<W>, grid, dim3(256), 0, st, p);
 }
 
