@@ -19,6 +19,7 @@
 namespace mi355x {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
 constexpr int MQ_BM = 64, MQ_BN = 64;
@@ -427,6 +428,22 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
                 }
             }
         }
+        // the mins term summ[r][t] = sum_j mn[r][j] * bsum[t][j] of the 64 x 64 tile is a K = 8
+        // product: two fp32 MFMAs per 16 x 16 tile.  Every product (< 2^18) and partial sum
+        // (< 2^21) is an integer below 2^24, so the result is exact in any order — the same
+        // value as the integer loop of k_mmq
+        v4f smm[4];
+        if constexpr (W::NSC == 8) {
+            const float a0 = (float) wmn[16 * wave + c16][h], a1 = (float) wmn[16 * wave + c16][h + 4];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int t = 16 * n + c16;
+                v4f z = {0.f, 0.f, 0.f, 0.f};
+                z = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, (float) xs[t][h], z, 0, 0, 0);
+                z = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, (float) xs[t][h + 4], z, 0, 0, 0);
+                smm[n] = z;
+            }
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int r = 16 * wave + 4 * h + i;
@@ -436,10 +453,7 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
                 const int t = 16 * n + c16;
                 const float dy = xd[t];
                 if constexpr (W::NSC == 8) {
-                    int summ = 0;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) summ += __mul24(wmn[r][j], xs[t][j]);
-                    acc[n][i] += (dw * dy) * (float) sumi[n][i] - (dmw * dy) * (float) summ;
+                    acc[n][i] += (dw * dy) * (float) sumi[n][i] - (dmw * dy) * smm[n][i];
                 } else {
                     acc[n][i] += (dw * dy) * (float) sumi[n][i];
                 }
