@@ -108,8 +108,10 @@ __device__ __forceinline__ float dot_f16_avx512_q4(const uint2 (&kh)[D / 16], co
     return __fadd_rn(__fadd_rn(w[0], w[2]), __fadd_rn(w[1], w[3]));
 }
 
-template <int D> struct fax_cfg {
-    static constexpr int CH = D <= 128 ? 256 : 128;   // positions per chunk (V chunk <= 64 KiB)
+template <int D, int CHO = 0> struct fax_cfg {
+    // positions per chunk (V chunk <= 64 KiB); CHO overrides it (prefill: a 32 KiB chunk lets
+    // more workgroups share a CU)
+    static constexpr int CH = CHO ? CHO : (D <= 128 ? 256 : 128);
     static constexpr int NP = CH / 64;                // score passes per chunk (64 positions each)
     static constexpr int RPP = 512 / D;               // V rows per 1 KiB global_load_lds piece
     static constexpr int U = 8;                       // phase-3 positions per batch
@@ -117,9 +119,9 @@ template <int D> struct fax_cfg {
 
 // OCC = workgroups per CU the register budget allows: 1 for decode (32-64 workgroups, every
 // register for ILP), 2 for prefill (thousands of workgroups; the LDS allows two)
-template <int D, int OCC = 1>
+template <int D, int OCC = 1, int CHO = 0>
 __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
-    using C = fax_cfg<D>;
+    using C = fax_cfg<D, CHO>;
     constexpr int CH = C::CH, U = C::U, NM = D / 16;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int qd = tid & 3;                 // lane in the quad of a position (phase 1)
@@ -420,12 +422,19 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     a.warm.nwg = (int) (wy * a.n_q);
     const dim3 grid((unsigned) a.n_q, (unsigned) (a.H * nq3 + wy));
     static const int pocc = getenv("GGML_MI355X_FA_PREFILL_OCC") ? atoi(getenv("GGML_MI355X_FA_PREFILL_OCC")) : 2;
-    const bool wide = a.n_q * a.H * nq3 > 256 && pocc == 2;   // prefill: more workgroups than CUs
+    // prefill chunk: GGML_MI355X_FA_PREFILL_CH = 128 (default: 32 KiB of V in LDS; half the
+    // phase-1 K registers, so OCC 2 fits 256 VGPRs without the 40 spills of CH 256 — pp512
+    // 9.6k -> 10.6k tok/s; OCC 3/4 spill and run slower, 8.5k / 8.2k) or 256 (64 KiB)
+    static const int pch = getenv("GGML_MI355X_FA_PREFILL_CH") ? atoi(getenv("GGML_MI355X_FA_PREFILL_CH")) : 128;
+    const bool wide = a.n_q * a.H * nq3 > 256 && pocc >= 2;   // prefill: more workgroups than CUs
     switch (a.D) {
         case 64:  hipLaunchKernelGGL(k_fattn_exact<64>, grid, dim3(256), 0, st, a); break;
         case 128:
-            if (wide) hipLaunchKernelGGL((k_fattn_exact<128, 2>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL(k_fattn_exact<128>, grid, dim3(256), 0, st, a);
+            if (!wide) hipLaunchKernelGGL(k_fattn_exact<128>, grid, dim3(256), 0, st, a);
+            else if (pch == 128 && pocc == 4) hipLaunchKernelGGL((k_fattn_exact<128, 4, 128>), grid, dim3(256), 0, st, a);
+            else if (pch == 128 && pocc == 3) hipLaunchKernelGGL((k_fattn_exact<128, 3, 128>), grid, dim3(256), 0, st, a);
+            else if (pch == 128) hipLaunchKernelGGL((k_fattn_exact<128, 2, 128>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((k_fattn_exact<128, 2>), grid, dim3(256), 0, st, a);
             break;
         case 256: hipLaunchKernelGGL(k_fattn_exact<256>, grid, dim3(256), 0, st, a); break;
         default: GGML_ABORT("mi355x: FA head size %d", (int) a.D);
