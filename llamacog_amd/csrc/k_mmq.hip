@@ -93,6 +93,7 @@ struct mmq_args {
     // activation columns off[z] .. off[z] + cnt[z] - 1, column j is pair list[j] = e + n_used * t and
     // lands at dst + e * nb1 + t * nb2; nullptr cnt = a plain MUL_MAT
     const int32_t * cnt; const int32_t * off; const int32_t * list; int64_t n_used; int64_t nb02; int64_t nb2;
+    int xcd;   // k_mmq_db: XCD-aware tile order (plain MUL_MAT, gridDim.x % 8 == 0)
 };
 
 template <class W>
@@ -287,8 +288,18 @@ __global__ __launch_bounds__(256, MQ_DB_OCC) void k_mmq_db(const mmq_args p) {
     __shared__ int xs[MQ_BN][8];   // Q8_K sums per 32-element chunk
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t row0 = (int64_t) blockIdx.x * MQ_BM;
-    const int64_t tok0 = (int64_t) blockIdx.y * MQ_BN;
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs in dispatch order, so
+    // dispatch slot L runs on XCD L % 8.  With p.xcd, XCD x takes row groups x, x + 8, ... and
+    // walks each one's token tiles back to back: the tiles sharing a 64-row weight slice run
+    // together on one XCD and read it from that XCD's L2 (a bijection for gridDim.x % 8 == 0)
+    unsigned bx = blockIdx.x, by = blockIdx.y;
+    if (p.xcd) {
+        const unsigned L = blockIdx.x + gridDim.x * blockIdx.y, slot = L >> 3;
+        bx = (L & 7) + 8 * (slot / gridDim.y);
+        by = slot % gridDim.y;
+    }
+    const int64_t row0 = (int64_t) bx * MQ_BM;
+    const int64_t tok0 = (int64_t) by * MQ_BN;
     const int h = lane >> 4, c16 = lane & 15;
     const uint8_t * Wb = p.W;
     int64_t T = p.T, col0 = 0;
@@ -717,6 +728,9 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
     p.dst = (float *) dst->data; p.nb1 = dst->nb[1];
     p.cnt = p.off = p.list = nullptr; p.n_used = 1; p.nb02 = 0; p.nb2 = 0;
     const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(p.T, MQ_BN));
+    // measured neutral on pp512 (10.3k-10.5k tok/s either way): the tiles are not L2-bound, so off
+    static const int xcd = getenv("GGML_MI355X_MMQ_XCD") ? atoi(getenv("GGML_MI355X_MMQ_XCD")) : 0;
+    p.xcd = xcd && grid.x % 8 == 0;
     switch (w->type) {
         case GGML_TYPE_Q4_K: launch_mmq<mq_q4_K>(ctx.stream, grid, p); break;
         case GGML_TYPE_Q5_K: launch_mmq<mq_q5_K>(ctx.stream, grid, p); break;
@@ -745,6 +759,7 @@ void mul_mat_q_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, const i
     p.T = n_pairs;
     p.dst = (float *) dst->data; p.nb1 = dst->nb[1];
     p.cnt = cnt; p.off = off; p.list = list; p.n_used = ids->ne[0]; p.nb02 = w->nb[2]; p.nb2 = dst->nb[2];
+    p.xcd = 0;
     const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(n_pairs, MQ_BN), (unsigned) w->ne[2]);
     switch (w->type) {
         case GGML_TYPE_Q4_K: launch_mmq<mq_q4_K>(ctx.stream, grid, p); break;
