@@ -13,6 +13,8 @@
 #include <string.h>
 
 #include "ggml.h"
+#include "ggml-alloc.h"
+#include "ggml-backend.h"
 #include "ggml-cpu.h"
 
 static struct ggml_context * mk_ctx(size_t mb) {
@@ -61,6 +63,46 @@ void gg_mul_mat(int type, const void * W, int64_t K, int64_t M, const float * X,
     run(ctx, y, nth);
     memcpy(Y, y->data, ggml_nbytes(y));
     ggml_free(ctx);
+}
+
+/* Y[T][M] = mul_mat(W[M][K], X[T][K]) the way libllama runs it on the CPU backend: the
+ * weight in the CPU device's first extra buffer type (CPU_REPACK: set_tensor repacks Q4_K /
+ * Q4_0 rows for the 8x8 AVX2 kernels, ggml-cpu/repack.cpp:1416-1480) when use_extra is set,
+ * else in the default CPU buffer; the graph computed by ggml_backend_graph_compute. */
+int gg_mul_mat_backend(int type, const void * W, int64_t K, int64_t M, const float * X, int64_t T, float * Y, int nth,
+                       int use_extra) {
+    ggml_backend_t be = ggml_backend_cpu_init();
+    ggml_backend_cpu_set_n_threads(be, nth);
+    ggml_backend_dev_t dev = ggml_backend_get_device(be);
+    ggml_backend_reg_t reg = ggml_backend_dev_backend_reg(dev);
+    ggml_backend_buffer_type_t wbuft = ggml_backend_get_default_buffer_type(be);
+    if (use_extra) {
+        ggml_backend_dev_get_extra_bufts_t get = (ggml_backend_dev_get_extra_bufts_t)
+            ggml_backend_reg_get_proc_address(reg, "ggml_backend_dev_get_extra_bufts");
+        ggml_backend_buffer_type_t * ex = get ? get(dev) : NULL;
+        if (!ex || !ex[0]) { ggml_backend_free(be); return -1; }
+        wbuft = ex[0];
+    }
+    struct ggml_init_params ip = {ggml_tensor_overhead() * 8 + ggml_graph_overhead(), NULL, true};
+    struct ggml_context * cw = ggml_init(ip);
+    struct ggml_context * cx = ggml_init(ip);
+    struct ggml_tensor * w = ggml_new_tensor_2d(cw, (enum ggml_type) type, K, M);
+    struct ggml_tensor * x = ggml_new_tensor_2d(cx, GGML_TYPE_F32, K, T);
+    struct ggml_tensor * y = ggml_mul_mat(cx, w, x);
+    ggml_backend_buffer_t bw = ggml_backend_alloc_ctx_tensors_from_buft(cw, wbuft);
+    ggml_backend_buffer_t bx = ggml_backend_alloc_ctx_tensors_from_buft(cx, ggml_backend_get_default_buffer_type(be));
+    ggml_backend_tensor_set(w, W, 0, ggml_nbytes(w));
+    ggml_backend_tensor_set(x, X, 0, ggml_nbytes(x));
+    struct ggml_cgraph * gf = ggml_new_graph(cx);
+    ggml_build_forward_expand(gf, y);
+    const int st = (int) ggml_backend_graph_compute(be, gf);
+    ggml_backend_tensor_get(y, Y, 0, ggml_nbytes(y));
+    ggml_backend_buffer_free(bw);
+    ggml_backend_buffer_free(bx);
+    ggml_free(cw);
+    ggml_free(cx);
+    ggml_backend_free(be);
+    return st;
 }
 
 /* Y[T][n_used][M] = mul_mat_id(As [n_as][M][K], X [T][ne11][K], ids [T][n_used]) on the CPU backend */

@@ -83,6 +83,8 @@ static float dot_avx512(const float * x, const float * y, int64_t n) {
     return (float) sumf;
 }
 
+float orc_dot_cpu(int type, int64_t n, const void * vx, const void * vy, int repack);
+
 /* K·Q of the CPU flash-attention for an f16 cache: Q rounded to f16, ggml_vec_dot_f16 */
 void orc_fa_scores(const float * q, const uint16_t * k, int64_t n, int64_t D, float * s);
 
@@ -397,6 +399,251 @@ void orc_mul_mat(int type, const void * W, int64_t K, int64_t M, const float * X
     free(xq);
 }
 
+/* ==== The CPU backend's float combination orders (x86-64-v4 build, the variant the
+ * reference's loader picks on the build container and on the MI355X host) =====================
+ * Integer parts are exact in any order; what these restate is where the CPU rounds.  Every
+ * kernel keeps per-block integer sums in int32 SIMD lanes and accumulates them into f32 lanes
+ * with one FMA per block, so the float result is a set of per-lane FMA chains over the blocks
+ * in order, then a fixed horizontal reduction.  In all the 256-bit kernels below a 32-bit lane
+ * holds the 4-byte group (e % 32) / 4 of every 32-element chunk: "class" c of element e. */
+
+/* hsum_float_8 (ggml-cpu/arch/x86/quants.c:27-58): ((a0+a4)+(a2+a6)) + ((a1+a5)+(a3+a7)) */
+static float hsum8(const float * a) {
+    float r[4];
+    for (int i = 0; i < 4; ++i) r[i] = a[i + 4] + a[i];
+    return (r[0] + r[2]) + (r[1] + r[3]);
+}
+
+/* unpacked weight quants of one 256-block (value per element, before the -32 of q6_K) */
+static void unpack_k(int type, const void * blk, int8_t * a) {
+    if (type == T_Q6_K) {
+        const b_q6_K * x = (const b_q6_K *) blk;
+        for (int h = 0; h < 2; ++h)
+            for (int l = 0; l < 32; ++l) {
+                const uint8_t * ql = x->ql + 64 * h; const uint8_t * qh = x->qh + 32 * h;
+                a[128 * h + l + 0]  = (int8_t) ((ql[l] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+                a[128 * h + l + 32] = (int8_t) ((ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+                a[128 * h + l + 64] = (int8_t) ((ql[l] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+                a[128 * h + l + 96] = (int8_t) ((ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+            }
+        return;
+    }
+    const uint8_t * q4 = type == T_Q4_K ? ((const b_q4_K *) blk)->qs : ((const b_q5_K *) blk)->qs;
+    const uint8_t * hm = type == T_Q5_K ? ((const b_q5_K *) blk)->qh : NULL;
+    uint8_t m = 1;
+    for (int j = 0; j < 4; ++j) {
+        for (int l = 0; l < 32; ++l) a[64 * j + l] = (int8_t) ((q4[32 * j + l] & 0xF) + (hm && (hm[l] & m) ? 16 : 0));
+        m <<= 1;
+        for (int l = 0; l < 32; ++l) a[64 * j + 32 + l] = (int8_t) ((q4[32 * j + l] >> 4) + (hm && (hm[l] & m) ? 16 : 0));
+        m <<= 1;
+    }
+}
+
+/* The per-class integers of one block: cls[c] = sum over elements e of class c of
+ * scale(e) * q(e) * y(e); min = sum_s m_s * (bsums[2s] + bsums[2s+1]) for q4_K / q5_K.
+ * Exposed for the GPU tests (the kernels produce the same integers). */
+void orc_block_classes(int type, const void * blk, const void * yblk, int32_t * cls, int32_t * imin) {
+    for (int c = 0; c < 8; ++c) cls[c] = 0;
+    if (imin) *imin = 0;
+    if (type == T_Q8_0) {
+        const b_q8_0 * x = (const b_q8_0 *) blk; const b_q8_0 * y = (const b_q8_0 *) yblk;
+        for (int e = 0; e < 32; ++e) cls[e / 4] += x->qs[e] * y->qs[e];
+        return;
+    }
+    if (type == T_Q4_0) {
+        const b_q4_0 * x = (const b_q4_0 *) blk; const b_q8_0 * y = (const b_q8_0 *) yblk;
+        for (int j = 0; j < 16; ++j) {
+            cls[j / 4] += ((x->qs[j] & 0xF) - 8) * y->qs[j];
+            cls[4 + j / 4] += ((x->qs[j] >> 4) - 8) * y->qs[j + 16];
+        }
+        return;
+    }
+    const b_q8_K * y = (const b_q8_K *) yblk;
+    int8_t a[QK_K];
+    unpack_k(type, blk, a);
+    if (type == T_Q6_K) {
+        const b_q6_K * x = (const b_q6_K *) blk;
+        for (int e = 0; e < QK_K; ++e) cls[(e % 32) / 4] += x->scales[e / 16] * a[e] * y->qs[e];
+        return;
+    }
+    const uint8_t * sc12 = type == T_Q4_K ? ((const b_q4_K *) blk)->scales : ((const b_q5_K *) blk)->scales;
+    int mn_sum = 0;
+    for (int s = 0; s < 8; ++s) {
+        uint8_t sc, mn;
+        get_scale_min_k4(s, sc12, &sc, &mn);
+        for (int l = 0; l < 32; ++l) cls[l / 4] += sc * a[32 * s + l] * y->qs[32 * s + l];
+        mn_sum += mn * (y->bsums[2 * s] + y->bsums[2 * s + 1]);
+    }
+    if (imin) *imin = mn_sum;
+}
+
+/* One output element of the CPU's mul_mat, weight row wx (n elements) against the activation
+ * row vy already in the vec_dot_type, in the order the x64-v4 CPU backend computes it:
+ *   repack = 0: the vec_dot kernels (ggml-cpu/arch/x86/quants.c):
+ *     q8_0  :965   acc[c] = fma(dx*dy, I[c], acc[c]) per 32-block;       hsum8(acc)
+ *               (llamafile tinyBLAS_Q0_AVX for T >= 2, sgemm.cpp:914-961, has the same order)
+ *     q4_K  :1837  acc[c] = fma(dy*dx, I[c], acc[c]); acc_m[k] = fma(-dy*dmin, P[k], acc_m[k])
+ *               with P[k] the min products of sub-blocks 2k, 2k+1; hsum8(acc) + ((m0+m2)+(m1+m3))
+ *     q5_K  :2062  acc[c] = fma(dy*dx, I[c], acc[c]); summs = fma(Imin, -dy*dmin, summs);
+ *               hsum8(acc) + summs
+ *     q6_K  :2324  acc[c] = fma(dy*dx, I[c], acc[c]);                       hsum8(acc)
+ *   repack = 1: weights in the CPU_REPACK buffer (ggml-cpu/repack.cpp:1416-1458, AVX2, rows % 8):
+ *     q4_K  ggml_gemv/gemm_q4_K_8x8_q8_K (arch/x86/repack.cpp:718, 1771):
+ *               A = fma(Iacc, dx*dy, A); B = fma(Imin, dmin*dy, B); A - B
+ *     q4_0  ggml_gemv/gemm_q4_0_8x8_q8_0 (arch/x86/repack.cpp:579, 992): A = fma(I, dx*dy, A)
+ */
+float orc_dot_cpu(int type, int64_t n, const void * vx, const void * vy, int repack) {
+    int32_t cls[8], imin;
+    if (type == T_Q8_0 || type == T_Q4_0) {
+        const int64_t nb = n / 32;
+        float acc[8] = {0}, A = 0.0f;
+        for (int64_t b = 0; b < nb; ++b) {
+            const b_q8_0 * y = (const b_q8_0 *) vy + b;
+            const void * xb = type == T_Q8_0 ? (const void *) ((const b_q8_0 *) vx + b) : (const void *) ((const b_q4_0 *) vx + b);
+            const uint16_t xd16 = type == T_Q8_0 ? ((const b_q8_0 *) xb)->d : ((const b_q4_0 *) xb)->d;
+            orc_block_classes(type, xb, y, cls, NULL);
+            const float d = orc_fp16_to_fp32(xd16) * orc_fp16_to_fp32(y->d);
+            if (type == T_Q4_0 && repack) {
+                int I = 0;
+                for (int c = 0; c < 8; ++c) I += cls[c];
+                A = fmaf((float) I, d, A);
+            } else {
+                for (int c = 0; c < 8; ++c) acc[c] = fmaf(d, (float) cls[c], acc[c]);
+            }
+        }
+        return (type == T_Q4_0 && repack) ? A : hsum8(acc);
+    }
+    const int64_t nb = n / QK_K;
+    const int bsz = orc_type_size(type);
+    float acc[8] = {0}, accm[4] = {0}, A = 0.0f, B = 0.0f, summs = 0.0f;
+    for (int64_t b = 0; b < nb; ++b) {
+        const char * xb = (const char *) vx + b * bsz;
+        const b_q8_K * y = (const b_q8_K *) vy + b;
+        orc_block_classes(type, xb, y, cls, &imin);
+        if (type == T_Q6_K) {
+            const float d = y->d * orc_fp16_to_fp32(((const b_q6_K *) xb)->d);
+            for (int c = 0; c < 8; ++c) acc[c] = fmaf(d, (float) cls[c], acc[c]);
+            continue;
+        }
+        const uint16_t d16 = type == T_Q4_K ? ((const b_q4_K *) xb)->d : ((const b_q5_K *) xb)->d;
+        const uint16_t m16 = type == T_Q4_K ? ((const b_q4_K *) xb)->dmin : ((const b_q5_K *) xb)->dmin;
+        if (type == T_Q4_K && repack == 1) {
+            int I = 0;
+            for (int c = 0; c < 8; ++c) I += cls[c];
+            A = fmaf((float) I, orc_fp16_to_fp32(d16) * y->d, A);
+            B = fmaf((float) imin, orc_fp16_to_fp32(m16) * y->d, B);
+            continue;
+        }
+        if (type == T_Q4_K && repack == 2) {
+            /* the gemm accumulates once per PAIR of sub-blocks (arch/x86/repack.cpp:2155-2168) */
+            const uint8_t * sc12 = ((const b_q4_K *) xb)->scales;
+            int8_t a[QK_K];
+            unpack_k(type, xb, a);
+            const float dd = orc_fp16_to_fp32(d16) * y->d, dm = orc_fp16_to_fp32(m16) * y->d;
+            for (int sb = 0; sb < 4; ++sb) {
+                int I = 0, Mn = 0;
+                for (int u = 0; u < 2; ++u) {
+                    const int s = 2 * sb + u;
+                    uint8_t sc, mn;
+                    get_scale_min_k4(s, sc12, &sc, &mn);
+                    int dot = 0;
+                    for (int l = 0; l < 32; ++l) dot += a[32 * s + l] * y->qs[32 * s + l];
+                    I += sc * dot;
+                    Mn += mn * (y->bsums[2 * s] + y->bsums[2 * s + 1]);
+                }
+                A = fmaf((float) I, dd, A);
+                B = fmaf((float) Mn, dm, B);
+            }
+            continue;
+        }
+        const float d = y->d * orc_fp16_to_fp32(d16);
+        const float dmin = -y->d * orc_fp16_to_fp32(m16);
+        for (int c = 0; c < 8; ++c) acc[c] = fmaf(d, (float) cls[c], acc[c]);
+        if (type == T_Q5_K) {
+            summs = fmaf((float) imin, dmin, summs);
+        } else {
+            const uint8_t * sc12 = ((const b_q4_K *) xb)->scales;
+            for (int k = 0; k < 4; ++k) {
+                uint8_t sc, m0, m1;
+                get_scale_min_k4(2 * k, sc12, &sc, &m0);
+                get_scale_min_k4(2 * k + 1, sc12, &sc, &m1);
+                const int P = m0 * (y->bsums[4 * k] + y->bsums[4 * k + 1]) + m1 * (y->bsums[4 * k + 2] + y->bsums[4 * k + 3]);
+                accm[k] = fmaf(dmin, (float) P, accm[k]);
+            }
+        }
+    }
+    if (type == T_Q4_K && repack) return A - B;   /* 1: gemv, 2: gemm */
+    if (type == T_Q5_K) return hsum8(acc) + summs;
+    if (type == T_Q4_K) return hsum8(acc) + ((accm[0] + accm[2]) + (accm[1] + accm[3]));
+    return hsum8(acc);
+}
+
+/* ggml_quantize_mat_q8_K_4x8 (arch/x86/repack.cpp:315-530), the activation quantizer of the
+ * repacked Q4_K gemm for every group of 4 rows: the values of quantize_row_q8_K_ref except
+ * for the sign of iscale, which is -127/amax whenever +amax occurs in the block (the scalar
+ * reference takes the sign of the FIRST element of largest magnitude). */
+void orc_quantize_row_q8_K_4x8(const float * x, void * vy, int64_t k) {
+    b_q8_K * y = (b_q8_K *) vy;
+    for (int64_t i = 0; i < k / QK_K; i++, x += QK_K) {
+        float amax = 0.0f;
+        for (int j = 0; j < QK_K; ++j) amax = MAXF(amax, fabsf(x[j]));
+        int pos = 0;
+        for (int j = 0; j < QK_K; ++j) pos |= x[j] == amax;
+        const float iscale = amax != 0.0f ? (pos ? -127.f / amax : 127.f / amax) : 0.0f;
+        for (int j = 0; j < QK_K; ++j) {
+            const volatile float prod = x[j] * iscale;
+            y[i].qs[j] = (int8_t) rintf(prod);
+        }
+        for (int j = 0; j < QK_K / 16; ++j) {
+            int sum = 0;
+            for (int ii = 0; ii < 16; ++ii) sum += y[i].qs[j * 16 + ii];
+            y[i].bsums[j] = (int16_t) sum;
+        }
+        y[i].d = amax != 0.0f ? 1 / iscale : 0.0f;
+    }
+}
+
+/* tinyBLAS<16, __m512> (llamafile/sgemm.cpp:331-427): per output one 16-lane FMA chain over K
+ * in steps of 16, then _mm512_reduce_add_ps — the CPU's f32 mul_mat for T >= 2 when
+ * K % 16 == 0 and M % 4 == 0 (sgemm.cpp:3324-3345) */
+static float dot_tinyblas16(const float * a, const float * b, int64_t n) {
+    float acc[16] = {0};
+    for (int64_t l = 0; l < n; l += 16)
+        for (int i = 0; i < 16; ++i) acc[i] = fmaf(a[l + i], b[l + i], acc[i]);
+    return reduce16(acc);
+}
+
+/* The CPU backend's mul_mat as libllama runs it (ggml-cpu/ggml-cpu.c:1192-1384, with the
+ * repack and llamafile paths).  repack = 1: Q4_K / Q4_0 weights with M % 8 == 0 sit in the
+ * CPU_REPACK buffer (libllama's default).  W: M rows of K; X: T rows of K; Y: T rows of M. */
+void orc_mul_mat_cpu(int type, const void * W, int64_t K, int64_t M, const float * X, int64_t T, float * Y, int repack) {
+    const size_t wrow = (size_t) (K / orc_block_size(type)) * orc_type_size(type);
+    if (type == T_F32) {
+        const int tiny = T >= 2 && K % 16 == 0 && M % 4 == 0;
+        for (int64_t t = 0; t < T; ++t)
+            for (int64_t m = 0; m < M; ++m) {
+                const float * w = (const float *) ((const char *) W + m * wrow);
+                Y[t * M + m] = tiny ? dot_tinyblas16(w, X + t * K, K) : dot_avx512(w, X + t * K, K);
+            }
+        return;
+    }
+    repack = repack && (type == T_Q4_K || type == T_Q4_0) && M % 8 == 0;
+    const int kq = type == T_Q4_K || type == T_Q5_K || type == T_Q6_K;
+    const size_t arow = kq ? (size_t) (K / 256) * sizeof(b_q8_K) : (size_t) (K / 32) * sizeof(b_q8_0);
+    char * xq = (char *) malloc(arow * T);
+    for (int64_t t = 0; t < T; ++t) {
+        if (!kq) orc_quantize_row_q8_0(X + t * K, xq + t * arow, K);
+        else if (repack && type == T_Q4_K && t < T - T % 4) orc_quantize_row_q8_K_4x8(X + t * K, xq + t * arow, K);
+        else orc_quantize_row_q8_K(X + t * K, xq + t * arow, K);
+    }
+    for (int64_t t = 0; t < T; ++t) {
+        const int mode = repack && type == T_Q4_K && t < T - T % 4 ? 2 : repack;
+        for (int64_t m = 0; m < M; ++m)
+            Y[t * M + m] = orc_dot_cpu(type, K, (const char *) W + m * wrow, xq + t * arow, mode);
+    }
+    free(xq);
+}
+
 /* ggml_compute_forward_mul_mat_id (ggml-cpu/ggml-cpu.c:1466-1600): for token t and slot e,
  * Y[t][e][:] = mul_mat(As[ids[t][e]], X[t][e % ne11]) with the mat-vec's per-row arithmetic
  * (the activation row quantized to the vec_dot_type, vec_dot per weight row).  As: n_as
@@ -578,7 +825,7 @@ void orc_flash_attn(const float * q, const void * k, const void * v, const uint1
                     for (int64_t d = 0; d < D; ++d) kf[d] = orc_fp16_to_fp32(((const uint16_t *) kd)[d]);
                     s = dot_avx512(kf, qf, D);
                 } else {
-                    s = orc_vec_dot(T_Q8_0, D, kd, q8, NULL, NULL);
+                    s = orc_dot_cpu(T_Q8_0, D, kd, q8, 0);   /* ggml_vec_dot_q8_0_q8_0 order */
                 }
                 s = s * scale;
                 if (softcap != 0.0f) s = softcap * tanhf(s);
@@ -593,8 +840,9 @@ void orc_flash_attn(const float * q, const void * k, const void * v, const uint1
                     } else {
                         vs = expf(s - M);
                     }
+                    /* ggml_vec_mad_f16, AVX-512: GGML_F16_VEC_FMA = _mm512_fmadd_ps (vec.h:262-291) */
                     for (int64_t d = 0; d < D; ++d)
-                        vkq16[d] = orc_fp32_to_fp16(orc_fp16_to_fp32(vkq16[d]) + orc_fp16_to_fp32(((const uint16_t *) vd)[d]) * vs);
+                        vkq16[d] = orc_fp32_to_fp16(fmaf(orc_fp16_to_fp32(((const uint16_t *) vd)[d]), vs, orc_fp16_to_fp32(vkq16[d])));
                 } else {
                     if (s > M) {
                         M = s;
@@ -604,7 +852,7 @@ void orc_flash_attn(const float * q, const void * k, const void * v, const uint1
                         vs = expf(s - M);
                     }
                     orc_dequantize_row(kv_type, vd, v32, D);
-                    for (int64_t d = 0; d < D; ++d) vkq32[d] += v32[d] * vs;
+                    for (int64_t d = 0; d < D; ++d) vkq32[d] = fmaf(v32[d], vs, vkq32[d]);   /* ggml_vec_mad_f32 */
                 }
                 S = FA_S_UPDATE(S, ms, vs);
             }

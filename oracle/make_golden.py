@@ -53,6 +53,8 @@ def load():
     lib.gg_mul_mat_id.argtypes = [ctypes.c_int, P, I64, I64, I64, P, I64, P, I64, I64, P, ctypes.c_int]
     lib.gg_argsort.argtypes = [P, I64, I64, ctypes.c_int, P]
     lib.gg_sum_rows.argtypes = [P, I64, I64, P]
+    lib.gg_mul_mat_backend.argtypes = [ctypes.c_int, P, I64, I64, P, I64, P, ctypes.c_int, ctypes.c_int]
+    lib.gg_mul_mat_backend.restype = ctypes.c_int
     lib.gg_init()
     return lib
 
@@ -150,11 +152,41 @@ def moe(lib):
     print(f"moe.npz {os.path.getsize(os.path.join(OUT, 'moe.npz'))} B")
 
 
+def cpu_orders(lib):
+    """mul_mat exactly as libllama runs it on the CPU backend (gg_mul_mat_backend): Q4_K / Q4_0
+    weights in the CPU_REPACK extra buffer (8x8 gemv for T % 4 rows, gemm for groups of 4),
+    the other types through the vec_dot / llamafile kernels; F32 (the MoE router) through
+    vec_dot_f32 at T = 1 and tinyBLAS at T >= 2.  These pin the float combination order that
+    oracle/ggml_oracle.c orc_mul_mat_cpu restates and the GPU kernels must reproduce."""
+    rng = np.random.default_rng(777)
+    g = {}
+    for t, name, M, K in ((Q4_K, "q4_K", 64, 2048), (Q6_K, "q6_K", 64, 2048), (Q5_K, "q5_K", 64, 1024),
+                          (Q8_0, "q8_0", 64, 1024), (Q4_0, "q4_0", 64, 1024), (F32, "f32", 8, 1024)):
+        w = (rng.standard_normal((M, K)) * 0.05).astype(np.float32)
+        w[: M // 4] = (0.1 + 2 * np.cos(np.arange(M // 4 * K, dtype=np.float32).reshape(M // 4, K) + 0.5)) * 0.05
+        wq = w if t == F32 else quantize(lib, t, w)
+        g[f"wq_{name}"] = wq
+        extra = 1 if t in (Q4_K, Q4_0) else 0
+        for T in (1, 3, 4, 9):
+            x = rng.standard_normal((T, K)).astype(np.float32)
+            if T >= 3:
+                x[1] = (0.1 + 2 * np.cos(np.arange(K, dtype=np.float32) + 1.0)).astype(np.float32)
+            y = np.zeros((T, M), dtype=np.float32)
+            st = lib.gg_mul_mat_backend(t, fptr(wq), K, M, fptr(x), T, fptr(y), 4, extra)
+            assert st == 0, st
+            g[f"x_{name}_{T}"] = x
+            g[f"y_{name}_{T}"] = y
+    np.savez_compressed(os.path.join(OUT, "mul_mat_cpu.npz"), **g)
+    print(f"mul_mat_cpu.npz {os.path.getsize(os.path.join(OUT, 'mul_mat_cpu.npz'))} B")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     lib = load()
     if "moe" in sys.argv[1:]:   # only the MoE fixture (the others stay as committed)
         return moe(lib)
+    if "cpu_orders" in sys.argv[1:]:
+        return cpu_orders(lib)
     rng = np.random.default_rng(1234)
 
     # ---- activation quantizers ------------------------------------------------------------
@@ -244,6 +276,7 @@ def main():
             fa[f"out_{kvname}_{n_q}"] = out
     np.savez_compressed(os.path.join(OUT, "flash_attn.npz"), D=D, H=H, Hkv=Hkv, n_kv=n_kv, **fa)
     moe(lib)
+    cpu_orders(lib)
     for f in sorted(os.listdir(OUT)):
         print(f"{f:28s} {os.path.getsize(os.path.join(OUT, f)):9d} B")
 

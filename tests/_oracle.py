@@ -45,6 +45,8 @@ def lib():
         L.orc_mul_mat_id.argtypes = [ctypes.c_int, P, I64, I64, I64, P, I64, I64, P, I64, I64, P]
         L.orc_argsort.argtypes = [P, I64, I64, ctypes.c_int, P]
         L.orc_sum_rows.argtypes = [P, I64, I64, P]
+        L.orc_mul_mat_cpu.argtypes = [ctypes.c_int, P, I64, I64, P, I64, P, ctypes.c_int]
+        L.orc_block_classes.argtypes = [ctypes.c_int, P, P, P, P]
         _lib = L
     return _lib
 
@@ -83,6 +85,15 @@ def mul_mat(t, wq, K, M, x):
     x = np.ascontiguousarray(x, dtype=np.float32)
     y = np.zeros((x.shape[0], M), dtype=np.float32)
     lib().orc_mul_mat(t, ptr(np.ascontiguousarray(wq)), K, M, ptr(x), x.shape[0], ptr(y))
+    return y
+
+
+def mul_mat_cpu(t, wq, K, M, x, repack=True):
+    """mul_mat in the CPU backend's exact float order as libllama runs it (orc_mul_mat_cpu):
+    Q4_K / Q4_0 weights repacked (rows % 8), the vec_dot / tinyBLAS orders otherwise."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.zeros((x.shape[0], M), dtype=np.float32)
+    lib().orc_mul_mat_cpu(t, ptr(np.ascontiguousarray(wq)), K, M, ptr(x), x.shape[0], ptr(y), 1 if repack else 0)
     return y
 
 

@@ -120,9 +120,9 @@ def test_flash_attn(golden_dir, n_q, kv):
     out = O.flash_attn(g[f"q_{n_q}"], g[f"k_{kv}_{n_q}"], g[f"v_{kv}_{n_q}"], g[f"mask_{n_q}"], kvt, D, H, Hkv, n_kv,
                        1.0 / np.sqrt(D))
     ref = g[f"out_{kv}_{n_q}"]
-    err = np.abs(out - ref).max() / np.abs(ref).max()
-    # f16 VKQ accumulation is restated rounding-for-rounding; only exp/dot-order ulps remain
-    assert err < (2e-3 if kv == "f16" else 2e-6), err
+    # bit-exact: K.Q in the CPU's vec_dot order (AVX-512 f16 / q8_0 class chains), libm expf,
+    # the FMA of ggml_vec_mad_f16 / _f32, the unfused S*ms + vs
+    assert (out.view(np.uint32) == ref.view(np.uint32)).all(), np.abs(out - ref).max() / np.abs(ref).max()
 
 
 MOE_TYPES = {"q4_K": O.Q4_K, "q5_K": O.Q5_K, "q6_K": O.Q6_K, "q8_0": O.Q8_0, "q4_0": O.Q4_0}
@@ -154,3 +154,20 @@ def test_sum_rows_restatement_bit_exact(golden_dir):
     g = load(golden_dir, "moe.npz")
     for nm in ("a", "b"):
         assert (O.sum_rows(g[f"sum_rows_{nm}_x"]).view(np.uint32) == g[f"sum_rows_{nm}_y"].view(np.uint32)).all()
+
+
+@pytest.mark.parametrize("name", ["q4_K", "q6_K", "q5_K", "q8_0", "q4_0", "f32"])
+@pytest.mark.parametrize("T", [1, 3, 4, 9])
+def test_mul_mat_cpu_order_bit_exact(golden_dir, name, T):
+    """orc_mul_mat_cpu reproduces the CPU backend's mul_mat BIT FOR BIT as libllama runs it:
+    repacked Q4_K gemv (T % 4 rows) and gemm (groups of 4), the AVX2 vec_dot class chains of
+    Q6_K / Q5_K / Q8_0, repacked Q4_0, and vec_dot_f32 / tinyBLAS for the f32 router
+    (goldens: gg_mul_mat_backend, the reference's own ggml_backend_graph_compute)."""
+    g = load(golden_dir, "mul_mat_cpu.npz")
+    t = {"q4_K": O.Q4_K, "q6_K": O.Q6_K, "q5_K": O.Q5_K, "q8_0": O.Q8_0, "q4_0": O.Q4_0, "f32": O.F32}[name]
+    wq = g[f"wq_{name}"]
+    x = g[f"x_{name}_{T}"]
+    y = g[f"y_{name}_{T}"]
+    got = O.mul_mat_cpu(t, wq, x.shape[1], y.shape[1], x)
+    assert (got.view(np.uint32) == y.view(np.uint32)).all(), \
+        f"{int((got.view(np.uint32) != y.view(np.uint32)).sum())} of {y.size} outputs differ"
