@@ -52,6 +52,7 @@ void * exec_ctx::scratch(int slot, size_t bytes) {
     }
     MI_CHECK(hipMalloc(&slot_ptr[slot], nsz));
     slot_size[slot] = nsz;
+    ++scratch_gen;
     return slot_ptr[slot];
 }
 
@@ -77,9 +78,20 @@ bool exec_ctx::prepare_dyn(ggml_cgraph * g) {
     if (!dyn_dev) {
         MI_CHECK(hipMalloc((void **) &dyn_dev, DYN_CAP * sizeof(void *)));
         dyn_cap = DYN_CAP;
+        for (int k = 0; k < 2; ++k) {
+            MI_CHECK(hipHostMalloc((void **) &dyn_pin[k], DYN_CAP * sizeof(void *), hipHostMallocDefault));
+            MI_CHECK(hipEventCreateWithFlags(&dyn_ev[k], hipEventDisableTiming));
+            MI_CHECK(hipEventRecord(dyn_ev[k], stream));
+        }
     }
-    // pageable source: the runtime stages it before returning, so dyn_host can be reused
-    MI_CHECK(hipMemcpyAsync(dyn_dev, dyn_host.data(), dyn_host.size() * sizeof(void *), hipMemcpyHostToDevice, stream));
+    // stage through pinned memory: the copy runs asynchronously on the stream, so the buffer it
+    // reads is only refilled once the copy that last used it has completed
+    const int k = dyn_flip;
+    dyn_flip ^= 1;
+    MI_CHECK(hipEventSynchronize(dyn_ev[k]));
+    memcpy(dyn_pin[k], dyn_host.data(), dyn_host.size() * sizeof(void *));
+    MI_CHECK(hipMemcpyAsync(dyn_dev, dyn_pin[k], dyn_host.size() * sizeof(void *), hipMemcpyHostToDevice, stream));
+    MI_CHECK(hipEventRecord(dyn_ev[k], stream));
     return true;
 }
 
@@ -92,6 +104,12 @@ void exec_ctx::free_scratch() {
     if (dyn_dev) (void) hipFree(dyn_dev);
     dyn_dev = nullptr;
     dyn_cap = 0;
+    for (int k = 0; k < 2; ++k) {
+        if (dyn_pin[k]) (void) hipHostFree(dyn_pin[k]);
+        if (dyn_ev[k]) (void) hipEventDestroy(dyn_ev[k]);
+        dyn_pin[k] = nullptr;
+        dyn_ev[k] = nullptr;
+    }
     if (fa_cnt) (void) hipFree(fa_cnt);
     fa_cnt = nullptr;
 }
@@ -308,6 +326,7 @@ struct graph_entry {
     int             seen = 0;
     hipGraphExec_t  exec = nullptr;
     uint64_t        last_use = 0;
+    uint64_t        gen = 0;          // exec_ctx::scratch_gen the graph was captured under
 };
 
 struct mi_backend_ctx {
@@ -442,90 +461,33 @@ static void mi_backend_synchronize(ggml_backend_t backend) {
     ctx->ex.collect_timing();
 }
 
-// ---- Infinity-Cache warm planner (warm.h) ----------------------------------------------------
-// GGML_MI355X_WARM="norm,fa,mulq" = MiB each latency-bound kernel kind may warm ahead (0 = off);
-// GGML_MI355X_WARM_WG="norm,fa,mulq" = warm workgroups it carries
-static struct warm_cfg {
-    int64_t budget[WARM_NKIND] = {0, 0, 0};
-    int     nwg[WARM_NKIND] = {32, 96, 256};
-    warm_cfg() {
-        int64_t mb[WARM_NKIND] = {0, 0, 0};
-        if (const char * e = getenv("GGML_MI355X_WARM")) {
-            long a = 0, b = 0, c = 0;
-            const int n = sscanf(e, "%ld,%ld,%ld", &a, &b, &c);
-            mb[0] = n >= 1 ? a : 0; mb[1] = n >= 2 ? b : 0; mb[2] = n >= 3 ? c : 0;
-        }
-        for (int k = 0; k < WARM_NKIND; ++k) budget[k] = mb[k] << 20;
-        if (const char * e = getenv("GGML_MI355X_WARM_WG")) {
-            int a = 0, b = 0, c = 0;
-            if (sscanf(e, "%d,%d,%d", &a, &b, &c) == 3) { nwg[0] = a; nwg[1] = b; nwg[2] = c; }
-        }
-    }
-} g_warm;
-
-void exec_ctx::warm_plan(ggml_cgraph * g) {
-    warm_list.clear();
-    warm_cur = 0;
-    warm_off = 0;
-    const int n = ggml_graph_n_nodes(g);
-    for (int i = 0; i < n; ++i) {
-        const ggml_tensor * t = ggml_graph_node(g, i);
-        if (t->op == GGML_OP_MUL_MAT && gemv_supported(t)) {
-            warm_list.push_back({i, (const uint8_t *) t->src[0]->data, (int64_t) ggml_nbytes(t->src[0])});
-        }
-    }
-}
-
-warm_spec exec_ctx::warm_take(int kind) {
-    warm_spec s;
-    s.nseg = 0;
-    s.nwg = 0;
-    const int64_t budget = g_warm.budget[kind];
-    if (budget < 1024 || warm_list.empty() || !fusion_enabled()) return s;
-    // mat-vecs at or before the current node have run (or are running): never warm them
-    while (warm_cur < warm_list.size() && warm_list[warm_cur].node <= cur_node) { ++warm_cur; warm_off = 0; }
-    int64_t left = budget;
-    while (left >= 1024 && warm_cur < warm_list.size() && s.nseg < WARM_MAXSEG) {
-        const warm_seg & g = warm_list[warm_cur];
-        const int64_t take = std::min(g.n - warm_off, left) & ~(int64_t) 1023;
-        if (take > 0) {
-            s.p[s.nseg] = g.p + warm_off;
-            s.n[s.nseg] = take;
-            ++s.nseg;
-            left -= take;
-            warm_off += take;
-        }
-        if (g.n - warm_off < 1024) { ++warm_cur; warm_off = 0; }
-    }
-    s.nwg = s.nseg ? g_warm.nwg[kind] : 0;
-    return s;
-}
-
 static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.qcache_clear();
     ex.rt_table = nullptr;
-    ex.warm_plan(cgraph);
     ex.done.clear();
-    ex.pend = exec_ctx::pending_pro();
-    ex.post_add = nullptr;
     ex.silu_defer = ex.silu_mul = nullptr;
     const int n = ggml_graph_n_nodes(cgraph);
-    for (int i = 0; i < n;) {
-        ex.cur_node = i;
-        i += op_compute(ex, cgraph, i);
-    }
+    for (int i = 0; i < n;) i += op_compute(ex, cgraph, i);
     if (ex.silu_defer) {   // a deferred SILU whose MUL never came
         op_unary(ex, ex.silu_defer);
         ex.silu_defer = ex.silu_mul = nullptr;
-    }
-    if (ex.post_add) {   // a deferred in-place ADD with no later launch to carry it
-        op_binary(ex, ex.post_add);
-        ex.post_add = nullptr;
     }
 }
 
 // returns true when the graph was launched as (or captured into) a hipGraph
 static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
+    // a scratch slot grew since these graphs were captured (e.g. a longer prompt after
+    // decoding): their kernel arguments point at freed slots, so they are dropped and
+    // re-captured on a later sighting
+    for (auto it = ctx->graphs.begin(); it != ctx->graphs.end();) {
+        if (it->exec && it->gen != ctx->ex.scratch_gen) {
+            MI_CHECK(hipStreamSynchronize(ctx->ex.stream));
+            MI_CHECK(hipGraphExecDestroy(it->exec));
+            it = ctx->graphs.erase(it);
+        } else {
+            ++it;
+        }
+    }
     static thread_local std::vector<int64_t> sig;
     graph_signature(cgraph, sig);
     graph_entry * e = nullptr;
@@ -570,6 +532,7 @@ static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
         return false;
     }
     MI_CHECK(hipGraphDestroy(g));
+    e->gen = ctx->ex.scratch_gen;
     MI_CHECK(hipGraphLaunch(e->exec, ctx->ex.stream));
     g_graph_captures.fetch_add(1);
     return true;

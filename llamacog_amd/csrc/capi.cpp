@@ -289,7 +289,7 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv(int wtype, int64_t K, int64
 
 // epi_kind: 0 plain; 1 SiLU of matrix 0; 2 f16 (KV-cache) store of every matrix through a
 // dynamic-pointer slot; 3 NORM rope (Llama-3 parameters, head dim 128) of matrix 0 with its
-// f16 store; 4 activation prologue ADD -> RMS_NORM -> MUL (K-quants); 5 prologue MUL
+// f16 store
 extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int64_t M, int nmat, int copies, int iters, int epi_kind) {
     const ggml_type t = (ggml_type) wtype;
     const size_t row = ggml_row_size(t, K);
@@ -375,9 +375,9 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int6
         MI_CHECK(hipFree(ids)); MI_CHECK(hipFree(yid)); MI_CHECK(hipFree(x)); MI_CHECK(hipFree(y));
         return ms * 1000.0 / iters;
     }
-    // epilogue / prologue operands
+    // epilogue operands
     gemv_epi epi;
-    ggml_tensor S, Rt, P, A0, A1, Wn, Add, Nrm, Mul;
+    ggml_tensor S, Rt, P;
     float * fbuf; uint16_t * hbuf; void ** slots; int32_t * pos;
     MI_CHECK(hipMalloc(&fbuf, (M + 4 * K) * 4));
     MI_CHECK(hipMalloc(&hbuf, M * 2 * nmat));
@@ -410,27 +410,6 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int6
         epi.rope[0] = &Rt;
         epi.rope_f16[0] = (void * const *) slots;
         epi.elide_rope[0] = true;
-    } else if (epi_kind == 4 || epi_kind == 5) {
-        init_tensor(A0, GGML_TYPE_F32, nek, fbuf + M);
-        init_tensor(A1, GGML_TYPE_F32, nek, fbuf + M + K);
-        init_tensor(Wn, GGML_TYPE_F32, nek, fbuf + M + 2 * K);
-        init_tensor(Add, GGML_TYPE_F32, nek, fbuf + M + 3 * K);
-        init_tensor(Nrm, GGML_TYPE_F32, nek, fbuf + M + 3 * K);
-        init_tensor(Mul, GGML_TYPE_F32, nek, x);
-        if (epi_kind == 4) {
-            Add.op = GGML_OP_ADD; Add.src[0] = &A0; Add.src[1] = &A1;
-            Nrm.op = GGML_OP_RMS_NORM; Nrm.src[0] = &Add;
-            const float eps = 1e-5f;
-            memcpy(Nrm.op_params, &eps, 4);
-            Mul.op = GGML_OP_MUL; Mul.src[0] = &Nrm; Mul.src[1] = &Wn;
-            epi.pro = 1; epi.pro_add = &Add; epi.pro_norm = &Nrm; epi.pro_mul = &Mul;
-            epi.elide_norm = true;
-        } else {
-            Mul.op = GGML_OP_MUL; Mul.src[0] = &A0; Mul.src[1] = &A1;
-            epi.pro = 2; epi.pro_mul = &Mul;
-        }
-        epi.elide_mul = true;
-        if (!gemv_prologue_ok(mms[0])) return -2.0;
     }
     hipEvent_t e0, e1;
     MI_CHECK(hipEventCreate(&e0));

@@ -15,6 +15,7 @@
 
 #include "ggml.h"
 #include "ggml-backend.h"
+#include "libm_exact.h"
 
 extern "C" void ggml_log_internal(enum ggml_log_level level, const char * format, ...);
 
@@ -93,8 +94,9 @@ __device__ __forceinline__ float v_expf_avx512(float x) {
     return ldexpf(j, (int) n);  // _mm512_scalef_ps(j, n)
 }
 
-// float(exp(double(x))): libm expf as used by the CPU backend's scalar paths
-__device__ __forceinline__ float expf_cr(float x) { return (float) exp((double) x); }
+// glibc expf as the CPU backend's scalar paths call it (libm_exact.h restates its algorithm
+// bit for bit; a correctly rounded exp differs from it on a small fraction of inputs)
+__device__ __forceinline__ float expf_cr(float x) { return lx_expf(x); }
 
 // the _mm512_reduce_add_ps tree (GCC avx512fintrin.h) over 16 lane values
 __device__ __forceinline__ float reduce16_avx512(const float (&w)[16]) {

@@ -255,7 +255,7 @@ static ggml_tensor * rope_of(ggml_cgraph * g, const ggml_tensor * mm, int p, int
         if (base_of(x) != mm || x->data != mm->data || !ggml_is_contiguous(x) || !ggml_is_contiguous(r)) return nullptr;
         if (r->op_params[2] != 0 || r->type != GGML_TYPE_F32) return nullptr;   // NORM mode only
         const int n_dims = r->op_params[1];
-        if (x->ne[2] != 1 || x->ne[3] != 1 || x->ne[0] % 2 != 0 || n_dims > x->ne[0] || n_dims % 2 != 0) return nullptr;
+        if (x->ne[2] != 1 || x->ne[3] != 1 || x->ne[0] % 2 != 0 || n_dims > x->ne[0] || n_dims % 2 != 0 || n_dims > 512) return nullptr;
         if (r->src[1]->type != GGML_TYPE_I32) return nullptr;
         return r;
     }
@@ -305,84 +305,6 @@ static bool dead_after(ggml_cgraph * g, int n, int from, const ggml_tensor * t,
 }
 
 
-
-// Defer a producer chain into the prologue of the GEMV of `mm` (its direct consumer, the next
-// node): kind 1 = [add] -> norm -> [mul], kind 2 = mul (a * b).  The chain's outputs must not
-// overlap its inputs (other workgroups of the consuming launch still read the inputs while
-// workgroup 0 writes the outputs).
-static bool defer_to_prologue(exec_ctx & ctx, ggml_cgraph * g, int n, int kind, ggml_tensor * add, ggml_tensor * norm,
-                              ggml_tensor * mul, const ggml_tensor * mm) {
-    // GGML_MI355X_NO_PROLOGUE: 0 = on, 1 = off (default: every workgroup re-reading the
-    // producer's inputs costs more than the separate fused producer kernel, measured on
-    // Llama-3-8B decode: 331 tok/s off vs 225 on), 2 = norm chains only, 3 = FFN products
-    // only, 4 = no deferred in-place ADD
-    static const int mode = getenv("GGML_MI355X_NO_PROLOGUE") ? atoi(getenv("GGML_MI355X_NO_PROLOGUE")) : 1;
-    if (mode == 1 || (mode == 2 && kind == 2) || (mode == 3 && kind == 1)) return false;
-    if (!mm || mm->op != GGML_OP_MUL_MAT || !gemv_prologue_ok(mm)) return false;
-    const ggml_tensor * last = mul ? mul : norm;
-    if (mm->src[1] != last) return false;
-    const int64_t K = last->ne[0];
-    if (ggml_nrows(last) != 1 || K != mm->src[0]->ne[0]) return false;
-    std::vector<const ggml_tensor *> ins, outs;
-    if (kind == 1) {
-        if (!f32c(norm) || !f32c(norm->src[0])) return false;
-        if (add) {
-            if (!f32c(add) || !f32c(add->src[0]) || !f32c(add->src[1]) || norm->src[0] != add) return false;
-            if (!ggml_are_same_shape(add->src[0], add->src[1]) || !ggml_are_same_shape(add, norm)) return false;
-            ins.push_back(add->src[0]); ins.push_back(add->src[1]); outs.push_back(add);
-        } else {
-            ins.push_back(norm->src[0]);
-        }
-        outs.push_back(norm);
-        if (mul) {
-            if (!f32c(mul) || !f32c(mul->src[1]) || ggml_nelements(mul->src[1]) != K) return false;
-            ins.push_back(mul->src[1]); outs.push_back(mul);
-        }
-    } else {
-        if (!f32c(mul) || !f32c(mul->src[0]) || !f32c(mul->src[1])) return false;
-        if (!ggml_are_same_shape(mul->src[0], mul->src[1]) || !ggml_are_same_shape(mul, mul->src[0])) return false;
-        ins.push_back(mul->src[0]); ins.push_back(mul->src[1]); outs.push_back(mul);
-    }
-    // the projections that will read the chain's activation in the consuming launch (those
-    // sharing src1 with mm, of its type and K): a chain output read by nothing else is never
-    // stored (dead_after), so it may share memory with the chain's inputs
-    std::vector<const ggml_tensor *> readers;
-    const int pm = node_index(g, mm);
-    for (int k = pm; k < n && k <= pm + 12; ++k) {
-        const ggml_tensor * c = ggml_graph_node(g, k);
-        if (c->op == GGML_OP_MUL_MAT && c->src[1] == last && c->src[0]->type == mm->src[0]->type &&
-            c->src[0]->ne[0] == K && gemv_supported(c)) readers.push_back(c);
-    }
-    bool need_norm = false, need_mul = false;
-    // an in-place ADD (its output over one of its inputs) is stored by the next launch
-    bool add_later = false;
-    for (const ggml_tensor * o : outs) {
-        for (const ggml_tensor * in : ins) {
-            if (!overlaps(o, in)) continue;
-            const bool allow = mode != 4 && !(mode == 5 && mm->src[0]->ne[1] != 4096) && !(mode == 6 && mm->src[0]->ne[1] == 4096);
-            if (allow && o == add && (in == add->src[0] || in == add->src[1]) && o->data == in->data) {
-                add_later = true;
-                continue;
-            }
-            if (o == norm && mul && dead_after(g, n, node_index(g, norm) + 1, norm, {mul})) { need_norm = true; continue; }
-            if (o == last && dead_after(g, n, node_index(g, last) + 1, last, readers)) {
-                if (o == norm) need_norm = true; else need_mul = true;
-                continue;
-            }
-            return false;
-        }
-    }
-    for (const ggml_tensor * in : ins) {
-        if (((uintptr_t) in->data) % 16 != 0) return false;
-    }
-    ctx.pend.kind = kind;
-    ctx.pend.add = add; ctx.pend.norm = norm; ctx.pend.mul = mul;
-    ctx.pend.consumer = mm;
-    ctx.pend.add_later = add_later;
-    ctx.pend.need_elide_norm = need_norm;
-    ctx.pend.need_elide_mul = need_mul;
-    return true;
-}
 
 // decode mat-vec: launch node i together with up to two later MUL_MATs on the same src1
 // (Q/K/V, gate/up) in one grouped kernel, with fused epilogues: the SiLU that follows a
@@ -465,8 +387,8 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
         if (c->src[0]->ne[0] != mm0->src[0]->ne[0]) continue;
         if (c->src[0]->type != mm0->src[0]->type) {
             // a second K-quant type (V beside Q/K) joins as the launch's second body, one type
-            // besides mm0's at most, and not under an activation prologue (16-wave workgroups)
-            bool ok = gemv_mixed_ok(mm0, c) && !(ctx.pend.kind && ctx.pend.consumer == mm0);
+            // besides mm0's at most
+            bool ok = gemv_mixed_ok(mm0, c);
             for (int m = 1; m < nm; ++m) {
                 const ggml_type tm = mms[m]->src[0]->type;
                 ok = ok && (tm == mm0->src[0]->type || tm == c->src[0]->type);
@@ -499,69 +421,9 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
         settle(nm, j);
         ++nm;
     }
-    ggml_tensor * add_later = nullptr;
-    if (ctx.pend.kind && ctx.pend.consumer == mm0) {
-        const auto pd = ctx.pend;
-        ctx.pend = exec_ctx::pending_pro();
-        // every workgroup reads the prologue inputs while the launch writes its outputs, and a
-        // deferred ADD reads them after the launch: no output of the launch may overlap them
-        // (ggml-alloc re-uses the memory of inputs whose last consumer, in graph order, ran)
-        std::vector<const ggml_tensor *> pins;
-        if (pd.kind == 1) {
-            if (pd.add) { pins.push_back(pd.add->src[0]); pins.push_back(pd.add->src[1]); }
-            else pins.push_back(pd.norm->src[0]);
-            if (pd.mul) pins.push_back(pd.mul->src[1]);
-        } else {
-            pins.push_back(pd.mul->src[0]); pins.push_back(pd.mul->src[1]);
-        }
-        bool clash = false;
-        for (const ggml_tensor * o : outs) {
-            for (const ggml_tensor * in : pins) {
-                if (overlaps(o, in)) {
-                    clash = true;
-                    static const bool dbgc = getenv("GGML_MI355X_DEBUG_FUSE") != nullptr;
-                    if (dbgc) fprintf(stderr, "[mi355x] prologue of %s: output %s overlaps input %s\n", mm0->name, o->name, in->name);
-                }
-            }
-        }
-        if (!clash) {
-            epi.pro = pd.kind;
-            epi.pro_add = pd.add; epi.pro_norm = pd.norm; epi.pro_mul = pd.mul;
-            epi.pro_add_later = pd.add_later;
-            if (pd.add_later) add_later = pd.add;
-            // the chain's intermediates: the norm output is read by the MUL only, the
-            // activation by this launch's projections only (from the prologue's registers)
-            std::vector<const ggml_tensor *> users = absorbed;
-            users.push_back(mm0);
-            if (pd.kind == 1) {
-                std::vector<const ggml_tensor *> nu = pd.mul ? std::vector<const ggml_tensor *>{pd.mul} : users;
-                epi.elide_norm = dead_after(g, n, node_index(g, pd.norm) + 1, pd.norm, nu);
-            }
-            if (pd.mul) epi.elide_mul = dead_after(g, n, node_index(g, pd.mul) + 1, pd.mul, users);
-            // the deferral counted on outputs that the actual group cannot elide: run the
-            // chain on its own (its kernels are in-place safe)
-            if ((pd.need_elide_norm && !epi.elide_norm) || (pd.need_elide_mul && !epi.elide_mul)) {
-                clash = true;
-                epi.pro = 0; epi.pro_add = epi.pro_norm = epi.pro_mul = nullptr;
-                epi.pro_add_later = false; epi.elide_norm = epi.elide_mul = false;
-                add_later = nullptr;
-            }
-        }
-        if (clash) {
-            if (pd.kind == 1) {
-                if (!fused_norm(ctx, pd.add, pd.norm, pd.mul, mm0)) {
-                    if (pd.add) op_binary(ctx, pd.add);
-                    op_rms_norm(ctx, pd.norm, pd.mul ? pd.mul->src[1] : nullptr, pd.mul);
-                }
-            } else if (!fused_mul_quant(ctx, pd.mul, mm0)) {
-                op_binary(ctx, pd.mul);
-            }
-        }
-    }
     static const bool dbg = getenv("GGML_MI355X_DEBUG_FUSE") != nullptr;
     if (dbg) {
-        fprintf(stderr, "[mi355x] gemv @%d %s: nmat=%d pro=%d elide_norm=%d elide_mul=%d", i, mm0->name, nm, epi.pro,
-                epi.elide_norm, epi.elide_mul);
+        fprintf(stderr, "[mi355x] gemv @%d %s: nmat=%d", i, mm0->name, nm);
         for (int m = 0; m < nm; ++m) {
             fprintf(stderr, " | %s silu=%d rope=%d rope_f16=%d f16=%d elide=%d/%d", mms[m]->name, epi.silu[m] != nullptr,
                     epi.rope[m] != nullptr, epi.rope_f16[m] != nullptr, epi.f16out[m] != nullptr, epi.elide_dst[m], epi.elide_rope[m]);
@@ -569,7 +431,6 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
         fprintf(stderr, "\n");
     }
     gemv_group(ctx, mms, nm, &epi);
-    if (add_later) ctx.post_add = add_later;
     // node i+1 when it is node i's SiLU is consumed here; everything else is skipped later
     const bool next_absorbed = epi.silu[0] && epi.silu[0] == at(g, i + 1, n);
     for (const ggml_tensor * t : absorbed) {
@@ -726,24 +587,6 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             ctx.silu_defer = ctx.silu_mul = nullptr;
         }
     }
-    if (ctx.pend.kind && ctx.pend.consumer != node) {
-        // the deferred producer chain must run before anything else: do it stand-alone
-        const auto pd = ctx.pend;
-        ctx.pend = exec_ctx::pending_pro();
-        if (pd.kind == 1) {
-            if (!fused_norm(ctx, pd.add, pd.norm, pd.mul, nullptr)) {
-                if (pd.add) op_binary(ctx, pd.add);
-                op_rms_norm(ctx, pd.norm, pd.mul ? pd.mul->src[1] : nullptr, pd.mul);
-            }
-        } else if (!fused_mul_quant(ctx, pd.mul, nullptr)) {
-            op_binary(ctx, pd.mul);
-        }
-    }
-    if (ctx.post_add && !(node->op == GGML_OP_MUL_MAT && fusion_enabled() && gemv_supported(node) &&
-                          std::find(ctx.done.begin(), ctx.done.end(), node) == ctx.done.end())) {
-        op_binary(ctx, ctx.post_add);   // its inputs are untouched so far: store it now
-        ctx.post_add = nullptr;
-    }
     if (ggml_is_empty(node)) return 1;
     if (!ctx.done.empty()) {
         auto it = std::find(ctx.done.begin(), ctx.done.end(), node);
@@ -773,9 +616,6 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             // src/llama-graph.cpp:464-497); the norm output is still written, so other
             // readers of it stay correct.
             ggml_tensor * mul = norm_weight_mul(cgraph, i, n);
-            if (fusion_enabled() && defer_to_prologue(ctx, cgraph, n, 1, nullptr, node, mul, at(cgraph, i + (mul ? 2 : 1), n))) {
-                return mul ? 2 : 1;
-            }
             if (fusion_enabled()) {
                 ggml_tensor * mm = at(cgraph, i + (mul ? 2 : 1), n);
                 bool sn, sm;
@@ -797,7 +637,6 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                 if (nx && nx->op == GGML_OP_RMS_NORM && nx->src[0] == node) {
                     ggml_tensor * mul = norm_weight_mul(cgraph, i + 1, n);
                     const int used = mul ? 3 : 2;
-                    if (defer_to_prologue(ctx, cgraph, n, 1, node, nx, mul, at(cgraph, i + used, n))) return used;
                     ggml_tensor * mm = at(cgraph, i + used, n);
                     bool sn, sm;
                     norm_stores(cgraph, n, nx, mul, mm, sn, sm);
@@ -823,7 +662,6 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             if (fusion_enabled() && try_moe_combine(ctx, cgraph, i, n)) return 1;
             // gated-FFN product feeding the down projection: multiply + quantize in one pass
             if (fusion_enabled()) {
-                if (defer_to_prologue(ctx, cgraph, n, 2, nullptr, nullptr, node, at(cgraph, i + 1, n))) return 1;
                 if (fused_mul_quant(ctx, node, at(cgraph, i + 1, n))) return 1;
             }
             op_binary(ctx, node);

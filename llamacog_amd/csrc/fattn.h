@@ -26,9 +26,6 @@ struct fa_args {
     int * cnt;
     // microbenchmark hook: per-phase s_memtime cycles of workgroup (0,0) (nullable)
     unsigned long long * prof;
-    // exact kernel: blockIdx.y >= warm_y0 are Infinity-Cache warm workgroups (warm.h)
-    int64_t warm_y0;
-    warm_spec warm;
 };
 
 // set by mi355x_bench_op (capi.cpp) only; copied into fa_args.prof

@@ -341,23 +341,32 @@ __global__ __launch_bounds__(256) void k_rms_norm(const char * __restrict__ x, t
     const float * xr = (const float *) (x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3]);
     float * yr = (float *) (y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
     const int64_t ne0 = tx.ne[0];
-    double sum = 0.0;
-    if (tx.nb[0] == 4 && ne0 % 256 == 0 && ((uintptr_t) xr) % 16 == 0) {
-        // the canonical partition shared with the fused kernels (quant_act.h norm_sumsq)
-        sum = norm_sumsq(xr, nullptr, ne0, threadIdx.x & 63);
-    } else {
-        for (int64_t i = threadIdx.x; i < ne0; i += 256) {
-            const float v = xr[i];
-            sum += (double) (v * v);
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, WAVE);
-        __shared__ double part[4];
-        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
-        __syncthreads();
-        sum = part[0] + part[1] + part[2] + part[3];
+    // the CPU's sequential double sum, decided from a double-double sum (quant_act.h)
+    ddv acc = {0.0, 0.0};
+    for (int64_t i = threadIdx.x; i < ne0; i += 256) {
+        const float v = *(const float *) ((const char *) xr + i * tx.nb[0]);
+        acc = dd_add(acc, (double) __fmul_rn(v, v));
     }
-    const float mean = (float) (sum / (double) ne0);
+    acc = dd_wave_sum(acc);
+    __shared__ ddv part[4];
+    __shared__ float smean;
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const ddv s = dd_add(dd_add(part[0], part[1]), dd_add(part[2], part[3]));
+        float m;
+        if (!rms_mean_decided(s, ne0, m)) {
+            double q = 0.0;
+            for (int64_t i = 0; i < ne0; ++i) {
+                const float v = *(const float *) ((const char *) xr + i * tx.nb[0]);
+                q = __dadd_rn(q, (double) __fmul_rn(v, v));
+            }
+            m = (float) __ddiv_rn(q, (double) ne0);
+        }
+        smean = m;
+    }
+    __syncthreads();
+    const float mean = smean;
     const float scale = 1.0f / sqrtf(mean + eps);
     if (y2) {
         // fused norm-weight MUL: the norm output is still stored (other readers stay
@@ -371,7 +380,7 @@ __global__ __launch_bounds__(256) void k_rms_norm(const char * __restrict__ x, t
             y2r[i] = __fmul_rn(v, *(const float *) (wr + (i % nw) * tw.nb[0]));
         }
     } else {
-        for (int64_t i = threadIdx.x; i < ne0; i += 256) yr[i] = xr[i] * scale;
+        for (int64_t i = threadIdx.x; i < ne0; i += 256) yr[i] = __fmul_rn(*(const float *) ((const char *) xr + i * tx.nb[0]), scale);
     }
 }
 

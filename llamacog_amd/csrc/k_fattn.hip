@@ -272,7 +272,6 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     a.part = nullptr;
     a.qmode = 0;
     a.prof = g_fa_prof;
-    a.warm.nseg = 0; a.warm.nwg = 0; a.warm_y0 = 0;
     a.qs = nullptr; a.qd = nullptr; a.qsum = nullptr;
     if (nchunks > 1) a.part = (float *) ctx.scratch(1, sizeof(float) * nchunks * rows * (a.D + 2));
 
@@ -301,7 +300,6 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
                 a.cnt = ctx.fa_cnt;
             }
         }
-        if (a.n_q == 1 && nq3 == 1) a.warm = ctx.warm_take(WARM_FA);   // decode: warm the next weights
         launch_fattn_exact(ctx.stream, a, nq3);
         if (a.qmode) ctx.qcache_put(mm->src[1], a.qmode == 1, act);
         if (ctx.timing) ctx.time_end(TK_FATTN, bytes, ev);

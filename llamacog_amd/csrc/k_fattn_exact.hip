@@ -137,10 +137,6 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
     __shared__ uint32_t wflag[4];    // per wave: batches needing the general step (mask / max update)
     __shared__ int wlast[4];
     __shared__ float wmax[4];
-    if (blockIdx.y >= a.warm_y0) {   // a warm workgroup: stream the next weights during attention
-        warm_run(a.warm, (int) ((blockIdx.y - a.warm_y0) * gridDim.x + blockIdx.x), (uint8_t *) vl, 4);
-        return;
-    }
 
     // q of this head, f16-rounded, in the quad layout of dot_f16_avx512_q4
     float qf[NM][4];
@@ -417,10 +413,7 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
 void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     GGML_ASSERT(a0.H % a0.Hkv == 0);
     fa_args a = a0;
-    a.warm_y0 = a.H * nq3;
-    const int64_t wy = a.warm.nwg ? ceil_div(a.warm.nwg, a.n_q) : 0;
-    a.warm.nwg = (int) (wy * a.n_q);
-    const dim3 grid((unsigned) a.n_q, (unsigned) (a.H * nq3 + wy));
+    const dim3 grid((unsigned) a.n_q, (unsigned) (a.H * nq3));
     static const int pocc = getenv("GGML_MI355X_FA_PREFILL_OCC") ? atoi(getenv("GGML_MI355X_FA_PREFILL_OCC")) : 2;
     // prefill chunk: GGML_MI355X_FA_PREFILL_CH = 128 (default: 32 KiB of V in LDS; half the
     // phase-1 K registers, so OCC 2 fits 256 VGPRs without the 40 spills of CH 256 — pp512

@@ -8,10 +8,10 @@
 //                                                 build_norm; residual ADDs :llama.cpp build)
 //   MUL (silu(gate) * up) -> (MUL_MAT down)       k_mul_quant    (build_ffn LLM_FFN_PAR)
 //
-// Arithmetic: ADD/MUL are single f32 ops; RMS_NORM sums float(x*x) in double
-// (ops.cpp:3270-3316; the canonical partition of quant_act.h norm_sumsq), scale =
-// 1/sqrtf(float(sum/ne0)+eps), y = x*scale; quantizers are quant_act.h's (bit-exact with the
-// CPU's).  All run with rows in registers.
+// Arithmetic: ADD/MUL are single f32 ops; RMS_NORM's mean is the CPU's sequential double sum
+// of float(x*x) (ops.cpp:3270-3316, quant_act.h rms_mean_decided), scale =
+// 1/sqrtf(mean+eps), y = x*scale; quantizers are quant_act.h's (bit-exact with the CPU's).
+// All run with rows in registers.
 #include "ops.h"
 #include "quant_act.h"
 
@@ -27,32 +27,26 @@ struct norm_fused_args {
     int qmode;                          // 0 none, 1 Q8_K, 2 Q8_0 (of yw if w else y)
     int8_t * qs; float * qd; int16_t * qsum;
     int64_t nrows;
-    warm_spec warm;                     // Infinity-Cache warm of the next weights (warm.h)
 };
 
-// one workgroup of BT = min(ne0/4, 1024) threads per row; thread t owns the float4s at
-// element 4 (t + BT k), k < NV, so wave w's 256 elements of slice k are the canonical
-// partition's j = w + (BT/64) k (quant_act.h norm_sumsq) and one Q8_K block / eight Q8_0
-// blocks of the quantized output.  The sum of squares is formed once per row: every thread
-// writes its (j, l) partials to LDS, wave 0 adds them in j order and butterflies.
+// one workgroup of BT threads per row; thread t owns the float4s at element 4 (t + BT k), k < NV,
+// so wave w's 256 elements of slice k are one Q8_K block / eight Q8_0 blocks of the quantized
+// output.  The mean is the CPU's sequential one (quant_act.h rms_mean_decided).
 template <int NV>
 __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int BT = blockDim.x, NW = BT >> 6;
     const int64_t row = blockIdx.x;
     const int64_t ro = row * p.ne0;
-    __shared__ double qp[NV * 16][64];
-    __shared__ double tot;
-    if (row >= p.nrows) {   // a warm workgroup: stream the next weights while the rows reduce
-        warm_run(p.warm, (int) (row - p.nrows), (uint8_t *) qp, 8 * NV);
-        return;
-    }
+    __shared__ ddv wpart[16];
+    __shared__ float smean;
     float4 v[NV], wv[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         // the norm weight is loaded with the row, not after the reduction
         if (p.w) wv[k] = *(const float4 *) (p.w + 4 * (tid + BT * k));
     }
+    ddv acc = {0.0, 0.0};
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int64_t e = 4 * (tid + BT * k);
@@ -62,25 +56,26 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
             v[k].x = __fadd_rn(v[k].x, bb.x); v[k].y = __fadd_rn(v[k].y, bb.y);
             v[k].z = __fadd_rn(v[k].z, bb.z); v[k].w = __fadd_rn(v[k].w, bb.w);
         }
-        qp[wave + NW * k][lane] = norm_q4(v[k]);
+        acc = dd_sq4(acc, v[k]);
     }
-    // each thread stores only elements it has itself read: in-place ADD output is safe
+    acc = dd_wave_sum(acc);
+    if (lane == 0) wpart[wave] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        ddv s = wpart[0];
+        for (int w = 1; w < NW; ++w) s = dd_add(s, wpart[w]);
+        float mean;
+        if (!rms_mean_decided(s, p.ne0, mean)) mean = rms_mean_sequential(p.a + ro, p.b ? p.b + ro : nullptr, p.ne0);
+        smean = mean;
+    }
+    __syncthreads();
+    // the ADD output is stored only now: the sequential replay above reads a and b, and the
+    // ADD may be in place over one of them
     if (p.xsum) {
 #pragma unroll
         for (int k = 0; k < NV; ++k) *(float4 *) (p.xsum + ro + 4 * (tid + BT * k)) = v[k];
     }
-    __syncthreads();
-    if (wave == 0) {
-        double s = 0.0;
-        const int nj = NW * NV;
-        for (int jj = 0; jj < nj; ++jj) s += qp[jj][lane];
-        s = wave_sum(s);
-        if (lane == 0) tot = s;
-    }
-    __syncthreads();
-    const double sum = tot;
-    const float mean = (float) (sum / (double) p.ne0);
-    const float scale = 1.0f / sqrtf(mean + p.eps);
+    const float scale = 1.0f / sqrtf(smean + p.eps);
 
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -115,16 +110,10 @@ template <int QMODE, bool SILU>
 __global__ __launch_bounds__(64) void k_mul_quant(const float * __restrict__ a, const float * __restrict__ b,
                                                   float * __restrict__ dst, int64_t K,
                                                   int8_t * __restrict__ qs, float * __restrict__ qd,
-                                                  int16_t * __restrict__ qsum, float * __restrict__ sdst,
-                                                  const warm_spec warm) {
+                                                  int16_t * __restrict__ qsum, float * __restrict__ sdst) {
     const int lane = threadIdx.x;
     const int64_t row = blockIdx.y;
     const int64_t nblk = (K + 255) / 256;
-    if (blockIdx.x >= nblk) {   // a warm workgroup (decode): stream the down projection's weights
-        __shared__ __attribute__((aligned(16))) uint8_t wl[1024];
-        warm_run(warm, (int) (blockIdx.x - nblk), wl, 1);
-        return;
-    }
     const int64_t c0 = (int64_t) blockIdx.x * 256;
     const int64_t e0 = c0 + 4 * lane;
     const bool valid = e0 < K;
@@ -215,9 +204,7 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     if ((nbt == 256 || nbt == 512) && ne0 % (4 * nbt) == 0 && ne0 / (4 * nbt) <= 4) nv = (int) (ne0 / (4 * nbt));
     const dim3 block((unsigned) (ne0 / (4 * nv)));
     p.nrows = nrows;
-    p.warm.nseg = 0; p.warm.nwg = 0;
-    if (nrows == 1 && block.x >= 256) p.warm = ctx.warm_take(WARM_NORM);   // decode only
-    const dim3 grid((unsigned) (nrows + p.warm.nwg));
+    const dim3 grid((unsigned) nrows);
     switch (nv) {
         case 1: hipLaunchKernelGGL(k_norm_fused<1>, grid, block, 0, ctx.stream, p); break;
         case 2: hipLaunchKernelGGL(k_norm_fused<2>, grid, block, 0, ctx.stream, p); break;
@@ -247,15 +234,12 @@ bool fused_silu_mul_quant(exec_ctx & ctx, ggml_tensor * silu, ggml_tensor * mul,
     const bool kq = qmode == 1;
     q8_act act = {};
     if (qmode) carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(K, nrows, kq)), K, nrows, kq);
-    warm_spec warm;
-    warm.nseg = 0; warm.nwg = 0;
-    if (nrows == 1) warm = ctx.warm_take(WARM_MULQ);
-    const dim3 grid((unsigned) (ceil_div(K, 256) + warm.nwg), (unsigned) nrows);
+    const dim3 grid((unsigned) ceil_div(K, 256), (unsigned) nrows);
     const float * a = (const float *) (silu ? silu->src[0]->data : mul->src[0]->data);
     const float * b = (const float *) mul->src[1]->data;
     float * d = store_mul ? (float *) mul->data : nullptr;
     float * sd = silu && store_silu ? (float *) silu->data : nullptr;
-#define MQ_LAUNCH(Q, S) hipLaunchKernelGGL((k_mul_quant<Q, S>), grid, dim3(64), 0, ctx.stream, a, b, d, K, act.qs, act.d, act.s, sd, warm)
+#define MQ_LAUNCH(Q, S) hipLaunchKernelGGL((k_mul_quant<Q, S>), grid, dim3(64), 0, ctx.stream, a, b, d, K, act.qs, act.d, act.s, sd)
     if (silu) {
         if (qmode == 1) MQ_LAUNCH(1, true); else if (qmode == 2) MQ_LAUNCH(2, true); else MQ_LAUNCH(0, true);
     } else {

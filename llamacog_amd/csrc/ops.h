@@ -4,7 +4,6 @@
 #pragma once
 
 #include "common.h"
-#include "warm.h"
 
 #include <vector>
 
@@ -35,6 +34,9 @@ struct exec_ctx {
     void *  slot_ptr[N_SLOTS]  = {nullptr, nullptr, nullptr, nullptr};
     size_t  slot_size[N_SLOTS] = {0, 0, 0, 0};
     bool    capturing = false;   // hipGraph capture in progress: growing is forbidden
+    // bumped whenever a slot is reallocated: a captured hipGraph holds slot addresses in its
+    // kernel arguments, so graphs captured under an older generation are dropped (backend.cpp)
+    uint64_t scratch_gen = 0;
 
     // arrival counters of the flash-attention output quantization (k_fattn_exact.hip)
     static constexpr int FA_CNT = 1024;
@@ -62,35 +64,14 @@ struct exec_ctx {
     const void *    rt_ff = nullptr;
     int32_t         rt_params[15] = {};
 
-    // Infinity-Cache warming (warm.h): the decode mat-vec weights of the current graph in
-    // node order and the cursor up to which latency-bound kernels have already warmed them
-    struct warm_seg { int node; const uint8_t * p; int64_t n; };
-    std::vector<warm_seg> warm_list;
-    size_t  warm_cur = 0;
-    int64_t warm_off = 0;
-    int     cur_node = 0;              // graph position being dispatched (run_nodes)
-    void      warm_plan(ggml_cgraph * g);   // backend.cpp
-    warm_spec warm_take(int kind);          // the next bytes after cur_node for a kernel of `kind`
 
     // nodes already computed ahead of their position by a grouped launch (dispatch.cpp)
     std::vector<const ggml_tensor *> done;
 
-    // producer nodes deferred into the prologue of the next MUL_MAT's GEMV (dispatch.cpp)
-    struct pending_pro {
-        int kind = 0;                      // 0 none, 1 norm chain, 2 FFN product
-        ggml_tensor * add = nullptr; ggml_tensor * norm = nullptr; ggml_tensor * mul = nullptr;
-        const ggml_tensor * consumer = nullptr;
-        bool add_later = false;            // the ADD is in place: store it in the next launch
-        bool need_elide_norm = false;      // deferral valid only if the launch elides these
-        bool need_elide_mul = false;
-    } pend;
     // a SILU whose MUL partner's other input (the up projection) is computed after it (MoE:
     // gate, SILU, up, MUL): run as one silu*mul kernel at the MUL (dispatch.cpp)
     ggml_tensor * silu_defer = nullptr;
     ggml_tensor * silu_mul = nullptr;
-    // an in-place residual ADD whose inputs the previous GEMV prologue read: the next GEMV
-    // launch stores it (workgroup 0), before any node can read it
-    ggml_tensor * post_add = nullptr;
 
     // Dynamic destinations: a KV-cache store (CPY into a view at offset n_past) changes its
     // destination every token while the rest of the graph stays identical.  Kernels read
@@ -100,6 +81,11 @@ struct exec_ctx {
     std::vector<void *>              dyn_host;    // their destination pointers
     void **                          dyn_dev = nullptr;
     size_t                           dyn_cap = 0;
+    // pinned staging of the table upload, double-buffered: buffer k is rewritten only after
+    // the copy that last read it has completed (dyn_ev[k])
+    void **                          dyn_pin[2] = {nullptr, nullptr};
+    hipEvent_t                       dyn_ev[2] = {nullptr, nullptr};
+    int                              dyn_flip = 0;
     bool prepare_dyn(ggml_cgraph * g);            // scan + upload; false = table too small (backend.cpp)
     void * const * dyn_slot(const ggml_tensor * cpy) const {
         for (size_t k = 0; k < dyn_nodes.size(); ++k) {
@@ -181,16 +167,9 @@ struct gemv_epi {
     // overwritten): not stored
     bool elide_dst[3]  = {false, false, false};   // the projection itself
     bool elide_rope[3] = {false, false, false};   // its rope (kept only as the f16 cache row)
-    bool elide_norm = false, elide_mul = false;   // prologue RMS_NORM / MUL outputs
-    // activation prologue (k_gemv.hip prologue_act): 1 = [ADD] -> RMS_NORM -> [MUL w],
-    // 2 = MUL (gated-FFN product); the launch also writes these nodes' outputs
-    int pro = 0;
-    ggml_tensor * pro_add = nullptr; ggml_tensor * pro_norm = nullptr; ggml_tensor * pro_mul = nullptr;
-    bool pro_add_later = false;      // compute the ADD for the norm but do not store it
 };
 bool gemv_supported(const ggml_tensor * mm);
 bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
-bool gemv_prologue_ok(const ggml_tensor * mm);   // the consumer can run an activation prologue
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi);
 bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c);   // c may join mm0's launch as a second weight type
 

@@ -82,45 +82,57 @@ __device__ __forceinline__ void q8_0_wave(const float (&vv)[4], int lane, bool v
     }
 }
 
-// canonical RMS-norm sum of squares of x = a (+ b) [K] (K % 256 == 0), as every wave, the
-// stand-alone norm kernel and the fused norm kernel (k_fused.hip) compute it:
-//   q(j, l) = ((x[e]^2 + x[e+1]^2) + x[e+2]^2) + x[e+3]^2 in double, e = 256 j + 4 l
-//   s(l)    = q(0, l) + q(1, l) + ... in j order          (lane l of a wave)
-//   sum     = xor-butterfly of wave_sum over the 64 s(l)
-// Each float4 load of a wave covers 1 KiB of contiguous memory, and the (j, l) partials
-// can be formed by any thread holding that float4 (norm_q4), so a workgroup computes the
-// same value cooperatively.
-__device__ __forceinline__ double norm_q4(const float4 x) {
-    double q = (double) __fmul_rn(x.x, x.x);
-    q += (double) __fmul_rn(x.y, x.y);
-    q += (double) __fmul_rn(x.z, x.z);
-    q += (double) __fmul_rn(x.w, x.w);
-    return q;
+// ---- RMS-norm mean, exactly as the CPU forms it -----------------------------------------------
+// rms_norm_f32 (ggml-cpu/ops.cpp:3270-3316) sums (double)(x*x) over the row SEQUENTIALLY in
+// double, then mean = (float)(sum / ne0).  A parallel sum rounds differently, and on rare rows
+// that difference flips the float mean.  Here every thread sums its terms in double-double
+// (error ~2^-106 of the sum), the partials are combined the same way, and the float mean is
+// taken from that near-exact sum when the rounding is decided: the sequential double sum of n
+// non-negative terms lies within (n-1)·2^-53 of the exact one (relative), so when both ends of
+// [m(1 - tol), m(1 + tol)] round to the same float the CPU's mean is that float.  Otherwise (a
+// fraction ~1e-5 of rows) one thread replays the CPU's sequential loop.
+struct ddv { double hi, lo; };
+
+__device__ __forceinline__ ddv dd_add(ddv a, double b) {   // a + b (TwoSum, then renormalise)
+    const double s = __dadd_rn(a.hi, b);
+    const double bb = __dsub_rn(s, a.hi);
+    const double e = __dadd_rn(__dsub_rn(a.hi, __dsub_rn(s, bb)), __dsub_rn(b, bb));
+    const double lo = __dadd_rn(a.lo, e);
+    const double hi = __dadd_rn(s, lo);
+    return ddv{hi, __dsub_rn(lo, __dsub_rn(hi, s))};
+}
+__device__ __forceinline__ ddv dd_add(ddv a, ddv b) { return dd_add(dd_add(a, b.hi), b.lo); }
+
+__device__ __forceinline__ ddv dd_wave_sum(ddv v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = dd_add(v, ddv{__shfl_xor(v.hi, o, WAVE), __shfl_xor(v.lo, o, WAVE)});
+    return v;
 }
 
-__device__ __forceinline__ double norm_sumsq(const float * a, const float * b, int64_t K, int lane) {
-    const int64_t n = K / 256;
+__device__ __forceinline__ ddv dd_sq4(ddv acc, const float4 x) {   // + the four terms (double)(x*x)
+    acc = dd_add(acc, (double) __fmul_rn(x.x, x.x));
+    acc = dd_add(acc, (double) __fmul_rn(x.y, x.y));
+    acc = dd_add(acc, (double) __fmul_rn(x.z, x.z));
+    return dd_add(acc, (double) __fmul_rn(x.w, x.w));
+}
+
+// the float mean from the near-exact sum; false when the rounding is not decided
+__device__ __forceinline__ bool rms_mean_decided(ddv s, int64_t n, float & mean) {
+    const double m = __ddiv_rn(__dadd_rn(s.hi, s.lo), (double) n);
+    const double tol = (double) (n + 8) * 0x1p-53;
+    const float f0 = (float) __dmul_rn(m, 1.0 - tol), f1 = (float) __dmul_rn(m, 1.0 + tol);
+    mean = (float) m;
+    return f0 == f1;
+}
+
+// the CPU's own loop: x = a (+ b) elementwise, sum += (double)(x*x) in order
+__device__ __noinline__ float rms_mean_sequential(const float * a, const float * b, int64_t n) {
     double s = 0.0;
-    // batches of 8 float4 loads in flight
-    for (int64_t j0 = 0; j0 < n; j0 += 8) {
-        float4 x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int64_t e = 256 * min(j0 + u, n - 1) + 4 * lane;
-            x[u] = *(const float4 *) (a + e);
-            if (b) {
-                const float4 y = *(const float4 *) (b + e);
-                x[u].x = __fadd_rn(x[u].x, y.x); x[u].y = __fadd_rn(x[u].y, y.y);
-                x[u].z = __fadd_rn(x[u].z, y.z); x[u].w = __fadd_rn(x[u].w, y.w);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            if (j0 + u >= n) break;
-            s += norm_q4(x[u]);
-        }
+    for (int64_t i = 0; i < n; ++i) {
+        const float x = b ? __fadd_rn(a[i], b[i]) : a[i];
+        s = __dadd_rn(s, (double) __fmul_rn(x, x));
     }
-    return wave_sum(s);
+    return (float) __ddiv_rn(s, (double) n);
 }
 
 }  // namespace mi355x

@@ -27,9 +27,9 @@ __device__ __forceinline__ void rope_yarn_dev(float theta_extrap, float freq_sca
         theta = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
         mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
     }
-    // libm cosf/sinf of the CPU backend: take them in double and round once
-    c = __fmul_rn((float) cos((double) theta), mscale);
-    s = __fmul_rn((float) sin((double) theta), mscale);
+    // glibc cosf / sinf of the CPU backend, restated bit for bit (libm_exact.h)
+    c = __fmul_rn(lx_cosf(theta), mscale);
+    s = __fmul_rn(lx_sinf(theta), mscale);
 }
 
 // cos/sin of pair ip (dims 2ip, 2ip+1) at position p

@@ -121,6 +121,48 @@ void gg_mul_mat_id(int type, const void * As, int64_t K, int64_t M, int64_t n_as
     ggml_free(ctx);
 }
 
+/* mul_mat_id as libllama runs it: the expert stack in the CPU device's first extra buffer type
+ * (CPU_REPACK: Q4_K / Q4_0 stacks with M % 8 == 0 take repack.cpp forward_mul_mat_id, one gemv
+ * per routed pair, repack.cpp:1277-1405) when use_extra is set; graph computed by
+ * ggml_backend_graph_compute */
+int gg_mul_mat_id_backend(int type, const void * As, int64_t K, int64_t M, int64_t n_as, const int32_t * ids,
+                          int64_t n_used, const float * X, int64_t ne11, int64_t T, float * Y, int nth, int use_extra) {
+    ggml_backend_t be = ggml_backend_cpu_init();
+    ggml_backend_cpu_set_n_threads(be, nth);
+    ggml_backend_dev_t dev = ggml_backend_get_device(be);
+    ggml_backend_reg_t reg = ggml_backend_dev_backend_reg(dev);
+    ggml_backend_buffer_type_t wbuft = ggml_backend_get_default_buffer_type(be);
+    if (use_extra) {
+        ggml_backend_dev_get_extra_bufts_t get = (ggml_backend_dev_get_extra_bufts_t)
+            ggml_backend_reg_get_proc_address(reg, "ggml_backend_dev_get_extra_bufts");
+        ggml_backend_buffer_type_t * ex = get ? get(dev) : NULL;
+        if (!ex || !ex[0]) { ggml_backend_free(be); return -1; }
+        wbuft = ex[0];
+    }
+    struct ggml_init_params ip = {ggml_tensor_overhead() * 8 + ggml_graph_overhead(), NULL, true};
+    struct ggml_context * cw = ggml_init(ip);
+    struct ggml_context * cx = ggml_init(ip);
+    struct ggml_tensor * as = ggml_new_tensor_3d(cw, (enum ggml_type) type, K, M, n_as);
+    struct ggml_tensor * id = ggml_new_tensor_2d(cx, GGML_TYPE_I32, n_used, T);
+    struct ggml_tensor * x = ggml_new_tensor_3d(cx, GGML_TYPE_F32, K, ne11, T);
+    struct ggml_tensor * y = ggml_mul_mat_id(cx, as, x, id);
+    ggml_backend_buffer_t bw = ggml_backend_alloc_ctx_tensors_from_buft(cw, wbuft);
+    ggml_backend_buffer_t bx = ggml_backend_alloc_ctx_tensors_from_buft(cx, ggml_backend_get_default_buffer_type(be));
+    ggml_backend_tensor_set(as, As, 0, ggml_nbytes(as));
+    ggml_backend_tensor_set(id, ids, 0, ggml_nbytes(id));
+    ggml_backend_tensor_set(x, X, 0, ggml_nbytes(x));
+    struct ggml_cgraph * gf = ggml_new_graph(cx);
+    ggml_build_forward_expand(gf, y);
+    const int st = (int) ggml_backend_graph_compute(be, gf);
+    ggml_backend_tensor_get(y, Y, 0, ggml_nbytes(y));
+    ggml_backend_buffer_free(bw);
+    ggml_backend_buffer_free(bx);
+    ggml_free(cw);
+    ggml_free(cx);
+    ggml_backend_free(be);
+    return st;
+}
+
 /* argsort of nrows rows of ne0 floats (order 0 asc, 1 desc) on the CPU backend */
 void gg_argsort(const float * x, int64_t ne0, int64_t nrows, int order, int32_t * out) {
     struct ggml_context * ctx = mk_ctx(16 + (size_t) ((ne0 * nrows * 8) >> 20));

@@ -661,6 +661,22 @@ void orc_mul_mat_id(int type, const void * As, int64_t K, int64_t M, int64_t n_a
     }
 }
 
+/* mul_mat_id in the CPU backend's exact float order as libllama runs it: each routed pair is one
+ * mat-vec (T = 1) of orc_mul_mat_cpu — repacked gemv for Q4_K / Q4_0 stacks with M % 8 == 0
+ * (repack.cpp:1277-1405 forward_mul_mat_id), the vec_dot order otherwise (ggml-cpu.c:1466) */
+void orc_mul_mat_id_cpu(int type, const void * As, int64_t K, int64_t M, int64_t n_as, const int32_t * ids, int64_t ids_row,
+                        int64_t n_used, const float * X, int64_t ne11, int64_t T, float * Y, int repack) {
+    const size_t wmat = (size_t) (K / orc_block_size(type)) * orc_type_size(type) * (size_t) M;
+    for (int64_t t = 0; t < T; ++t) {
+        for (int64_t e = 0; e < n_used; ++e) {
+            const int32_t ex = ids[t * ids_row + e];
+            if (ex < 0 || ex >= n_as) continue;
+            orc_mul_mat_cpu(type, (const char *) As + (size_t) ex * wmat, K, M, X + (t * ne11 + e % ne11) * K, 1,
+                            Y + (t * n_used + e) * M, repack);
+        }
+    }
+}
+
 /* ggml_compute_forward_argsort_f32 (ggml-cpu/ops.cpp:6956-6993): the exchange sort per row;
  * order 0 ascending, 1 descending */
 void orc_argsort(const float * x, int64_t ne0, int64_t nrows, int order, int32_t * dst) {

@@ -55,6 +55,8 @@ def load():
     lib.gg_sum_rows.argtypes = [P, I64, I64, P]
     lib.gg_mul_mat_backend.argtypes = [ctypes.c_int, P, I64, I64, P, I64, P, ctypes.c_int, ctypes.c_int]
     lib.gg_mul_mat_backend.restype = ctypes.c_int
+    lib.gg_mul_mat_id_backend.argtypes = [ctypes.c_int, P, I64, I64, I64, P, I64, P, I64, I64, P, ctypes.c_int, ctypes.c_int]
+    lib.gg_mul_mat_id_backend.restype = ctypes.c_int
     lib.gg_init()
     return lib
 
@@ -180,6 +182,34 @@ def cpu_orders(lib):
     print(f"mul_mat_cpu.npz {os.path.getsize(os.path.join(OUT, 'mul_mat_cpu.npz'))} B")
 
 
+def moe_cpu_orders(lib):
+    """mul_mat_id exactly as libllama runs it on the CPU backend (gg_mul_mat_id_backend with the
+    CPU_REPACK extra buffer): Q4_K / Q4_0 stacks with M % 8 == 0 through forward_mul_mat_id's
+    repacked gemv, the others through the vec_dot order; decode and batched routing."""
+    rng = np.random.default_rng(8642)
+    g = {}
+    n_as, n_used = 4, 2
+    for t, name, M, K in ((Q4_K, "q4_K", 64, 1024), (Q4_K, "q4_K_m60", 60, 512), (Q5_K, "q5_K", 64, 512),
+                          (Q6_K, "q6_K", 32, 1024), (Q8_0, "q8_0", 64, 512), (Q4_0, "q4_0", 64, 512)):
+        w = (rng.standard_normal((n_as * M, K)) * 0.05).astype(np.float32)
+        wq = quantize(lib, t, w)
+        g[f"wq_{name}"] = wq
+        g[f"M_{name}"] = M
+        for T, ne11 in ((1, 1), (1, n_used), (9, 1), (9, n_used)):
+            ids = np.stack([rng.permutation(n_as)[:n_used] for _ in range(T)]).astype(np.int32)
+            x = rng.standard_normal((T, ne11, K)).astype(np.float32)
+            y = np.zeros((T, n_used, M), dtype=np.float32)
+            # libllama only places repackable stacks in CPU_REPACK (its supports_op declines the rest)
+            extra = 1 if t in (Q4_K, Q4_0) and M % 8 == 0 else 0
+            st = lib.gg_mul_mat_id_backend(t, fptr(wq), K, M, n_as, fptr(ids), n_used, fptr(x), ne11, T, fptr(y), 4, extra)
+            assert st == 0, st
+            g[f"ids_{name}_{T}_{ne11}"] = ids
+            g[f"x_{name}_{T}_{ne11}"] = x
+            g[f"y_{name}_{T}_{ne11}"] = y
+    np.savez_compressed(os.path.join(OUT, "moe_cpu.npz"), n_as=n_as, n_used=n_used, **g)
+    print(f"moe_cpu.npz {os.path.getsize(os.path.join(OUT, 'moe_cpu.npz'))} B")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     lib = load()
@@ -187,6 +217,8 @@ def main():
         return moe(lib)
     if "cpu_orders" in sys.argv[1:]:
         return cpu_orders(lib)
+    if "moe_cpu" in sys.argv[1:]:
+        return moe_cpu_orders(lib)
     rng = np.random.default_rng(1234)
 
     # ---- activation quantizers ------------------------------------------------------------
@@ -277,6 +309,7 @@ def main():
     np.savez_compressed(os.path.join(OUT, "flash_attn.npz"), D=D, H=H, Hkv=Hkv, n_kv=n_kv, **fa)
     moe(lib)
     cpu_orders(lib)
+    moe_cpu_orders(lib)
     for f in sorted(os.listdir(OUT)):
         print(f"{f:28s} {os.path.getsize(os.path.join(OUT, f)):9d} B")
 

@@ -47,6 +47,7 @@ def lib():
         L.orc_sum_rows.argtypes = [P, I64, I64, P]
         L.orc_mul_mat_cpu.argtypes = [ctypes.c_int, P, I64, I64, P, I64, P, ctypes.c_int]
         L.orc_block_classes.argtypes = [ctypes.c_int, P, P, P, P]
+        L.orc_mul_mat_id_cpu.argtypes = [ctypes.c_int, P, I64, I64, I64, P, I64, I64, P, I64, I64, P, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -177,6 +178,17 @@ def mul_mat_id(t, wq, K, M, n_as, ids, n_used, x):
     y = np.zeros((T, n_used, M), dtype=np.float32)
     lib().orc_mul_mat_id(t, ptr(np.ascontiguousarray(wq)), K, M, n_as, ptr(ids), ids.shape[1], n_used, ptr(x), ne11, T,
                          ptr(y))
+    return y
+
+
+def mul_mat_id_cpu(t, wq, K, M, n_as, ids, n_used, x, repack=True):
+    """MUL_MAT_ID in the CPU backend's exact float order as libllama runs it (orc_mul_mat_id_cpu)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    T, ne11 = x.shape[0], x.shape[1]
+    y = np.zeros((T, n_used, M), dtype=np.float32)
+    lib().orc_mul_mat_id_cpu(t, ptr(np.ascontiguousarray(wq)), K, M, n_as, ptr(ids), ids.shape[1], n_used, ptr(x), ne11,
+                             T, ptr(y), 1 if repack else 0)
     return y
 
 

@@ -3,12 +3,10 @@
 * test-backend-ops (the reference's per-op harness, tests/test-backend-ops.cpp) run against
   the MI355X device for every op family the plugin supports (NMSE bounds of the reference);
 * greedy decoding of synthetic GGUF models through libllama on MI355X vs the reference CPU
-  backend in the same process: identical token ids (unless the CPU's own top-2 logits are a
-  near tie), logits within the per-test bound of the logit range.  Measured drift is
-  1-3e-2: integer block sums are bit-exact but the fp32 combination order of the mat-vec
-  differs from the CPU's repacked-Q4_K / AVX2 paths, and each layer re-quantizes its input
-  to Q8_K, which amplifies 1e-7 differences (the reference's own AVX2 vs AVX-512 CPU
-  builds differ by ~7e-3 on these models);
+  backend in the same process: identical token ids and BIT-IDENTICAL logits at every step
+  (prompt and generation).  Every kernel on the path reproduces the CPU backend's integer
+  sums and fp32 operation order as libllama runs it (qtypes.h, libm_exact.h, the sequential
+  RMS-norm mean), so there is no tolerance to state;
 * every node of the llama graph (except the embedding GET_ROWS) runs on the MI355X device.
 """
 import os
@@ -42,47 +40,55 @@ def _greedy(cfg, n_prompt, n_gen, fa, kv="f16", layers=None):
     prompt = [1] + rng.integers(300, gs.CONFIGS[cfg].n_vocab, n_prompt - 1).tolist()
     res = {}
     for gpu in (True, False):
-        m = la.Model(path, gpu=gpu, n_ctx=512, flash_attn=fa, kv_type=kv, n_threads=16)
+        m = la.Model(path, gpu=gpu, n_ctx=max(512, n_prompt + n_gen + 64), flash_attn=fa, kv_type=kv, n_threads=16)
         res[gpu] = m.greedy(prompt, n_gen)
         m.close()
     return res
 
 
-def _check(res, max_rel):
+def _check(res):
+    """ids equal and logits bit-identical at every step; on failure report the first step that
+    differs and how far"""
     (ids_g, lg_g), (ids_c, lg_c) = res[True], res[False]
-    rel = [float(np.abs(lg_g[i] - lg_c[i]).max() / np.abs(lg_c[i]).max()) for i in range(len(ids_c))]
     for i in range(len(ids_c)):
-        if ids_g[i] != ids_c[i]:
-            top2 = np.sort(lg_c[i])[-2:]
-            gap = (top2[1] - top2[0]) / np.abs(lg_c[i]).max()
-            assert gap < 4 * max_rel, f"step {i}: ids {ids_g[i]} vs {ids_c[i]}, cpu top-2 gap {gap:.2e}, rel {rel}"
-            break  # sequences legitimately diverge after a near tie
-    first = next((i for i in range(len(ids_c)) if ids_g[i] != ids_c[i]), len(ids_c))
-    assert max(rel[: max(first, 1)]) < max_rel, rel
-    return rel
+        same = lg_g[i].view(np.uint32) == lg_c[i].view(np.uint32)
+        if not same.all() or ids_g[i] != ids_c[i]:
+            rel = float(np.abs(lg_g[i] - lg_c[i]).max() / np.abs(lg_c[i]).max())
+            raise AssertionError(f"step {i}: ids {ids_g[i]} vs {ids_c[i]}, {int((~same).sum())} logits differ, "
+                                 f"max rel {rel:.2e}")
+    return 0.0
 
 
 @pytest.mark.parametrize("fa", [True, False])
 def test_greedy_tiny_q4km(fa):
-    rel = _check(_greedy("tiny-q4km", 16, 16, fa), 3e-2)
-    print("tiny-q4km fa", fa, "max rel logit err", max(rel))
+    _check(_greedy("tiny-q4km", 16, 16, fa))
 
 
 def test_greedy_tiny_q8_0():
-    _check(_greedy("tiny-q8_0", 16, 16, True), 3e-2)
+    _check(_greedy("tiny-q8_0", 16, 16, True))
 
 
 def test_greedy_tiny_moe_q5km():
     """Mixtral-style MoE FFN (router soft_max -> top-k ARGSORT -> GET_ROWS -> SUM_ROWS/DIV ->
     MUL_MAT_ID up/gate/down -> weighted sum) entirely on MI355X, vs the CPU backend; prompt
     decode exercises the expert-sorted batch path, generation the per-pair decode path."""
-    rel = _check(_greedy("tiny-moe-q5km", 16, 16, True), 3e-2)
-    print("tiny-moe-q5km max rel logit err", max(rel))
+    _check(_greedy("tiny-moe-q5km", 16, 16, True))
 
 
 def test_greedy_llama3_8b_2layer_q4km():
-    rel = _check(_greedy("llama3-8b-2l-q4km", 32, 16, True), 5e-2)
-    print("llama3-8b-2l max rel logit err", max(rel))
+    _check(_greedy("llama3-8b-2l-q4km", 32, 16, True))
+
+
+def test_greedy_llama3_8b_2layer_prompt512():
+    """A 512-token prompt (pp512's ubatch: the MFMA prefill tile, prefill flash attention) then
+    decode, bit-identical to the CPU backend."""
+    _check(_greedy("llama3-8b-2l-q4km", 512, 8, True))
+
+
+@pytest.mark.skip(reason="q8_0 KV cache: the GPU context aborts at creation; fixed with the exact q8_0-KV flash attention")
+def test_greedy_tiny_q8_0_kv_cache():
+    """A q8_0 KV cache (-ctk q8_0 -ctv q8_0) with flash attention."""
+    _check(_greedy("tiny-q4km", 16, 16, True, kv="q8_0"))
 
 
 @pytest.mark.parametrize("cfg", ["llama3-8b-2l-q4km", "tiny-q8_0", "tiny-moe-q5km"])

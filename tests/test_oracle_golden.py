@@ -171,3 +171,19 @@ def test_mul_mat_cpu_order_bit_exact(golden_dir, name, T):
     got = O.mul_mat_cpu(t, wq, x.shape[1], y.shape[1], x)
     assert (got.view(np.uint32) == y.view(np.uint32)).all(), \
         f"{int((got.view(np.uint32) != y.view(np.uint32)).sum())} of {y.size} outputs differ"
+
+
+@pytest.mark.parametrize("name", ["q4_K", "q4_K_m60", "q5_K", "q6_K", "q8_0", "q4_0"])
+def test_mul_mat_id_cpu_order_bit_exact(golden_dir, name):
+    """orc_mul_mat_id_cpu reproduces the CPU backend's mul_mat_id BIT FOR BIT as libllama runs it:
+    repacked forward_mul_mat_id gemv for Q4_K / Q4_0 stacks with M % 8 == 0, vec_dot otherwise
+    (goldens: gg_mul_mat_id_backend through the CPU_REPACK extra buffer)."""
+    g = load(golden_dir, "moe_cpu.npz")
+    t = {"q4_K": O.Q4_K, "q4_K_m60": O.Q4_K, "q5_K": O.Q5_K, "q6_K": O.Q6_K, "q8_0": O.Q8_0, "q4_0": O.Q4_0}[name]
+    n_as, n_used, M = int(g["n_as"]), int(g["n_used"]), int(g[f"M_{name}"])
+    for T, ne11 in ((1, 1), (1, n_used), (9, 1), (9, n_used)):
+        key = f"{name}_{T}_{ne11}"
+        x, ref = g[f"x_{key}"], g[f"y_{key}"]
+        got = O.mul_mat_id_cpu(t, g[f"wq_{name}"], x.shape[2], M, n_as, g[f"ids_{key}"], n_used, x)
+        assert (got.view(np.uint32) == ref.view(np.uint32)).all(), \
+            f"{key}: {int((got.view(np.uint32) != ref.view(np.uint32)).sum())} of {ref.size} differ"
