@@ -195,6 +195,14 @@ class Model:
         self.lib.llb_dump_clear(self.h)
         return out
 
+    def decode(self, tokens: list[int]):
+        """llama_decode of one batch; returns a copy of the last token's logits."""
+        import numpy as np
+        p = (ctypes.c_int32 * len(tokens))(*tokens)
+        if self.lib.llb_decode(self.h, p, len(tokens)) != 0:
+            raise RuntimeError("llama_decode failed")
+        return np.ctypeslib.as_array(self.lib.llb_logits(self.h), shape=(self.n_vocab,)).copy()
+
     def greedy(self, prompt: list[int], n_gen: int, want_logits: bool = True):
         import numpy as np
         p = (ctypes.c_int32 * len(prompt))(*prompt)

@@ -282,14 +282,312 @@ __global__ __launch_bounds__(256, 2) void k_mmq_q4K(const mmq_args p) {
     }
 }
 
+// ==== class-exact prefill tile for Q6_K / Q5_K (the vec_dot order, qtypes.h) ====================
+// The CPU's vec_dot keeps, per 256-block, eight integer "class" sums (class c = bytes 4c..4c+3
+// of every 32-element chunk) and runs eight fp32 chains acc[c] = fma(dy·d, cls_b[c], acc[c])
+// over the blocks, then hsum_float_8 (Q5_K adds the chain summs = fma(Imin, -dy·dmin, summs)).
+// On MFMA: per K block the 64 rows' weights are folded into class-major int8 planes in LDS —
+// the 32 weights of class c in K order 4·chunk + j, each pre-multiplied by its sub-block scale
+// and split as w' = 64·hi + lo (Q6_K: sc·(q-32) in [-4096, 4064] -> hi in [-64, 64], lo in
+// [0, 63]; Q5_K: sc·q <= 1953) — so a class integer is two v_mfma_i32_16x16x32_i8 (the lo
+// product accumulates onto the hi product shifted by 6), exact.  The token tile is the Q8_K rows
+// as staged by LDS-DMA (XOR-swizzled 16-byte chunks); a lane's B fragment of class c is the 4
+// bytes of each of its two chunks.  8 fp32 chains per output live in registers through the K
+// loop.
+template <class W> struct mc_stage {
+    static constexpr int XD = MQ_BN * 256;           // token scales [64] f32 after the rows
+    static constexpr int XS = XD + MQ_BN * 4;        // token bsums [64][16] i16
+    static constexpr int BYTES = XS + MQ_BN * 32;
+};
+
+__device__ __forceinline__ uint32_t pk_bytes(uint32_t e, uint32_t o) {   // bytes 0,2 from e, 1,3 from o
+    return (e & 0x00ff00ffu) | ((o & 0x00ff00ffu) << 8);
+}
+typedef short sh2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ sh2 as_sh2(uint32_t u) { sh2 v; __builtin_memcpy(&v, &u, 4); return v; }
+__device__ __forceinline__ uint32_t as_u32(sh2 v) { uint32_t u; __builtin_memcpy(&u, &v, 4); return u; }
+
+// four weights (bytes of q, unsigned) -> hi / lo bytes of sc·(q - bias) (16-bit lanes: exact)
+__device__ __forceinline__ void fold4(uint32_t q, int sc, int bias, uint32_t & hi, uint32_t & lo) {
+    const sh2 b2 = {(short) bias, (short) bias}, s2 = {(short) sc, (short) sc};
+    const sh2 we = (as_sh2(q & 0x00ff00ffu) - b2) * s2;
+    const sh2 wo = (as_sh2((q >> 8) & 0x00ff00ffu) - b2) * s2;
+    const sh2 sh = {6, 6}, m63 = {63, 63};
+    hi = pk_bytes(as_u32(we >> sh), as_u32(wo >> sh));
+    lo = pk_bytes(as_u32(we & m63), as_u32(wo & m63));
+}
+
+// Q6_K: a thread folds class c of one row.  Element e = 128n + 32g + l sits in chunk 4n + g;
+// its 6 bits are ql[64n + 32(g&1) + l] nibble g>>1 and qh[32n + l] bits 2g; its scale
+// scales[2·chunk + (l >= 16)] (dequantize_row_q6_K, ggml-quants.c:1684); class c is l = 4c..4c+3
+struct mc_q6_K {
+    static constexpr int BLK = 210;
+    static constexpr bool MINS = false;
+    struct raw { uint32_t ql[2][2]; uint32_t qh[2]; uint4 sc; uint32_t d; };
+    __device__ static void load(const uint8_t * blk, int c, raw & r) {
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            r.ql[n][0] = ld4(blk + 64 * n + 4 * c);
+            r.ql[n][1] = ld4(blk + 64 * n + 32 + 4 * c);
+            r.qh[n] = ld4(blk + 128 + 32 * n + 4 * c);
+        }
+        r.sc = ld16(blk + 192);
+        r.d = ld2(blk + 208);
+    }
+    // hi/lo[chunk]: the 4 bytes of class c in chunk `chunk`
+    __device__ static void fold(const raw & r, int c, uint32_t (&hi)[8], uint32_t (&lo)[8]) {
+        const uint32_t scw[4] = {r.sc.x, r.sc.y, r.sc.z, r.sc.w};
+#pragma unroll
+        for (int ch = 0; ch < 8; ++ch) {
+            const int n = ch >> 2, g = ch & 3;
+            const uint32_t q = ((r.ql[n][g & 1] >> (4 * (g >> 1))) & 0x0f0f0f0fu) | (((r.qh[n] >> (2 * g)) & 0x03030303u) << 4);
+            const int si = 2 * ch + (c >= 4 ? 1 : 0);
+            const int sc = (int8_t) ((scw[si >> 2] >> (8 * (si & 3))) & 0xff);
+            fold4(q, sc, 32, hi[ch], lo[ch]);
+        }
+    }
+    __device__ static float d_of(const raw & r) { return h2f((uint16_t) r.d); }
+    __device__ static float dmin_of(const raw &) { return 0.0f; }
+    __device__ static void mins_of(const raw &, int (&)[8]) {}
+};
+
+// Q5_K: chunk (sub-block) s = 2j + nib: element l of it is qs[32j + l] nibble nib with bit
+// (qh[l] >> s) & 1 on top (dequantize_row_q5_K, ggml-quants.c:1476); scale / min get_scale_min_k4(s)
+struct mc_q5_K {
+    static constexpr int BLK = 176;
+    static constexpr bool MINS = true;
+    struct raw { uint32_t qs[4]; uint32_t qh; uint4 hdr; };
+    __device__ static void load(const uint8_t * blk, int c, raw & r) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r.qs[j] = ld4(blk + 48 + 32 * j + 4 * c);
+        r.qh = ld4(blk + 16 + 4 * c);
+        r.hdr = ld16(blk);
+    }
+    __device__ static void scmin(const raw & r, int s, int & sc, int & m) {
+        const uint8_t * q = (const uint8_t *) &r.hdr + 4;
+        scale_min_k4(s, q, sc, m);
+    }
+    __device__ static void fold(const raw & r, int, uint32_t (&hi)[8], uint32_t (&lo)[8]) {
+#pragma unroll
+        for (int ch = 0; ch < 8; ++ch) {
+            int sc, m;
+            scmin(r, ch, sc, m);
+            const uint32_t q = ((r.qs[ch >> 1] >> (4 * (ch & 1))) & 0x0f0f0f0fu) | (((r.qh >> ch) & 0x01010101u) << 4);
+            fold4(q, sc, 0, hi[ch], lo[ch]);
+        }
+    }
+    __device__ static float d_of(const raw & r) { return h2f((uint16_t) (r.hdr.x & 0xffff)); }
+    __device__ static float dmin_of(const raw & r) { return h2f((uint16_t) (r.hdr.x >> 16)); }
+    __device__ static void mins_of(const raw & r, int (&mn)[8]) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) { int sc; scmin(r, s, sc, mn[s]); }
+    }
+};
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// 512 threads: wave w computes rows 16 (w & 3) .. +15 of the 64-row tile for tokens 32 (w >> 2) ..
+// +31 (two 16-token MFMA tiles): 8 x 2 x 4 = 64 chain registers per lane
+template <class W>
+__global__ __launch_bounds__(512, 2) void k_mmq_cls(const mmq_args p) {
+    using S = mc_stage<W>;
+    __shared__ __attribute__((aligned(16))) uint8_t st[2][S::BYTES];      // token stages
+    __shared__ __attribute__((aligned(16))) uint8_t ph[MQ_BM * 256];       // folded planes, swizzled
+    __shared__ __attribute__((aligned(16))) uint8_t pl[MQ_BM * 256];
+    __shared__ float wd[MQ_BM], wdm[MQ_BM];
+    __shared__ float wmn[W::MINS ? MQ_BM : 1][8];   // Q5_K mins (exact in f32)
+    __shared__ float xsb[W::MINS ? MQ_BN : 1][8];   // Q5_K per-token sub-block sums
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rg = wave & 3, tg = wave >> 2;
+    const int64_t row0 = (int64_t) blockIdx.x * MQ_BM;
+    const int64_t tok0 = (int64_t) blockIdx.y * MQ_BN;
+    const int h = lane >> 4, c16 = lane & 15;
+    const uint8_t * Wb = p.W;
+    int64_t T = p.T, col0 = 0;
+    if (p.cnt) {
+        T = p.cnt[blockIdx.z];
+        if (tok0 >= T) return;   // uniform: no barrier passed yet
+        col0 = p.off[blockIdx.z];
+        Wb = p.W + (int64_t) blockIdx.z * p.nb02;
+    }
+    const int64_t KB = p.K / 256;
+    // token-side LDS-DMA sources: instruction i = wave + 8k of 16 (1 KiB each)
+    const int8_t * xsrc[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int c = 64 * (wave + 8 * k) + lane, t = c >> 4, part = (c & 15) ^ (t & 15);
+        xsrc[k] = p.xq + (col0 + min(tok0 + t, T - 1)) * p.K + 16 * part;
+    }
+    const float * dsrc = p.xd + (col0 + min(tok0 + lane, T - 1)) * KB;
+    const int16_t * ssrc;
+    {
+        const int c = 64 * (wave == 2 ? 1 : 0) + lane, t = c >> 1, half = c & 1;
+        ssrc = p.xs + (col0 + min(tok0 + t, T - 1)) * (p.K / 16) + 8 * half;
+    }
+    auto issue_x = [&](int64_t b, int s) {
+        uint8_t * base = st[s];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            __builtin_amdgcn_global_load_lds((const void *) (xsrc[k] + b * 256), (lds_ptr_t) (base + 1024 * (wave + 8 * k)), 16, 0, 0);
+        }
+        if (wave == 0) {
+            __builtin_amdgcn_global_load_lds((const void *) (dsrc + b), (lds_ptr_t) (base + S::XD), 4, 0, 0);
+        } else if (W::MINS && wave <= 2) {
+            __builtin_amdgcn_global_load_lds((const void *) (ssrc + b * 16), (lds_ptr_t) (base + S::XS + 1024 * (wave - 1)), 16, 0, 0);
+        }
+    };
+    // the fold: thread = (row fr, class fc); its raw bytes come straight from global memory
+    const int fr = tid >> 3, fc = tid & 7;
+    const uint8_t * wsrc = Wb + min(row0 + fr, p.M - 1) * p.nb01;
+    typename W::raw wr;
+
+    float acc[8][2][4];
+    float summs[W::MINS ? 2 : 1][4];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[c][n][i] = 0.0f;
+#pragma unroll
+    for (int n = 0; n < (W::MINS ? 2 : 1); ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) summs[n][i] = 0.0f;
+
+    issue_x(0, 0);
+    W::load(wsrc, fc, wr);
+    const int ra = 16 * rg + c16;   // A row of this lane
+    for (int64_t b = 0; b < p.nblk; ++b) {
+        const int s = (int) (b & 1);
+        const int8_t * xq = (const int8_t *) st[s];
+        const float * xd = (const float *) (st[s] + S::XD);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // token stage s and this thread's raw weights landed; block b-1 is done with the planes
+        {
+            uint32_t hi[8], lo[8];
+            W::fold(wr, fc, hi, lo);
+            const int sw = 2 * (fr & 15);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {   // 8-byte slot 4c + q of the row, XOR-swizzled
+                const int slot = (4 * fc + q) ^ sw;
+                *(uint2 *) (ph + fr * 256 + 8 * slot) = make_uint2(hi[2 * q], hi[2 * q + 1]);
+                *(uint2 *) (pl + fr * 256 + 8 * slot) = make_uint2(lo[2 * q], lo[2 * q + 1]);
+            }
+            if (fc == 0) {
+                wd[fr] = W::d_of(wr);
+                wdm[fr] = W::dmin_of(wr);
+                if constexpr (W::MINS) {
+                    int mn[8];
+                    W::mins_of(wr, mn);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) wmn[fr][j] = (float) mn[j];
+                }
+            }
+            if constexpr (W::MINS) {
+                if (tid < MQ_BN) {
+                    const int16_t * s16 = (const int16_t *) (st[s] + S::XS) + 16 * tid;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) xsb[tid][j] = (float) (s16[2 * j] + s16[2 * j + 1]);
+                }
+            }
+        }
+        __syncthreads();
+        const bool more = b + 1 < p.nblk;
+        if (more) {
+            issue_x(b + 1, s ^ 1);
+            W::load(wsrc + (b + 1) * W::BLK, fc, wr);
+        }
+        float f[2][4];   // dy·d, as the CPU forms it
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            const float dy = xd[32 * tg + 16 * n + c16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f[n][i] = dy * wd[16 * rg + 4 * h + i];
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int slot = (4 * c + h) ^ (2 * c16);
+            const long ahi = *(const long *) (ph + ra * 256 + 8 * slot);
+            const long alo = *(const long *) (pl + ra * 256 + 8 * slot);
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const int8_t * xr = xq + (32 * tg + 16 * n + c16) * 256 + 4 * (c & 3);
+                const uint32_t b0 = *(const uint32_t *) (xr + 16 * ((4 * h + (c >> 2)) ^ c16));
+                const uint32_t b1 = *(const uint32_t *) (xr + 16 * ((4 * h + 2 + (c >> 2)) ^ c16));
+                const long bf = (long) b0 | ((long) b1 << 32);
+                v4i r = {0, 0, 0, 0};
+                r = __builtin_amdgcn_mfma_i32_16x16x32_i8(ahi, bf, r, 0, 0, 0);
+                r[0] <<= 6; r[1] <<= 6; r[2] <<= 6; r[3] <<= 6;
+                r = __builtin_amdgcn_mfma_i32_16x16x32_i8(alo, bf, r, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[c][n][i] = fmaf(f[n][i], (float) r[i], acc[c][n][i]);
+            }
+        }
+        if constexpr (W::MINS) {
+            // Imin[r][t] = sum_s mins[r][s] * bsum[t][s]: a K = 8 product, exact in fp32 (every
+            // partial sum is an integer below 2^24): two f32 MFMAs per 16 x 16 tile
+            const float a0 = wmn[ra][h], a1 = wmn[ra][h + 4];
+#pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                const int t = 32 * tg + 16 * n + c16;
+                v4f z = {0.f, 0.f, 0.f, 0.f};
+                z = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, xsb[t][h], z, 0, 0, 0);
+                z = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, xsb[t][h + 4], z, 0, 0, 0);
+                const float dy = xd[t];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) summs[n][i] = fmaf(z[i], -dy * wdm[16 * rg + 4 * h + i], summs[n][i]);
+            }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        const int64_t t = tok0 + 32 * tg + 16 * n + c16;
+        if (t >= T) continue;
+        char * drow = (char *) p.dst + t * p.nb1;
+        if (p.cnt) {
+            const int pair = p.list[col0 + t];
+            drow = (char *) p.dst + (pair % p.n_used) * p.nb1 + (pair / p.n_used) * p.nb2;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t m = row0 + 16 * rg + 4 * h + i;
+            // hsum_float_8: ((a0+a4)+(a2+a6)) + ((a1+a5)+(a3+a7))
+            float v = __fadd_rn(__fadd_rn(__fadd_rn(acc[0][n][i], acc[4][n][i]), __fadd_rn(acc[2][n][i], acc[6][n][i])),
+                                __fadd_rn(__fadd_rn(acc[1][n][i], acc[5][n][i]), __fadd_rn(acc[3][n][i], acc[7][n][i])));
+            if constexpr (W::MINS) v = __fadd_rn(v, summs[n][i]);
+            if (m < p.M) *(float *) (drow + m * 4) = v;
+        }
+    }
+}
+
 // ---- host --------------------------------------------------------------------------------------
-// Q4_K weights with M % 8 == 0 (the repacked order) and a batch of >= 16 tokens
+// Q4_K weights with M % 8 == 0 (the repacked order), Q5_K / Q6_K (the vec_dot order), and a
+// batch of >= 16 tokens
+static bool mmq_type_ok(const ggml_tensor * w) {
+    return (w->type == GGML_TYPE_Q4_K && w->ne[1] % 8 == 0) || w->type == GGML_TYPE_Q5_K || w->type == GGML_TYPE_Q6_K;
+}
+
+template <class W>
+static void launch_cls(hipStream_t st, const dim3 & grid, const mmq_args & p) {
+    hipLaunchKernelGGL(k_mmq_cls<W>, grid, dim3(512), 0, st, p);
+}
+
+static void launch_mmq(hipStream_t st, ggml_type t, const dim3 & grid, const mmq_args & p) {
+    switch (t) {
+        case GGML_TYPE_Q4_K: hipLaunchKernelGGL(k_mmq_q4K<mq_q4_K>, grid, dim3(256), 0, st, p); break;
+        case GGML_TYPE_Q5_K: launch_cls<mc_q5_K>(st, grid, p); break;
+        case GGML_TYPE_Q6_K: launch_cls<mc_q6_K>(st, grid, p); break;
+        default: GGML_ABORT("mi355x: mmq type");
+    }
+}
+
 bool mmq_supported(const ggml_tensor * dst) {
     static const bool off = getenv("GGML_MI355X_NO_MMQ") && atoi(getenv("GGML_MI355X_NO_MMQ")) != 0;
     if (off) return false;
     const ggml_tensor * w = dst->src[0];
     const ggml_tensor * x = dst->src[1];
-    if (w->type != GGML_TYPE_Q4_K || w->ne[1] % 8 != 0) return false;
+    if (!mmq_type_ok(w)) return false;
     if (x->type != GGML_TYPE_F32 || dst->type != GGML_TYPE_F32) return false;
     if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1) return false;
     if (x->ne[1] < 16) return false;             // small batches stay on the mat-vec path
@@ -316,7 +614,7 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
     p.dst = (float *) dst->data; p.nb1 = dst->nb[1];
     p.cnt = p.off = p.list = nullptr; p.n_used = 1; p.nb02 = 0; p.nb2 = 0;
     const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(p.T, MQ_BN));
-    hipLaunchKernelGGL(k_mmq_q4K<mq_q4_K>, grid, dim3(256), 0, ctx.stream, p);
+    launch_mmq(ctx.stream, w->type, grid, p);
     if (ctx.timing) ctx.time_end(TK_MMQ, flops, ev);
 }
 
@@ -326,8 +624,7 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
 // (repack.cpp:1385-1402): every token takes the per-block order.
 bool mmq_id_supported(const ggml_tensor * dst) {
     static const bool off = getenv("GGML_MI355X_NO_MMQ") && atoi(getenv("GGML_MI355X_NO_MMQ")) != 0;
-    const ggml_tensor * w = dst->src[0];
-    return !off && w->type == GGML_TYPE_Q4_K && w->ne[1] % 8 == 0;
+    return !off && mmq_type_ok(dst->src[0]);
 }
 
 void mul_mat_q_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, const int32_t * cnt, const int32_t * off,
@@ -342,7 +639,7 @@ void mul_mat_q_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, const i
     p.dst = (float *) dst->data; p.nb1 = dst->nb[1];
     p.cnt = cnt; p.off = off; p.list = list; p.n_used = ids->ne[0]; p.nb02 = w->nb[2]; p.nb2 = dst->nb[2];
     const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(n_pairs, MQ_BN), (unsigned) w->ne[2]);
-    hipLaunchKernelGGL(k_mmq_q4K<mq_q4_K>, grid, dim3(256), 0, ctx.stream, p);
+    launch_mmq(ctx.stream, w->type, grid, p);
 }
 
 }  // namespace mi355x

@@ -118,6 +118,34 @@ def test_fused_and_graph_replay_bit_identical(cfg):
     assert (la_.view(np.uint32) == lb.view(np.uint32)).all(), np.abs(la_ - lb).max()
 
 
+def test_graph_replay_survives_scratch_growth():
+    """A multi-turn flow: prompt, decode (the decode graph is captured and replayed), a longer
+    batch (the scratch arena grows and frees the slots the captured graph points at), decode
+    again.  The replayed graphs must be dropped and re-captured: every step's logits equal the
+    CPU backend's bit for bit, and replays happen after the long batch too."""
+    path = gs.ensure("llama3-8b-2l-q4km")
+    rng = np.random.default_rng(3)
+    V = gs.CONFIGS["llama3-8b-2l-q4km"].n_vocab
+    steps = ([[1] + rng.integers(300, V, 7).tolist()] + [[int(t)] for t in rng.integers(300, V, 4)] +
+             [rng.integers(300, V, 200).tolist()] + [[int(t)] for t in rng.integers(300, V, 6)])
+    out = {}
+    for gpu in (True, False):
+        m = la.Model(path, gpu=gpu, n_ctx=512, n_threads=16)
+        logits = []
+        for k, s in enumerate(steps):
+            if gpu and k == 6:
+                c0, r0 = la.graph_stats()
+            logits.append(m.decode(s))
+        if gpu:
+            c1, r1 = la.graph_stats()
+            assert c1 > c0 and r1 > r0, ("no capture / replay after the long batch", c1 - c0, r1 - r0)
+        out[gpu] = np.stack(logits)
+        m.close()
+    for k in range(len(steps)):
+        same = out[True][k].view(np.uint32) == out[False][k].view(np.uint32)
+        assert same.all(), f"step {k} ({len(steps[k])} tokens): {int((~same).sum())} logits differ"
+
+
 @pytest.mark.parametrize("cfg", ["tiny-q4km", "tiny-moe-q5km"])
 def test_graph_runs_on_mi355x(cfg):
     path = gs.ensure(cfg)
