@@ -238,6 +238,17 @@ void op_cpy(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst, const gg
                            (uint16_t * const *) dslot);
         return;
     }
+    if (src->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_Q8_0 && ggml_is_contiguous(src) && ggml_is_contiguous(dst) &&
+        src->ne[0] != dst->ne[0]) {
+        // contiguous both sides (the KV-cache store of a [D, H, T] Kcur): the same 32-blocks as
+        // quantizing src row by row (dup_to_q, ops.cpp), as one flat row
+        t4 S1 = S, D1 = D;
+        S1.ne[0] = D1.ne[0] = n;
+        for (int k = 1; k < 4; ++k) { S1.ne[k] = D1.ne[k] = 1; S1.nb[k] = S.nb[0] * n; D1.nb[k] = ggml_row_size(GGML_TYPE_Q8_0, n); }
+        dim3 g((unsigned) ceil_div(n, 256), 1u);
+        hipLaunchKernelGGL(k_cpy_f32_q8_0, g, dim3(64), 0, ctx.stream, (const char *) src->data, S1, (char *) dst->data, D1, dslot);
+        return;
+    }
     if (src->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_Q8_0) {
         const int64_t nrows = src->ne[1] * src->ne[2] * src->ne[3];
         dim3 g((unsigned) ceil_div(src->ne[0], 256), (unsigned) nrows);

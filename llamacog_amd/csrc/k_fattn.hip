@@ -280,7 +280,7 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     if (ctx.timing) ctx.time_begin(TK_FATTN, bytes, ev);
     static const bool fast = getenv("GGML_MI355X_FA_FAST") != nullptr && atoi(getenv("GGML_MI355X_FA_FAST")) != 0;
     a.cnt = nullptr;
-    if (!fast && a.k_type == GGML_TYPE_F16) {
+    if (!fast && (a.k_type == GGML_TYPE_F16 || a.k_type == GGML_TYPE_Q8_0)) {
         // fused quantization of the output for the next MUL_MAT (decode: one row)
         q8_act act;
         if (mm && a.n_q == 1 && nq3 == 1 && mmv_q_supported_type(mm->src[0]->type) &&

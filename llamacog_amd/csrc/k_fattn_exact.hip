@@ -1,4 +1,4 @@
-// k_fattn_exact.hip — CPU-exact flash attention over an f16 KV cache (the default; the
+// k_fattn_exact.hip — CPU-exact flash attention over an f16 or q8_0 KV cache (the default; the
 // split-K f32 kernel in k_fattn.hip is selected with GGML_MI355X_FA_FAST=1).
 //
 // Reproduces ggml_compute_forward_flash_attn_ext_f16 (ggml-cpu/ops.cpp:7015-7232) as the
@@ -10,7 +10,11 @@
 //   * s = s*scale (softcap: softcap*tanh(s)), + slope*mask (ops.cpp:7100-7115);
 //   * the online softmax walks the cache in order and accumulates VKQ in f16 with the
 //     vec_mad_f16 / vec_scale_f16 roundings (vec.h:262-290, 410-440): y = f16(fma(v,vs,y)),
-//     y = f16(y*ms); S = S*ms + vs (not contracted); expf taken in double and rounded.
+//     y = f16(y*ms); S = S*ms + vs (not contracted); glibc expf (libm_exact.h).
+// q8_0 cache (Q8 = true): Q is quantized to q8_0 (the x86 quantize_row_q8_0), K·Q is
+// ggml_vec_dot_q8_0_q8_0's class chains (arch/x86/quants.c:965: acc[c] = fma(dk·dq, cls[c],
+// acc[c]) over the blocks, hsum_float_8), V is dequantized (d·q) and VKQ accumulates in f32:
+// y = fma(v, vs, y), y = y*ms (ggml_vec_mad_f32 / ggml_vec_scale_f32).
 //
 // MI355X structure: one workgroup of 256 threads per (query row, query head) — 32 CUs busy
 // for a Llama-3-8B decode step rather than one per KV head.  The cache is walked in chunks
@@ -119,10 +123,10 @@ template <int D, int CHO = 0> struct fax_cfg {
 
 // OCC = workgroups per CU the register budget allows: 1 for decode (32-64 workgroups, every
 // register for ILP), 2 for prefill (thousands of workgroups; the LDS allows two)
-template <int D, int OCC = 1, int CHO = 0>
+template <int D, int OCC = 1, int CHO = 0, bool Q8 = false>
 __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
     using C = fax_cfg<D, CHO>;
-    constexpr int CH = C::CH, U = C::U, NM = D / 16;
+    constexpr int CH = C::CH, U = C::U, NM = D / 16, NB = D / 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int qd = tid & 3;                 // lane in the quad of a position (phase 1)
     const int64_t iq1 = blockIdx.x;
@@ -130,7 +134,12 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
     const int64_t iq3 = blockIdx.y / a.H;
     const int64_t hk = h / (a.H / a.Hkv);
 
-    __shared__ __attribute__((aligned(16))) uint16_t vl[CH * D];   // V chunk, [pos][D] f16
+    // V chunk: [pos][D] f16, or (Q8) [pos][D] int8 + [pos][D/32] block scales
+    __shared__ __attribute__((aligned(16))) uint16_t vl[Q8 ? CH * D / 2 : CH * D];
+    __shared__ float vd[Q8 ? CH * NB : 1];
+    __shared__ __attribute__((aligned(16))) int8_t qq[Q8 ? D : 1];   // Q as q8_0 (Q8)
+    __shared__ float qqd[Q8 ? NB : 1];
+    __shared__ int16_t qqs[Q8 ? NB : 1];
     __shared__ __attribute__((aligned(16))) float sc[CH + 6 * U];    // scores -> vs coefficient (0 where masked)
     __shared__ __attribute__((aligned(16))) float cm[CH + 6 * U];    // ms coefficient (1 where masked)
     __shared__ __attribute__((aligned(16))) float mk[CH + 6 * U];    // mask values of the chunk (-inf = skipped)
@@ -157,6 +166,26 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
             qf[m][0] = f16r(q4[m].x); qf[m][1] = f16r(q4[m].y); qf[m][2] = f16r(q4[m].z); qf[m][3] = f16r(q4[m].w);
         }
     }
+    // Q8: q as q8_0 blocks (lane qd of a quad takes classes 2qd, 2qd+1 of every block)
+    uint2 qb[Q8 ? NB : 1];
+    float qdb[Q8 ? NB : 1];
+    if constexpr (Q8) {
+        if (wave == 0) {
+            const float * qrow = (const float *) (a.q + iq1 * a.nbq1 + h * a.nbq2 + iq3 * a.nbq3);
+            for (int b0 = 0; b0 < D; b0 += 256) {
+                const bool valid = b0 + 4 * lane < D;
+                float qv[4] = {0.f, 0.f, 0.f, 0.f};
+                if (valid) { const float4 t = *(const float4 *) (qrow + b0 + 4 * lane); qv[0] = t.x; qv[1] = t.y; qv[2] = t.z; qv[3] = t.w; }
+                q8_0_wave(qv, lane, valid, qq + b0, qqd + b0 / 32, qqs + b0 / 32);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            qb[b] = *(const uint2 *) (qq + 32 * b + 8 * qd);
+            qdb[b] = qqd[b];
+        }
+    }
     const float slope = a.max_bias > 0.0f
         ? (float) ((uint32_t) h < a.n_head_log2 ? pow((double) a.m0, (double) (h + 1))
                                                : pow((double) a.m1, (double) (2 * ((uint32_t) h - a.n_head_log2) + 1)))
@@ -165,6 +194,7 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
     // phase-3 state: output dim d = tid (threads < D)
     const int d = tid;
     uint32_t yb = 0;   // f16 bits (low half)
+    float yf = 0.0f;   // Q8: the f32 accumulator
     float S = 0.0f;
     float mcarry = -INFINITY;   // running max of the previous chunks (uniform)
 
@@ -195,17 +225,64 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
         mark(0);
         if (nrun == 0) { __syncthreads(); continue; }   // whole chunk masked
         // ---- phase 0: V rows [0, nrun) HBM -> LDS (async; waited on before phase 3) -------
-        {
+        if constexpr (!Q8) {
             const int r_in = lane / (D / 8), col = lane % (D / 8);
             for (int p = wave; p * C::RPP < nrun; p += 4) {
                 const int row = min(p * C::RPP + r_in, nrun - 1);
                 const char * src = vbase + (c0 + row) * a.nbv1 + col * 16;
                 __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (vl + p * 512), 16, 0, 0);
             }
+        } else {
+            // q8_0 blocks (34 B, 2-byte aligned): quants to vq[pos][D], scales to vd[pos][D/32]
+            int8_t * vq = (int8_t *) vl;
+            for (int i = tid; i < nrun * NB; i += 256) {
+                const int row = i / NB, b = i % NB;
+                const uint8_t * src = (const uint8_t *) vbase + (c0 + row) * a.nbv1 + 34 * b;
+                const uint4 lo = ld16(src + 2), hi = ld16(src + 18);
+                *(uint4 *) (vq + row * D + 32 * b) = lo;
+                *(uint4 *) (vq + row * D + 32 * b + 16) = hi;
+                vd[row * NB + b] = h2f(ld2(src));
+            }
         }
         mark(1);
         // ---- phase 1: scores, 4 lanes per position, every K load of the chunk in flight ----
-        {
+        if constexpr (Q8) {
+            // lane qd holds bytes 8qd .. 8qd+7 of every block: classes 2qd, 2qd+1
+            uint2 kb[C::NP][NB];
+            uint32_t kd[C::NP][NB];
+#pragma unroll
+            for (int p = 0; p < C::NP; ++p) {
+                const int j = min(64 * p + (tid >> 2), nrun - 1);
+                const uint8_t * krow = (const uint8_t *) kbase + (c0 + j) * a.nbk1;
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    if (64 * p < nrun) { kb[p][b] = ld8(krow + 34 * b + 2 + 8 * qd); kd[p][b] = ld2(krow + 34 * b); }
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < C::NP; ++p) {
+                if (64 * p >= nrun) break;
+                const int j = 64 * p + (tid >> 2);
+                float ae = 0.0f, ao = 0.0f;
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    const float dd = __fmul_rn(h2f((uint16_t) kd[p][b]), qdb[b]);
+                    ae = fmaf(dd, (float) dot4((int) kb[p][b].x, (int) qb[b].x, 0), ae);
+                    ao = fmaf(dd, (float) dot4((int) kb[p][b].y, (int) qb[b].y, 0), ao);
+                }
+                // hsum_float_8 over the quad: lanes hold (a[2q], a[2q+1])
+                ae = __fadd_rn(ae, quad_from_plus2(ae));
+                ao = __fadd_rn(ao, quad_from_plus2(ao));
+                ae = __fadd_rn(ae, quad_from_plus1(ae));
+                ao = __fadd_rn(ao, quad_from_plus1(ao));
+                const float w = __fadd_rn(ae, ao);
+                if (qd == 0 && j < nrun) {
+                    float s = __fmul_rn(w, a.scale);
+                    if (a.softcap != 0.0f) s = __fmul_rn(a.softcap, tanhf(s));
+                    sc[j] = __fadd_rn(s, __fmul_rn(slope, mk[j]));
+                }
+            }
+        } else {
             uint2 kh[C::NP][NM];
 #pragma unroll
             for (int p = 0; p < C::NP; ++p) {
@@ -284,7 +361,22 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
         // ---- phase 3: sequential f16 recurrence (V from LDS) --------------------------------
         // y = f16(y*ms) and S*ms only where the running max moved (ms != 1: y*1 and S*1 are
         // identities); masked / padded positions keep the state (-0 must survive)
-        if (d < D) {
+        if (Q8 && d < D) {
+            // f32 recurrence: y = y*ms where the running max moved, y = fma(v, vs, y),
+            // S = S*ms + vs; masked positions keep the state
+            const int8_t * vq = (const int8_t *) vl;
+            for (int j = 0; j < nrun; ++j) {
+                const float v = __fmul_rn((float) vq[j * D + d], vd[j * NB + d / 32]);
+                const float vs = sc[j], ms = cm[j];
+                const bool live = __float_as_uint(mk[j]) != 0xff800000u;
+                const bool upd = __float_as_uint(ms) != 0x3f800000u;
+                const float ys = upd ? __fmul_rn(yf, ms) : yf;
+                const float Ss = upd ? __fmul_rn(S, ms) : S;
+                yf = live ? fmaf(v, vs, ys) : yf;
+                S = live ? __fadd_rn(Ss, vs) : S;
+            }
+        }
+        if (!Q8 && d < D) {
             // batches of U positions, software-pipelined: batch n+1's V values and
             // coefficients are read from LDS while batch n computes
             // (a prefetch past the chunk end reads other LDS arrays or past the allocation, which
@@ -356,7 +448,7 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
 
     // ---- output and its optional quantization ------------------------------------------------
     float * drow = (float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H + h * a.nb1_dst + iq3 * a.nb2_dst);
-    const float o = d < D ? __fmul_rn(h2f((uint16_t) yb), 1.0f / S) : 0.0f;
+    const float o = d < D ? __fmul_rn(Q8 ? yf : h2f((uint16_t) yb), 1.0f / S) : 0.0f;
     // a Q8_K block spanning several heads is handed to the last of their workgroups: the
     // outputs are stored write-through (sc1) and drained before the counter add, and read
     // back with sc1 loads, so no L2 write-back fence is needed (MI355X_MICROARCH.md,
@@ -420,6 +512,18 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     // 9.6k -> 10.6k tok/s; OCC 3/4 spill and run slower, 8.5k / 8.2k) or 256 (64 KiB)
     static const int pch = getenv("GGML_MI355X_FA_PREFILL_CH") ? atoi(getenv("GGML_MI355X_FA_PREFILL_CH")) : 128;
     const bool wide = a.n_q * a.H * nq3 > 256 && pocc >= 2;   // prefill: more workgroups than CUs
+    if (a.k_type == GGML_TYPE_Q8_0) {
+        switch (a.D) {
+            case 64:  hipLaunchKernelGGL((k_fattn_exact<64, 1, 0, true>), grid, dim3(256), 0, st, a); break;
+            case 128:
+                if (wide) hipLaunchKernelGGL((k_fattn_exact<128, 2, 128, true>), grid, dim3(256), 0, st, a);
+                else hipLaunchKernelGGL((k_fattn_exact<128, 1, 0, true>), grid, dim3(256), 0, st, a);
+                break;
+            case 256: hipLaunchKernelGGL((k_fattn_exact<256, 1, 0, true>), grid, dim3(256), 0, st, a); break;
+            default: GGML_ABORT("mi355x: FA head size %d", (int) a.D);
+        }
+        return;
+    }
     switch (a.D) {
         case 64:  hipLaunchKernelGGL(k_fattn_exact<64>, grid, dim3(256), 0, st, a); break;
         case 128:

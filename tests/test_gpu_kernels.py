@@ -143,12 +143,30 @@ def test_flash_attn_f16_golden(K, golden_dir, n_q):
 
 @pytest.mark.parametrize("n_q", [1, 7])
 def test_flash_attn_q8_0_golden(K, golden_dir, n_q):
+    """q8_0 KV cache: Q quantized to q8_0, vec_dot_q8_0_q8_0 class chains, f32 VKQ: bit-exact."""
     g = load(golden_dir, "flash_attn.npz")
     D, H, Hkv, n_kv = int(g["D"]), int(g["H"]), int(g["Hkv"]), int(g["n_kv"])
     out = K.flash_attn(g[f"q_{n_q}"], g[f"k_q8_0_{n_q}"], g[f"v_q8_0_{n_q}"], g[f"mask_{n_q}"], O.Q8_0, D, H, Hkv, n_kv,
                        1.0 / np.sqrt(D))
-    ref = g[f"out_q8_0_{n_q}"]
-    assert np.abs(out - ref).max() / np.abs(ref).max() < 1e-5
+    assert_bits(out, g[f"out_q8_0_{n_q}"], f"flash_attn q8_0 n_q={n_q}")
+
+
+@pytest.mark.parametrize("n_kv,n_q", [(256, 1), (1024, 1), (700, 9), (512, 64)])
+def test_flash_attn_q8_0_llama_shapes_bit_exact(K, n_kv, n_q):
+    """q8_0 cache at Llama-3-8B head layout (D 128, 32 / 8 heads), causal mask, vs the oracle."""
+    rng = np.random.default_rng(n_kv + 3 * n_q)
+    D, H, Hkv = 128, 32, 8
+    q = rng.standard_normal((n_q, H, D)).astype(np.float32)
+    kf = rng.standard_normal((n_kv * Hkv, D)).astype(np.float32)
+    vf = rng.standard_normal((n_kv * Hkv, D)).astype(np.float32)
+    k = O.quantize_rows(O.Q8_0, kf).reshape(n_kv, -1)
+    v = O.quantize_rows(O.Q8_0, vf).reshape(n_kv, -1)
+    m = np.zeros((n_q, n_kv), dtype=np.float16)
+    for r in range(n_q):
+        m[r, n_kv - n_q + r + 1:] = -np.inf
+    out = K.flash_attn(q, k, v, m.view(np.uint16), O.Q8_0, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    ref = O.flash_attn(q, k, v, m.view(np.uint16), O.Q8_0, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    assert_bits(out, ref, f"flash_attn q8_0 n_kv={n_kv} n_q={n_q}")
 
 
 @pytest.mark.parametrize("n_kv,n_q,Hkv,G", [(256, 1, 8, 4), (1024, 1, 8, 4), (4096, 1, 8, 8), (512, 32, 8, 4),

@@ -85,7 +85,6 @@ def test_greedy_llama3_8b_2layer_prompt512():
     _check(_greedy("llama3-8b-2l-q4km", 512, 8, True))
 
 
-@pytest.mark.skip(reason="q8_0 KV cache: the GPU context aborts at creation; fixed with the exact q8_0-KV flash attention")
 def test_greedy_tiny_q8_0_kv_cache():
     """A q8_0 KV cache (-ctk q8_0 -ctv q8_0) with flash attention."""
     _check(_greedy("tiny-q4km", 16, 16, True, kv="q8_0"))
