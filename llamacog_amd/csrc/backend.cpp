@@ -112,6 +112,10 @@ void exec_ctx::free_scratch() {
     }
     if (fa_cnt) (void) hipFree(fa_cnt);
     fa_cnt = nullptr;
+    if (tail_cnt) (void) hipFree(tail_cnt);
+    tail_cnt = nullptr;
+    if (rsum_buf) (void) hipFree(rsum_buf);
+    rsum_buf = nullptr;
 }
 
 hipEvent_t exec_ctx::get_event() {
@@ -466,12 +470,17 @@ static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.rt_table = nullptr;
     ex.done.clear();
     ex.silu_defer = ex.silu_mul = nullptr;
+    ex.pro = {};
+    ex.nsite = 0;
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) i += op_compute(ex, cgraph, i);
     if (ex.silu_defer) {   // a deferred SILU whose MUL never came
         op_unary(ex, ex.silu_defer);
         ex.silu_defer = ex.silu_mul = nullptr;
     }
+    // the residual sums of this graph, read by now: zero for the next graph
+    if (ex.nsite) MI_CHECK(hipMemsetAsync(ex.rsum_buf, 0, (size_t) ex.nsite * exec_ctx::SITE_DOUBLES * sizeof(double), ex.stream));
+    ex.pro = {};
 }
 
 // returns true when the graph was launched as (or captured into) a hipGraph

@@ -80,6 +80,42 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// DPP lane exchanges (VALU, no LDS round trip): within quads (xor 1, xor 2), half-row mirror
+// (lane i <-> 7-i of each 8) and row mirror (i <-> 15-i of each 16).  Every pairing is total,
+// so a commutative reduction over them leaves each group's result in all of its lanes.
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
+__device__ __forceinline__ int quad_sum(int v) { v += dpp<DPP_XOR1>(v); return v + dpp<DPP_XOR2>(v); }
+__device__ __forceinline__ float dppf_xor1(float v) { return __int_as_float(dpp<DPP_XOR1>(__float_as_int(v))); }
+__device__ __forceinline__ float dppf_xor2(float v) { return __int_as_float(dpp<DPP_XOR2>(__float_as_int(v))); }
+// lane i <- lane i^4: row_shr:4 for lanes with bit 2 set, row_shl:4 for the others
+__device__ __forceinline__ float dppf_xor4(float v) {
+    const int up = dpp<0x114>(__float_as_int(v)), dn = dpp<0x104>(__float_as_int(v));
+    return __int_as_float((threadIdx.x & 4) ? up : dn);
+}
+__device__ __forceinline__ int oct_sum(int v) { v = quad_sum(v); return v + dpp<DPP_HMIRROR>(v); }
+// wave-uniform max / min of unsigned 32-bit values (all 64 lanes active): rows by DPP, then
+// the four row results by readlane
+__device__ __forceinline__ uint32_t wave_umax(uint32_t v) {
+    v = max(v, (uint32_t) dpp<DPP_XOR1>((int) v));
+    v = max(v, (uint32_t) dpp<DPP_XOR2>((int) v));
+    v = max(v, (uint32_t) dpp<DPP_HMIRROR>((int) v));
+    v = max(v, (uint32_t) dpp<DPP_MIRROR>((int) v));
+    const uint32_t a = (uint32_t) __builtin_amdgcn_readlane((int) v, 0), b = (uint32_t) __builtin_amdgcn_readlane((int) v, 16);
+    const uint32_t c = (uint32_t) __builtin_amdgcn_readlane((int) v, 32), d = (uint32_t) __builtin_amdgcn_readlane((int) v, 48);
+    return max(max(a, b), max(c, d));
+}
+__device__ __forceinline__ uint32_t wave_umin(uint32_t v) {
+    v = min(v, (uint32_t) dpp<DPP_XOR1>((int) v));
+    v = min(v, (uint32_t) dpp<DPP_XOR2>((int) v));
+    v = min(v, (uint32_t) dpp<DPP_HMIRROR>((int) v));
+    v = min(v, (uint32_t) dpp<DPP_MIRROR>((int) v));
+    const uint32_t a = (uint32_t) __builtin_amdgcn_readlane((int) v, 0), b = (uint32_t) __builtin_amdgcn_readlane((int) v, 16);
+    const uint32_t c = (uint32_t) __builtin_amdgcn_readlane((int) v, 32), d = (uint32_t) __builtin_amdgcn_readlane((int) v, 48);
+    return min(min(a, b), min(c, d));
+}
+
 // ggml_v_expf of the AVX-512 CPU backend (ggml-cpu/vec.h:731-756), bit-exact: the
 // reference's SiLU and soft_max use it, not libm expf.
 __device__ __forceinline__ float v_expf_avx512(float x) {

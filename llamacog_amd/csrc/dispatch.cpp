@@ -308,6 +308,120 @@ static bool dead_after(ggml_cgraph * g, int n, int from, const ggml_tensor * t,
 
 
 
+// the next node after p that computes something (not a view), or n
+static int next_compute(ggml_cgraph * g, int p, int n) {
+    for (int k = p + 1; k < n; ++k) {
+        if (!is_view_op(ggml_graph_node(g, k))) return k;
+    }
+    return n;
+}
+
+static void norm_stores(ggml_cgraph * g, int n, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm,
+                        bool & store_norm, bool & store_mul);
+
+// Residual producer (k_gemv.hip): the single projection mm0 at node i is followed by
+// ADD(mm0, res) -> RMS_NORM -> [MUL w] (the residual and the next norm, build_norm in
+// src/llama-graph.cpp:464-497) whose only readers are decode mat-vecs.  The producer stores
+// x = mm0 + res (mm0 itself is dead) and the sum of squares; the consumers form the norm in
+// their prologue, so neither the RMS_NORM nor the MUL runs as a node.  Same-lane in-place
+// aliases of mm0 / res by the ADD output are safe (each row is read before it is written).
+static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tensor * mm0, gemv_epi & epi,
+                       std::vector<const ggml_tensor *> & absorbed) {
+    const int pa = next_compute(g, i, n);
+    ggml_tensor * ad = at(g, pa, n);
+    if (!ad || ad->op != GGML_OP_ADD || !f32c(ad)) return;
+    const ggml_tensor * res = ad->src[0] == mm0 ? ad->src[1] : (ad->src[1] == mm0 ? ad->src[0] : nullptr);
+    if (!res || res == mm0 || !f32c(res) || !ggml_are_same_shape(res, mm0) || !ggml_are_same_shape(ad, mm0) ||
+        !computed_before(ctx, g, res, i)) return;
+    if (overlaps(ad, res) && ad->data != res->data) return;
+    if (!dead_after(g, n, pa, mm0, {ad})) return;   // mm0 itself is not stored
+    const int pn = next_compute(g, pa, n);
+    ggml_tensor * nm = at(g, pn, n);
+    if (!nm || nm->op != GGML_OP_RMS_NORM || nm->src[0] != ad || !f32c(nm) || nm->ne[0] % 256 != 0 || nm->ne[0] > 16384 ||
+        ggml_nrows(nm) != 1) return;
+    ggml_tensor * mul = norm_weight_mul(g, pn, n);
+    if (mul && (!f32c(mul) || !ggml_is_contiguous(mul->src[1]))) return;
+    ggml_tensor * last = mul ? mul : nm;
+    ggml_tensor * mm = at(g, next_compute(g, node_index(g, last), n), n);
+    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != last || !gemv_supported(mm)) return;
+    // every reader of the chain's output must be a decode mat-vec (each forms the activation in
+    // its own prologue), and the norm output itself may be read only by the MUL
+    std::vector<const ggml_tensor *> readers;
+    const int pl = node_index(g, last);
+    for (int k = pl + 1; k < n && k <= pl + 16; ++k) {
+        const ggml_tensor * c = ggml_graph_node(g, k);
+        if (c->op == GGML_OP_MUL_MAT && c->src[1] == last && gemv_supported(c)) readers.push_back(c);
+    }
+    if (!dead_after(g, n, pl + 1, last, readers)) return;
+    if (mul && !dead_after(g, n, pn + 1, nm, {mul})) return;
+    double * site = gemv_rsum_site(ctx);
+    if (!site) return;
+    epi.rres = (const float *) res->data;
+    epi.rxsum = (float *) ad->data;
+    epi.rsum = site;
+    float eps;
+    memcpy(&eps, nm->op_params, sizeof(float));
+    ctx.pro = {last, last->data, (const float *) ad->data, mul ? (const float *) mul->src[1]->data : nullptr, site, eps, nm->ne[0]};
+    absorbed.push_back(ad);
+    absorbed.push_back(nm);
+    if (mul) absorbed.push_back(mul);
+}
+
+// GEMV tail 2: the gate/up pair of this launch is followed by SILU(gate) and MUL(silu, up)
+// (build_ffn LLM_FFN_SILU + PAR, src/llama-graph.cpp:555-616), optionally feeding the down
+// mat-vec.  Both are hoisted to this launch: checked like every hoisted node; their outputs may
+// alias the gate / up outputs only exactly (the same lane reads, then writes, each element).
+static void plan_tail_swiglu(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tensor * const * mms, gemv_epi & epi,
+                             std::vector<const ggml_tensor *> & absorbed) {
+    if (mms[0]->src[0]->type != mms[1]->src[0]->type || mms[0]->ne[0] != mms[1]->ne[0] || mms[0]->ne[0] % 256 != 0 ||
+        mms[0]->ne[0] / 256 > exec_ctx::TAIL_CNT) return;
+    auto skipped = [&](const ggml_tensor * c) {
+        return is_view_op(c) || std::find(absorbed.begin(), absorbed.end(), c) != absorbed.end() ||
+               std::find(ctx.done.begin(), ctx.done.end(), c) != ctx.done.end();
+    };
+    int ps = -1;
+    for (int k = i + 1; k < n && k <= i + 6; ++k) {
+        ggml_tensor * c = ggml_graph_node(g, k);
+        if (skipped(c)) continue;
+        if (c->op == GGML_OP_UNARY && ggml_get_unary_op(c) == GGML_UNARY_OP_SILU && (c->src[0] == mms[0] || c->src[0] == mms[1])) ps = k;
+        break;
+    }
+    if (ps < 0) return;
+    ggml_tensor * sl = ggml_graph_node(g, ps);
+    const int tg = sl->src[0] == mms[0] ? 0 : 1, tu = 1 - tg;
+    int pm = -1;
+    for (int k = ps + 1; k < n && k <= ps + 4; ++k) {
+        ggml_tensor * c = ggml_graph_node(g, k);
+        if (skipped(c)) continue;
+        if (c->op == GGML_OP_MUL && ((c->src[0] == sl && c->src[1] == mms[tu]) || (c->src[1] == sl && c->src[0] == mms[tu]))) pm = k;
+        break;
+    }
+    if (pm < 0) return;
+    ggml_tensor * mul = ggml_graph_node(g, pm);
+    if (!f32c(sl) || !f32c(mul) || !ggml_are_same_shape(sl, mms[tg]) || !ggml_are_same_shape(mul, mms[tg])) return;
+    auto clash = [](const ggml_tensor * t, const ggml_tensor * o) {
+        return overlaps(t, o) && !(t->data == o->data && ggml_nbytes(t) == ggml_nbytes(o));
+    };
+    if (clash(sl, mms[0]) || clash(sl, mms[1]) || clash(mul, mms[0]) || clash(mul, mms[1]) || clash(mul, sl)) return;
+    const ggml_tensor * o1[1] = {sl};
+    if (!can_hoist(g, i, ps, o1, 1, absorbed)) return;
+    std::vector<const ggml_tensor *> ab2 = absorbed;
+    ab2.push_back(sl);
+    const ggml_tensor * o2[1] = {mul};
+    if (!can_hoist(g, i, pm, o2, 1, ab2)) return;
+    ggml_tensor * down = at(g, next_compute(g, pm, n), n);
+    if (down && !(down->op == GGML_OP_MUL_MAT && down->src[1] == mul && gemv_supported(down))) down = nullptr;
+    epi.tail = true;
+    epi.t_gate = tg; epi.t_up = tu;
+    epi.t_silu = sl; epi.t_mul = mul;
+    epi.t_store_silu = !dead_after(g, n, ps + 1, sl, {mul});
+    epi.t_store_mul = !(down && dead_after(g, n, pm + 1, mul, {down}));
+    epi.tq_for = down;
+    epi.tq_key = mul;
+    absorbed.push_back(sl);
+    absorbed.push_back(mul);
+}
+
 // decode mat-vec: launch node i together with up to two later MUL_MATs on the same src1
 // (Q/K/V, gate/up) in one grouped kernel, with fused epilogues: the SiLU that follows a
 // projection, the NORM-mode ROPE of a projection, and f16 KV-cache stores (CPY) of a
@@ -318,6 +432,10 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     ggml_tensor * mms[3] = {mm0, nullptr, nullptr};
     gemv_epi epi;
     int nm = 1;
+    // the activation of a pending norm prologue (plan_resid at the producer)
+    if (ctx.pro.last && ctx.pro.last == mm0->src[1] && ctx.pro.data == mm0->src[1]->data) {
+        epi.px = ctx.pro.x; epi.pw = ctx.pro.w; epi.psum = ctx.pro.sum; epi.peps = ctx.pro.eps; epi.pn = ctx.pro.n;
+    }
     std::vector<const ggml_tensor *> absorbed;   // nodes this launch computes (besides node i)
     std::vector<const ggml_tensor *> outs = {mm0};
 
@@ -431,6 +549,21 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
                     epi.rope[m] != nullptr, epi.rope_f16[m] != nullptr, epi.f16out[m] != nullptr, epi.elide_dst[m], epi.elide_rope[m]);
         }
         fprintf(stderr, "\n");
+    }
+    // the next norm chain moves into this launch (residual producer) and its consumers
+    // (prologue); silu(gate) * up into the gate/up launch (SwiGLU tail).  GGML_MI355X_TAILS=0 /
+    // GGML_MI355X_RESID=0 run those chains as their own launches (k_fused.hip)
+    static const bool tails = !getenv("GGML_MI355X_TAILS") || atoi(getenv("GGML_MI355X_TAILS")) != 0;
+    static const bool resid = !getenv("GGML_MI355X_RESID") || atoi(getenv("GGML_MI355X_RESID")) != 0;
+    bool plain = true;
+    for (int m = 0; m < nm; ++m) {
+        plain = plain && !epi.silu[m] && !epi.rope[m] && !epi.f16out[m] && !epi.rope_f16[m] && !epi.elide_dst[m];
+    }
+    if (resid && plain && nm == 1) plan_resid(ctx, g, i, n, mm0, epi, absorbed);
+    if (tails && plain && nm == 2 && gemv_tail_ready(ctx)) plan_tail_swiglu(ctx, g, i, n, mms, epi, absorbed);
+    if (dbg && (epi.tail || epi.rres || epi.px)) {
+        fprintf(stderr, "[mi355x]   tail=%d -> %s resid=%d prologue=%d\n", epi.tail, epi.tq_for ? epi.tq_for->name : "(none)",
+                epi.rres != nullptr, epi.px != nullptr);
     }
     gemv_group(ctx, mms, nm, &epi);
     // node i+1 when it is node i's SiLU is consumed here; everything else is skipped later
@@ -644,6 +777,20 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                     norm_stores(cgraph, n, nx, mul, mm, sn, sm);
                     const ggml_tensor * qkey = nullptr;
                     if (ggml_tensor * c = moe_quant_consumer(cgraph, n, mul ? mul : nx, mm, &qkey)) mm = c;
+                    static const bool dbga = getenv("GGML_MI355X_DEBUG_ALIAS") != nullptr;
+                    if (dbga) {
+                        const ggml_tensor * last = mul ? mul : nx;
+                        fprintf(stderr, "[alias] @%d add=%s a=%s res=%s: add==a %d add==res %d norm~a %d norm~res %d mul~norm %d |", i, node->name,
+                                node->src[0]->name, node->src[1]->name, node->data == node->src[0]->data, node->data == node->src[1]->data,
+                                overlaps(nx, node->src[0]), overlaps(nx, node->src[1]), mul && mul->data == nx->data);
+                        for (int k = i + used; k < n && k < i + used + 14; ++k) {
+                            const ggml_tensor * c = ggml_graph_node(cgraph, k);
+                            if (is_view_op(c)) continue;
+                            const bool r = overlaps(c, node->src[0]) || overlaps(c, node->src[1]) || overlaps(c, node) || overlaps(c, last);
+                            fprintf(stderr, " %s:%s%s", ggml_op_name(c->op), c->name, r ? "[ALIAS]" : "");
+                        }
+                        fprintf(stderr, "\n");
+                    }
                     if (fused_norm(ctx, node, nx, mul, mm, sn, sm, qkey)) return used;
                 }
             }

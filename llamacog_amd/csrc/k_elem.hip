@@ -352,19 +352,19 @@ __global__ __launch_bounds__(256) void k_rms_norm(const char * __restrict__ x, t
     const float * xr = (const float *) (x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3]);
     float * yr = (float *) (y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
     const int64_t ne0 = tx.ne[0];
-    // the CPU's sequential double sum, decided from a double-double sum (quant_act.h)
-    ddv acc = {0.0, 0.0};
+    // the CPU's sequential double sum, decided from a parallel one (quant_act.h)
+    double acc = 0.0;
     for (int64_t i = threadIdx.x; i < ne0; i += 256) {
         const float v = *(const float *) ((const char *) xr + i * tx.nb[0]);
-        acc = dd_add(acc, (double) __fmul_rn(v, v));
+        acc = __dadd_rn(acc, (double) __fmul_rn(v, v));
     }
-    acc = dd_wave_sum(acc);
-    __shared__ ddv part[4];
+    acc = wave_sum(acc);
+    __shared__ double part[4];
     __shared__ float smean;
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const ddv s = dd_add(dd_add(part[0], part[1]), dd_add(part[2], part[3]));
+        const double s = __dadd_rn(__dadd_rn(part[0], part[1]), __dadd_rn(part[2], part[3]));
         float m;
         if (!rms_mean_decided(s, ne0, m)) {
             double q = 0.0;

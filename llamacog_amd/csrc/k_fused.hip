@@ -38,7 +38,7 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
     const int BT = blockDim.x, NW = BT >> 6;
     const int64_t row = blockIdx.x;
     const int64_t ro = row * p.ne0;
-    __shared__ ddv wpart[16];
+    __shared__ double wpart[16];
     __shared__ float smean;
     float4 v[NV], wv[NV];
 #pragma unroll
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
         // the norm weight is loaded with the row, not after the reduction
         if (p.w) wv[k] = *(const float4 *) (p.w + 4 * (tid + BT * k));
     }
-    ddv acc = {0.0, 0.0};
+    double acc = 0.0;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int64_t e = 4 * (tid + BT * k);
@@ -56,17 +56,20 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
             v[k].x = __fadd_rn(v[k].x, bb.x); v[k].y = __fadd_rn(v[k].y, bb.y);
             v[k].z = __fadd_rn(v[k].z, bb.z); v[k].w = __fadd_rn(v[k].w, bb.w);
         }
-        acc = dd_sq4(acc, v[k]);
+        acc = __dadd_rn(acc, sq4(v[k]));
     }
-    acc = dd_wave_sum(acc);
+    acc = wave_sum(acc);
     if (lane == 0) wpart[wave] = acc;
     __syncthreads();
-    if (tid == 0) {
-        ddv s = wpart[0];
-        for (int w = 1; w < NW; ++w) s = dd_add(s, wpart[w]);
-        float mean;
-        if (!rms_mean_decided(s, p.ne0, mean)) mean = rms_mean_sequential(p.a + ro, p.b ? p.b + ro : nullptr, p.ne0);
-        smean = mean;
+    if (wave == 0) {
+        double t = lane < NW ? wpart[lane] : 0.0;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) t = __dadd_rn(t, __shfl_xor(t, o, WAVE));
+        if (lane == 0) {
+            float mean;
+            if (!rms_mean_decided(t, p.ne0, mean)) mean = rms_mean_sequential(p.a + ro, p.b ? p.b + ro : nullptr, p.ne0);
+            smean = mean;
+        }
     }
     __syncthreads();
     // the ADD output is stored only now: the sequential replay above reads a and b, and the

@@ -14,11 +14,21 @@
 //     types in one launch (k_gemv_pipe2: Q4_K Q/K beside a Q6_K V);
 //   * fused epilogues: the NORM-mode RoPE of Q/K (rows 2i, 2i+1 lie in one group), f16
 //     KV-cache stores (destinations from the dynamic-pointer table, exec_ctx::dyn_slot), and
-//     optionally the SiLU of a gate projection.
+//     optionally the SiLU of a gate projection;
+//   * tail (SwiGLU): a gate/up launch also forms silu(gate) * up and its Q8_K / Q8_0 blocks for
+//     the down projection: per Q8_K block, the last of the block's row groups to finish (a
+//     device-scope arrival counter; the projection rows travel write-through, sc1) runs it.
+//     Bits as the stand-alone k_mul_quant (k_fused.hip), one launch fewer;
+//   * residual producer / norm prologue (a mat-vec followed by ADD -> RMS_NORM -> [MUL] ->
+//     mat-vec): the producer stores x = v + res instead of v and adds its rows' sum of
+//     (double)(x*x) to eight per-XCD words; every workgroup of the consumer forms the CPU's
+//     mean from them (quant_act.h rms_mean_decided), y = x * scale * w, and quantizes it into
+//     LDS as its activation.  The RMS_NORM launch disappears; nothing waits on a last arriver.
 #include "ops.h"
 #include <hip/hip_ext.h>
 #include "rope.h"
 #include "qtypes.h"
+#include "quant_act.h"
 
 namespace mi355x {
 
@@ -42,7 +52,135 @@ struct gemv_args {
     const int32_t * rope_pos; const float * rope_ff; int64_t rope_d;
     int need_pairs;
     const float2 * rtab_g;                // the graph's cos/sin table of the position (rope_table)
+    // SwiGLU tail (see above); kind 0 = none, 2 = silu(dst[gate]) * dst[up]
+    struct tail_t {
+        int kind; int64_t n;
+        int gate, up; float * silu_out; float * mul_out;
+        int qmode; int8_t * qs; float * qd; int16_t * qsum;
+        int * cnt;
+    } tl;
+    // residual producer (MODE 0, one matrix): x = v + rres[row] goes to rxsum[row] (v itself is
+    // dead), sum of (double)(x*x) to rsum[32 * (workgroup & 7)]
+    const float * rres; float * rxsum; double * rsum;
+    // norm prologue: the activation is quant(RMS_NORM(x) [* w]) formed in LDS at byte lds_off
+    struct pro_t {
+        const float * x; const float * w; const double * sum; float eps; int64_t n; int qmode; uint32_t lds_off;
+    } pro;
 };
+
+// ---- SwiGLU tail (the last workgroup of each Q8_K block) -------------------------------------------
+__device__ __forceinline__ float ld_wt(const float * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float4 ld_wt4(const float * p) { return make_float4(ld_wt(p), ld_wt(p + 1), ld_wt(p + 2), ld_wt(p + 3)); }
+
+// tail 2, one wave per finished Q8_K block: m = silu(gate) * up (ggml_vec_silu_f32's AVX-512
+// ggml_v_silu on the 16-element chunks, libm expf on the tail; vec.cpp:233), quantized
+__device__ __forceinline__ void tail_swiglu(const gemv_args & p, int blk, int lane) {
+    const auto & t = p.tl;
+    const int64_t e = 256 * (int64_t) blk + 4 * lane;
+    const float4 g = ld_wt4(p.dst[t.gate] + e), u = ld_wt4(p.dst[t.up] + e);
+    const int64_t nvec = (t.n / 16) * 16;
+    float s[4] = {g.x, g.y, g.z, g.w};
+    const float uu[4] = {u.x, u.y, u.z, u.w};
+    float m[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        s[c] = e + c < nvec ? s[c] / (1.0f + v_expf_avx512(-s[c])) : s[c] / (1.0f + expf_cr(-s[c]));
+        m[c] = __fmul_rn(s[c], uu[c]);
+    }
+    if (t.silu_out) *(float4 *) (t.silu_out + e) = make_float4(s[0], s[1], s[2], s[3]);
+    if (t.mul_out) *(float4 *) (t.mul_out + e) = make_float4(m[0], m[1], m[2], m[3]);
+    const int64_t c0 = 256 * (int64_t) blk;
+    if (t.qmode == 1) q8K_wave(m, lane, t.qs + c0, t.qsum + c0 / 16, t.qd + c0 / 256);
+    else if (t.qmode == 2) q8_0_wave(m, lane, true, t.qs + c0, t.qd + c0 / 32, t.qsum + c0 / 32);
+}
+
+// arrival: every workgroup drains its write-through stores, then one lane reports each of its
+// row groups on its Q8_K block's counter (MI355X_MICROARCH.md, inter-workgroup visibility, first
+// hand-off row); the report that completes a block's count makes this workgroup run that block.
+// Returning atomics on one word serialize at the memory side (~88 per us, MI355X_MICROARCH.md
+// dequeue row) and words of one line share that limit, so each counter owns a 4-KiB line.
+constexpr int TAIL_STRIDE = 1024;   // ints between counter words
+__device__ __forceinline__ void gemv_tail(const gemv_args & p, int kg, int64_t wg0, int64_t nwg, int rpg) {
+    const auto & t = p.tl;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int tlist[GEMV_MAXG];
+    __shared__ int tn;
+    if (threadIdx.x == 0) {
+        int n = 0;
+        const int per = 2 * (256 / rpg);   // row groups of a Q8_K block: gate and up
+        for (int k = 0; k < kg; ++k) {
+            const int64_t g = wg0 + (int64_t) k * nwg;
+            const int mi = g >= p.blk0[1] ? 1 : 0;
+            const int blk = (int) ((g - p.blk0[mi]) * rpg / 256);
+            int * c = t.cnt + blk * TAIL_STRIDE;
+            if (__hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per - 1) {
+                tlist[n++] = blk;
+                __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        tn = n;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x >> 6; i < tn; i += 4) tail_swiglu(p, tlist[i], threadIdx.x & 63);
+}
+
+// ---- norm prologue ---------------------------------------------------------------------------------
+// The consumer's activation, formed by every workgroup: mean from the producer's eight partial
+// sums (summed in a fixed order; decided, else the CPU's own loop over x), y = x * scale (* w),
+// quantized (Q8_K: q8K_row16, wave w lane l owns elements 16 (l & 15) .. +15 of block
+// 16 pass + 4 w + (l >> 4); Q8_0: q8_0_row16 over the same elements) into buf in the gemv_act layout.
+__device__ __forceinline__ void gemv_prologue(const gemv_args & p, uint8_t * buf, gemv_act & A) {
+    const auto & r = p.pro;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int NB = (int) (r.n / 256);
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s = __dadd_rn(s, r.sum[32 * k]);
+    float mean;
+    if (!rms_mean_decided(s, r.n, mean)) {   // uniform: every thread holds the same s
+        __shared__ float pmean;
+        if (tid == 0) pmean = rms_mean_sequential(r.x, nullptr, r.n);
+        __syncthreads();
+        mean = pmean;
+    }
+    const float scale = 1.0f / sqrtf(mean + r.eps);
+    int8_t * qs = (int8_t *) buf;
+    float * qd = (float *) (buf + r.n);
+    int16_t * qsum = (int16_t *) (buf + r.n + 4 * (r.qmode == 1 ? r.n / 256 : r.n / 32));
+    for (int b0 = 0; b0 < NB; b0 += 16) {
+        const int b = b0 + 4 * wave + (lane >> 4);
+        if (b >= NB) continue;   // whole rows of 16 lanes
+        const int64_t e0 = 256 * (int64_t) b + 16 * (lane & 15);
+        float4 xv[4], wv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            xv[k] = *(const float4 *) (r.x + e0 + 4 * k);
+            wv[k] = r.w ? *(const float4 *) (r.w + e0 + 4 * k) : make_float4(1.f, 1.f, 1.f, 1.f);
+        }
+        float y[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float xx[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+            const float ww[4] = {wv[k].x, wv[k].y, wv[k].z, wv[k].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float yn = __fmul_rn(xx[c], scale);
+                y[4 * k + c] = r.w ? __fmul_rn(yn, ww[c]) : yn;
+            }
+        }
+        if (r.qmode == 1) q8K_row16(y, lane, qs + 256 * (int64_t) b, qsum + 16 * (int64_t) b, qd + b);
+        else q8_0_row16(y, lane, qs + 256 * (int64_t) b, qd + 8 * (int64_t) b, qsum + 8 * (int64_t) b);
+    }
+    __syncthreads();
+    A = {qs, qd, qsum};
+}
+
+// LDS bytes of the prologue's activation (gemv_act layout, 16-B aligned pieces)
+static inline uint32_t pro_lds_bytes(int64_t n, int qmode) {
+    const int64_t nd = qmode == 1 ? n / 256 : n / 32, ns = qmode == 1 ? n / 16 : n / 32;
+    return (uint32_t) (n + 4 * nd + ((2 * ns + 15) / 16) * 16);
+}
 
 // epilogue of one output row; v = this row's value, vp = the value of its rope partner row^1
 __device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t M, int64_t row, float v, float vp,
@@ -111,7 +249,9 @@ __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_
     int64_t g = wg0;
     if (g < ngroups) fetch(g, cur);
     typename T::act x;
-    T::load(p.A, tt, x);
+    gemv_act A = p.A;
+    if (p.pro.x) gemv_prologue(p, (uint8_t *) xr + p.pro.lds_off, A);
+    T::load(A, tt, x);
     __shared__ float2 rtab[MODE ? GEMV_ROPE_MAXPAIRS : 1];
     // KV-cache destinations of the f16 epilogues, read from the dynamic-pointer table now
     // rather than as a dependent load in the epilogue
@@ -131,10 +271,21 @@ __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_
     // walker lanes: row wr of this wave's R rows, class / sub-lane ws
     const int wr = lane / T::LPR, ws = lane % T::LPR;
     const int wrc = wr < R ? wr : 0;
+    // residual producer: the residual of the walker lane's row, loaded a group ahead
+    auto res_of = [&](int64_t gg) {
+        int mi;
+        int64_t row0;
+        locate(gg, mi, row0);
+        return p.rres[min(row0 + wrc, p.M[0] - 1)];
+    };
+    float rc = 0.0f, rn = 0.0f;
+    double ss = 0.0;
+    if (MODE == 0 && p.rres && g < ngroups) rc = res_of(g);
     int par = 0, kg = 0;
     for (; g < ngroups; g += nwg, par ^= 1, ++kg) {
         const int64_t gn = g + nwg;
         if (gn < ngroups) fetch(gn, nxt);
+        if (MODE == 0 && p.rres && gn < ngroups) rn = res_of(gn);
         uint32_t * xb = xr + (size_t) par * RPG * nb * T::RS;
 #pragma unroll
         for (int r = 0; r < R; ++r) T::rec(cur[r], tt, x, active, xb + (size_t) (rowl0 + r) * nb * T::RS);
@@ -147,7 +298,17 @@ __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_
                     int mi;
                     int64_t row0;
                     locate(g, mi, row0);
-                    if (row0 + wr < p.M[mi]) p.dst[mi][row0 + wr] = v;
+                    if (row0 + wr < p.M[mi]) {
+                        if (p.rres) {   // ADD(v, res): the CPU's single f32 add
+                            const float xv = __fadd_rn(v, rc);
+                            p.rxsum[row0 + wr] = xv;
+                            ss = __dadd_rn(ss, (double) __fmul_rn(xv, xv));
+                        } else if (p.tl.kind) {
+                            __hip_atomic_store(p.dst[mi] + row0 + wr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        } else {
+                            p.dst[mi][row0 + wr] = v;
+                        }
+                    }
                 } else {
                     res[kg * RPG + rowl0 + wr] = v;
                 }
@@ -155,6 +316,21 @@ __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) cur[r] = nxt[r];
+        rc = rn;
+    }
+    if constexpr (MODE == 0) {
+        if (p.tl.kind) gemv_tail(p, kg, wg0, nwg, RPG);
+        if (p.rres) {
+            // this workgroup's rows' sum of squares to its XCD's word (no-return atomic)
+            ss = wave_sum(ss);
+            __shared__ double rpart[4];
+            if (lane == 0) rpart[wave] = ss;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const double tot = __dadd_rn(__dadd_rn(rpart[0], rpart[1]), __dadd_rn(rpart[2], rpart[3]));
+                __hip_atomic_fetch_add(p.rsum + 32 * (wg0 & 7), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
     if constexpr (MODE >= 1) {
         __syncthreads();
@@ -254,8 +430,19 @@ static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
         static const int wgs4 = getenv("GGML_MI355X_GEMV_WGS4") ? atoi(getenv("GGML_MI355X_GEMV_WGS4")) : 5 * g_num_cu;
         if (wgs4 > 0) grid = std::min<int64_t>(ng, wgs4);
     }
-    if (MODE >= 1) grid = std::max<int64_t>(grid, ceil_div(ng, GEMV_MAXG));   // LDS-parked row sums
-    const size_t lds = 4 * xrec_dwords<T>(RPG, a.ntasks / T::per_block);
+    if (a.pro.x) {
+        // every workgroup forms the activation: one resident round (GGML_MI355X_PRO_WGS), so no
+        // workgroup pays the prologue after the weight stream is under way
+        static const int pro_wgs = getenv("GGML_MI355X_PRO_WGS") ? atoi(getenv("GGML_MI355X_PRO_WGS")) : 1024;
+        if (pro_wgs > 0) grid = std::min<int64_t>(grid, pro_wgs);
+    }
+    if (MODE >= 1 || a.tl.kind) grid = std::max<int64_t>(grid, ceil_div(ng, GEMV_MAXG));   // LDS-parked row sums / tail lists
+    size_t lds = 4 * xrec_dwords<T>(RPG, a.ntasks / T::per_block);
+    if (a.pro.x) {   // the prologue's activation follows the records
+        lds = (lds + 15) / 16 * 16;
+        a.pro.lds_off = (uint32_t) lds;
+        lds += pro_lds_bytes(a.pro.n, a.pro.qmode);
+    }
     if (t_ev_beg) {
         hipExtLaunchKernelGGL((k_gemv_pipe<T, R, WPR, MODE>), dim3((unsigned) grid), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a, ng);
     } else {
@@ -265,12 +452,13 @@ static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
 
 static bool needs_epilogue(const gemv_args & a, int nmat) {
     bool epi = a.need_pairs;
-    for (int i = 0; i < nmat; ++i) epi = epi || !a.dst[i] || a.silu[i] || a.f16out[i] || a.rope_out[i] || a.rope_f16[i];
+    for (int i = 0; i < nmat; ++i) epi = epi || (!a.dst[i] && !a.rres) || a.silu[i] || a.f16out[i] || a.rope_out[i] || a.rope_f16[i];
     return epi;
 }
 
 template <class T, int R, int WPR>
 static void launch_pipe(hipStream_t st, gemv_args & a, int nmat) {
+    GGML_ASSERT(!((a.tl.kind || a.rres) && needs_epilogue(a, nmat)) && "mi355x: GEMV tail / residual with epilogues");
     if (needs_epilogue(a, nmat)) launch_pipe_m<T, R, WPR, 1>(st, a, nmat);
     else launch_pipe_m<T, R, WPR, 0>(st, a, nmat);
 }
@@ -314,8 +502,13 @@ static void launch_pipe2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a
         return std::max<int64_t>(std::min<int64_t>(ng, g_gemv_wgs), ceil_div(ng, GEMV_MAXG));   // LDS-parked row sums
     };
     const int64_t w1 = grid_of(ng1), w2 = grid_of(ng2);
-    const size_t lds = 4 * std::max(xrec_dwords<T1>((NWV / WPR) * 2, a1.ntasks / T1::per_block),
-                                     xrec_dwords<T2>((NWV / WPR) * R2, a2.ntasks / T2::per_block));
+    size_t lds = 4 * std::max(xrec_dwords<T1>((NWV / WPR) * 2, a1.ntasks / T1::per_block),
+                               xrec_dwords<T2>((NWV / WPR) * R2, a2.ntasks / T2::per_block));
+    if (a1.pro.x) {   // the prologue's activation follows the records (both bodies)
+        lds = (lds + 15) / 16 * 16;
+        a1.pro.lds_off = a2.pro.lds_off = (uint32_t) lds;
+        lds += pro_lds_bytes(a1.pro.n, a1.pro.qmode);
+    }
     if (t_ev_beg) {
         hipExtLaunchKernelGGL((k_gemv_pipe2<T1, T2, R2, WPR>), dim3((unsigned) (w1 + w2)), dim3(64 * NWV), lds, st, t_ev_beg, t_ev_end,
                               0, a1, ng1, w1, a2, ng2);
@@ -394,8 +587,9 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
     for (int i = 0; i < nmat; ++i) bytes += (double) ggml_nbytes(mms[i]->src[0]) + (double) ggml_nbytes(mms[i]);
     bytes += (double) src1->ne[0] * (kq ? 1.14 : 1.0);
 
-    q8_act act;
-    if (!ctx.qcache_get(src1, kq, act)) {
+    const bool pro = epi && epi->px;
+    q8_act act = {};
+    if (!pro && !ctx.qcache_get(src1, kq, act)) {
         quantize_act(ctx, src1, kq, act, exec_ctx::QSLOT);
         ctx.qcache_put(src1, kq, act);
     }
@@ -427,6 +621,36 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         }
     }
     a.A = {act.qs, act.d, act.s};
+    if (pro) {
+        GGML_ASSERT(epi->pn == src1->ne[0] && epi->pn % 256 == 0);
+        a.pro = {epi->px, epi->pw, epi->psum, epi->peps, epi->pn, kq ? 1 : 2, 0};
+    }
+    if (epi && epi->rres) {
+        GGML_ASSERT(nmat == 1 && epi->rsum);
+        a.rres = epi->rres; a.rxsum = epi->rxsum; a.rsum = epi->rsum;
+        a.dst[0] = nullptr;   // v is dead: only x = v + res is stored
+    }
+    // SwiGLU tail: the down projection's quantized input goes to the slot this launch does not read
+    q8_act tact = {};
+    const bool tkq = epi && epi->tq_for && is_kq(epi->tq_for->src[0]->type);
+    if (epi && epi->tail) {
+        GGML_ASSERT(ctx.tail_cnt && !needs_epilogue(a, nmat));
+        auto & t = a.tl;
+        t.kind = 2;
+        t.n = mms[epi->t_gate]->ne[0];
+        GGML_ASSERT(nmat == 2 && t.n % 256 == 0 && t.n / 256 <= exec_ctx::TAIL_CNT);
+        t.gate = epi->t_gate;
+        t.up = epi->t_up;
+        t.silu_out = epi->t_silu && epi->t_store_silu ? (float *) epi->t_silu->data : nullptr;
+        t.mul_out = epi->t_mul && epi->t_store_mul ? (float *) epi->t_mul->data : nullptr;
+        t.qmode = epi->tq_for ? (tkq ? 1 : 2) : 0;
+        if (t.qmode) {
+            const int slot = act.qs && ctx.qslot_of(act.qs) == exec_ctx::QSLOT ? exec_ctx::QSLOT2 : exec_ctx::QSLOT;
+            carve_act(tact, ctx.scratch(slot, q8_act::bytes(t.n, 1, tkq)), t.n, 1, tkq);
+            t.qs = tact.qs; t.qd = tact.d; t.qsum = tact.s;
+        }
+        t.cnt = ctx.tail_cnt;
+    }
     const int64_t nblk = src1->ne[0] / ggml_blck_size(wt);
     if (ctx.timing) {
         t_ev_beg = ctx.get_event();
@@ -451,6 +675,7 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         }
     };
     if (n2) {
+        GGML_ASSERT(!a.tl.kind);
         auto part = [&](gemv_args & d, const int * idx, int cnt) {
             d.need_pairs = 0;
             for (int k = 0; k < GEMV_MAXMAT; ++k) {
@@ -482,6 +707,26 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         ctx.pending.push_back({t_ev_beg, t_ev_end, bytes, TK_MMV});
         t_ev_beg = t_ev_end = nullptr;
     }
+    if (a.tl.qmode) ctx.qcache_put(epi->tq_key, tkq, tact);
+}
+
+// the SwiGLU tails' arrival counters exist (allocated outside any capture, zeroed once)
+bool gemv_tail_ready(exec_ctx & ctx) {
+    if (!ctx.tail_cnt && !ctx.capturing) {
+        MI_CHECK(hipMalloc(&ctx.tail_cnt, (size_t) exec_ctx::TAIL_CNT * TAIL_STRIDE * sizeof(int)));
+        MI_CHECK(hipMemsetAsync(ctx.tail_cnt, 0, (size_t) exec_ctx::TAIL_CNT * TAIL_STRIDE * sizeof(int), ctx.stream));
+    }
+    return ctx.tail_cnt != nullptr;
+}
+
+double * gemv_rsum_site(exec_ctx & ctx) {
+    if (!ctx.rsum_buf && !ctx.capturing) {
+        const size_t bytes = (size_t) exec_ctx::MAX_SITES * exec_ctx::SITE_DOUBLES * sizeof(double);
+        MI_CHECK(hipMalloc(&ctx.rsum_buf, bytes));
+        MI_CHECK(hipMemsetAsync(ctx.rsum_buf, 0, bytes, ctx.stream));
+    }
+    if (!ctx.rsum_buf || ctx.nsite >= exec_ctx::MAX_SITES) return nullptr;
+    return ctx.rsum_buf + (size_t) exec_ctx::SITE_DOUBLES * ctx.nsite++;
 }
 
 }  // namespace mi355x

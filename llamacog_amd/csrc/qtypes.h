@@ -37,9 +37,9 @@ __device__ __forceinline__ uint32_t asu(float f) { return __float_as_uint(f); }
 // hsum_float_8 over the 8 lanes s = 0..7 of a class group (lane s holds acc[s]); every lane of
 // the group ends with ((a0+a4)+(a2+a6)) + ((a1+a5)+(a3+a7))
 __device__ __forceinline__ float hsum8_lanes(float v) {
-    v = __fadd_rn(v, __shfl_xor(v, 4, WAVE));
-    v = __fadd_rn(v, __shfl_xor(v, 2, WAVE));
-    return __fadd_rn(v, __shfl_xor(v, 1, WAVE));
+    v = __fadd_rn(v, dppf_xor4(v));
+    v = __fadd_rn(v, dppf_xor2(v));
+    return __fadd_rn(v, dppf_xor1(v));
 }
 
 // class chains: lane s of the group walks acc = fma(f, cls[s], acc) over nb records of RS
@@ -127,8 +127,8 @@ struct g_q4_K {
         int sumi, summ;
         q4k_ints(w, t, x, sumi, summ);
         if (!active) sumi = summ = 0;
-        sumi += __shfl_xor(sumi, 1, WAVE); sumi += __shfl_xor(sumi, 2, WAVE);
-        summ += __shfl_xor(summ, 1, WAVE); summ += __shfl_xor(summ, 2, WAVE);
+        sumi = quad_sum(sumi);
+        summ = quad_sum(summ);
         if (active && (t & 3) == 0) {
             const float d = h2f(w.hdr.x & 0xffff), dmin = h2f(w.hdr.x >> 16);
             *(uint4 *) (rr + (t >> 2) * RS) = make_uint4((uint32_t) sumi, (uint32_t) summ, asu(d * x.dy), asu(dmin * x.dy));
@@ -211,8 +211,7 @@ struct g_q4_K_c {
         for (int i = 0; i < 8; ++i) {
             c[i] = sc_lo * dot4((int) (q[i] & 0x0f0f0f0f), x.a[i], 0) + sc_hi * dot4((int) ((q[i] >> 4) & 0x0f0f0f0f), x.a[8 + i], 0);
             if (!active) c[i] = 0;
-            c[i] += __shfl_xor(c[i], 1, WAVE);
-            c[i] += __shfl_xor(c[i], 2, WAVE);
+            c[i] = quad_sum(c[i]);
         }
         if (!active) return;
         uint32_t * r = rr + (t >> 2) * RS;
@@ -228,8 +227,8 @@ struct g_q4_K_c {
         const float acc = class_chain(rr, nb, RS, 12, s);
         float m = 0.0f;
         for (int b = 0; b < nb; ++b) m = fmaf(asf(rr[b * RS + 13]), (float) (int) rr[b * RS + 8 + (s & 3)], m);
-        float mm = __fadd_rn(m, __shfl_xor(m, 2, WAVE));   // (m0+m2), (m1+m3)
-        mm = __fadd_rn(mm, __shfl_xor(mm, 1, WAVE));
+        float mm = __fadd_rn(m, dppf_xor2(m));   // (m0+m2), (m1+m3)
+        mm = __fadd_rn(mm, dppf_xor1(mm));
         return __fadd_rn(hsum8_lanes(acc), mm);
     }
 };
@@ -263,12 +262,10 @@ struct g_q5_K {
             const uint32_t hi = ((q[i] >> 4) & 0x0f0f0f0f) | (((qh[i] >> (2 * j + 1)) & 0x01010101) << 4);
             c[i] = sc_lo * dot4((int) lo, x.a[i], 0) + sc_hi * dot4((int) hi, x.a[8 + i], 0);
             if (!active) c[i] = 0;
-            c[i] += __shfl_xor(c[i], 1, WAVE);
-            c[i] += __shfl_xor(c[i], 2, WAVE);
+            c[i] = quad_sum(c[i]);
         }
         int mn = active ? m_lo * x.bs0 + m_hi * x.bs1 : 0;
-        mn += __shfl_xor(mn, 1, WAVE);
-        mn += __shfl_xor(mn, 2, WAVE);
+        mn = quad_sum(mn);
         if (active && j == 0) {
             uint32_t * r = rr + (t >> 2) * RS;
 #pragma unroll
@@ -337,7 +334,7 @@ struct g_q6_K {
             const int s2 = dot4((int) (((L[i] >> 4) & 0x0f0f0f0f) | (((H[i] >> 4) & 0x03030303) << 4)), A2[i], N2[i]);
             const int s3 = dot4((int) (((M[i] >> 4) & 0x0f0f0f0f) | (((H[i] >> 6) & 0x03030303) << 4)), A3[i], N3[i]);
             c[i] = active ? sc0 * s0 + sc1 * s1 + sc2 * s2 + sc3 * s3 : 0;
-            c[i] += __shfl_xor(c[i], 2, WAVE);   // the other half h of the block
+            c[i] += dpp<DPP_XOR2>(c[i]);   // the other half h of the block
         }
         if (active && (t & 2) == 0) {
             uint32_t * r = rr + (t >> 2) * RS;

@@ -11,28 +11,28 @@ namespace mi355x {
 // Q8_K block (bit-exact quantize_row_q8_K_ref, ggml-quants.c:2471-2508): the first index of
 // max |x| wins, iscale = -127/max, q = min(127, nearest_int(iscale*x)), d = 1/iscale,
 // bsums over 16.  q -> the block's 256 int8, bsum -> its 16 sums, d -> its scale.
+// The reductions run on DPP / readlane (common.h): max |x| as the unsigned order of the
+// non-negative floats' bits, then the lowest index holding it (== the sequential strict '>'
+// scan), whose value is read from its lane.  All 64 lanes must be active.
 __device__ __forceinline__ void q8K_wave(const float (&vv)[4], int lane, int8_t * q, int16_t * bsum, float * d) {
-    float amax = 0.0f, vmax = 0.0f;
-    int   imax = 0x7fffffff;
+    float la = 0.0f;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float ax = fabsf(vv[k]);
-        if (ax > amax) { amax = ax; vmax = vv[k]; imax = 4 * lane + k; }
-    }
-    // wave argmax with lowest-index tie break (== sequential strict '>' scan)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float oa = __shfl_xor(amax, o, WAVE);
-        const float ov = __shfl_xor(vmax, o, WAVE);
-        const int   oi = __shfl_xor(imax, o, WAVE);
-        if (oa > amax || (oa == amax && oi < imax)) { amax = oa; vmax = ov; imax = oi; }
-    }
+    for (int k = 0; k < 4; ++k) la = fmaxf(la, fabsf(vv[k]));
+    const uint32_t abits = wave_umax(__float_as_uint(la));
+    const float amax = __uint_as_float(abits);
     if (amax == 0.0f) {
         *(uint32_t *) (q + 4 * lane) = 0;
         if (lane < 16) bsum[lane] = 0;
         if (lane == 0) *d = 0.0f;
         return;
     }
+    uint32_t cand = 0xffffffffu;
+#pragma unroll
+    for (int k = 3; k >= 0; --k) cand = fabsf(vv[k]) == amax ? (uint32_t) (4 * lane + k) : cand;
+    const uint32_t imax = wave_umin(cand);
+    const int kk = (int) (imax & 3);
+    const float vsel = kk == 0 ? vv[0] : (kk == 1 ? vv[1] : (kk == 2 ? vv[2] : vv[3]));
+    const float vmax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vsel), (int) (imax >> 2)));
     const float iscale = -127.0f / vmax;
     int s = 0;
     uint32_t packed = 0;
@@ -44,21 +44,102 @@ __device__ __forceinline__ void q8K_wave(const float (&vv)[4], int lane, int8_t 
         packed |= (uint32_t) (iv & 0xff) << (8 * k);
     }
     *(uint32_t *) (q + 4 * lane) = packed;
-    s += __shfl_xor(s, 1, WAVE);
-    s += __shfl_xor(s, 2, WAVE);
+    s = quad_sum(s);
     if ((lane & 3) == 0) bsum[lane >> 2] = (int16_t) s;
     if (lane == 0) *d = 1.0f / iscale;
 }
 
+// The same Q8_K block over 16 lanes (a DPP row), lane j = lane & 15 holding elements
+// 16j .. 16j+15: four blocks per wave, reductions within the row only (no readlane), and the
+// lane's 16 quantized values are exactly its 16-sum.  Bits as q8K_wave.
+__device__ __forceinline__ void q8K_row16(const float (&v)[16], int lane, int8_t * q, int16_t * bsum, float * d) {
+    const int j = lane & 15;
+    float la = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) la = fmaxf(la, fabsf(v[i]));
+    uint32_t ab = __float_as_uint(la);
+    ab = max(ab, (uint32_t) dpp<DPP_XOR1>((int) ab));
+    ab = max(ab, (uint32_t) dpp<DPP_XOR2>((int) ab));
+    ab = max(ab, (uint32_t) dpp<DPP_HMIRROR>((int) ab));
+    ab = max(ab, (uint32_t) dpp<DPP_MIRROR>((int) ab));
+    const float amax = __uint_as_float(ab);
+    if (amax == 0.0f) {
+        *(uint4 *) (q + 16 * j) = make_uint4(0, 0, 0, 0);
+        bsum[j] = 0;
+        if (j == 0) *d = 0.0f;
+        return;
+    }
+    // the first index holding max |x| (the CPU's strict '>' scan) and its value
+    uint32_t cand = 0xffffffffu;
+    float mine = 0.0f;
+#pragma unroll
+    for (int i = 15; i >= 0; --i) {
+        if (fabsf(v[i]) == amax) { cand = (uint32_t) (16 * j + i); mine = v[i]; }
+    }
+    uint32_t im = cand;
+    im = min(im, (uint32_t) dpp<DPP_XOR1>((int) im));
+    im = min(im, (uint32_t) dpp<DPP_XOR2>((int) im));
+    im = min(im, (uint32_t) dpp<DPP_HMIRROR>((int) im));
+    im = min(im, (uint32_t) dpp<DPP_MIRROR>((int) im));
+    int vb = (int) (im >> 4) == j ? __float_as_int(mine) : 0;   // one lane of the row holds it
+    vb |= dpp<DPP_XOR1>(vb);
+    vb |= dpp<DPP_XOR2>(vb);
+    vb |= dpp<DPP_HMIRROR>(vb);
+    vb |= dpp<DPP_MIRROR>(vb);
+    const float iscale = -127.0f / __int_as_float(vb);
+    int s = 0;
+    uint32_t pk[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        int iv = (int) rintf(__fmul_rn(iscale, v[i]));   // nearest_int: round-half-even
+        iv = iv < 127 ? iv : 127;
+        s += iv;
+        pk[i >> 2] |= (uint32_t) (iv & 0xff) << (8 * (i & 3));
+    }
+    *(uint4 *) (q + 16 * j) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    bsum[j] = (int16_t) s;
+    if (j == 0) *d = 1.0f / iscale;
+}
+
+// Eight Q8_0 blocks of 256 elements over 16 lanes, lane j holding elements 16j .. 16j+15 (half
+// of block j >> 1, the partner half in lane j ^ 1).  Bits as q8_0_wave.
+__device__ __forceinline__ void q8_0_row16(const float (&v)[16], int lane, int8_t * q, float * d, int16_t * s8) {
+    const int j = lane & 15;
+    float la = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) la = fmaxf(la, fabsf(v[i]));
+    uint32_t ab = __float_as_uint(la);
+    ab = max(ab, (uint32_t) dpp<DPP_XOR1>((int) ab));
+    const float amax = __uint_as_float(ab);
+    const float dd = amax / 127.0f;
+    const float id = amax != 0.0f ? 127.0f / amax : 0.0f;
+    int s = 0;
+    uint32_t pk[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        int iv = (int) rintf(__fmul_rn(v[i], id));
+        iv = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
+        s += iv;
+        pk[i >> 2] |= (uint32_t) (iv & 0xff) << (8 * (i & 3));
+    }
+    s += dpp<DPP_XOR1>(s);
+    *(uint4 *) (q + 16 * j) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    if ((j & 1) == 0) {
+        d[j >> 1]  = h2f(f2h(dd));
+        s8[j >> 1] = (int16_t) s;
+    }
+}
+
 // eight Q8_0 blocks with the x86 AVX rounding (ggml-cpu/arch/x86/quants.c:278-372):
 // d = amax/127, id = 127/amax, q = round-half-even(x*id); d is stored as fp16 by the CPU,
-// so the fp16-rounded value is kept.  Eight lanes per 32-block.  `valid` = lane's
-// elements exist (rows that are not a multiple of 256).
+// so the fp16-rounded value is kept.  Eight lanes per 32-block (DPP within the 8).  `valid` =
+// lane's elements exist (rows that are not a multiple of 256).  All 64 lanes must be active.
 __device__ __forceinline__ void q8_0_wave(const float (&vv)[4], int lane, bool valid, int8_t * q, float * d, int16_t * s8) {
-    float amax = fmaxf(fmaxf(fabsf(vv[0]), fabsf(vv[1])), fmaxf(fabsf(vv[2]), fabsf(vv[3])));
-    amax = fmaxf(amax, __shfl_xor(amax, 1, WAVE));
-    amax = fmaxf(amax, __shfl_xor(amax, 2, WAVE));
-    amax = fmaxf(amax, __shfl_xor(amax, 4, WAVE));
+    uint32_t ab = __float_as_uint(fmaxf(fmaxf(fabsf(vv[0]), fabsf(vv[1])), fmaxf(fabsf(vv[2]), fabsf(vv[3]))));
+    ab = max(ab, (uint32_t) dpp<DPP_XOR1>((int) ab));
+    ab = max(ab, (uint32_t) dpp<DPP_XOR2>((int) ab));
+    ab = max(ab, (uint32_t) dpp<DPP_HMIRROR>((int) ab));
+    const float amax = __uint_as_float(ab);
     const float dd = amax / 127.0f;
     const float id = amax != 0.0f ? 127.0f / amax : 0.0f;
     int s = 0;
@@ -70,9 +151,7 @@ __device__ __forceinline__ void q8_0_wave(const float (&vv)[4], int lane, bool v
         s += iv;
         packed |= (uint32_t) (iv & 0xff) << (8 * k);
     }
-    s += __shfl_xor(s, 1, WAVE);
-    s += __shfl_xor(s, 2, WAVE);
-    s += __shfl_xor(s, 4, WAVE);
+    s = oct_sum(s);
     if (valid) {
         *(uint32_t *) (q + 4 * lane) = packed;
         if ((lane & 7) == 0) {
@@ -85,41 +164,22 @@ __device__ __forceinline__ void q8_0_wave(const float (&vv)[4], int lane, bool v
 // ---- RMS-norm mean, exactly as the CPU forms it -----------------------------------------------
 // rms_norm_f32 (ggml-cpu/ops.cpp:3270-3316) sums (double)(x*x) over the row SEQUENTIALLY in
 // double, then mean = (float)(sum / ne0).  A parallel sum rounds differently, and on rare rows
-// that difference flips the float mean.  Here every thread sums its terms in double-double
-// (error ~2^-106 of the sum), the partials are combined the same way, and the float mean is
-// taken from that near-exact sum when the rounding is decided: the sequential double sum of n
-// non-negative terms lies within (n-1)·2^-53 of the exact one (relative), so when both ends of
-// [m(1 - tol), m(1 + tol)] round to the same float the CPU's mean is that float.  Otherwise (a
-// fraction ~1e-5 of rows) one thread replays the CPU's sequential loop.
-struct ddv { double hi, lo; };
-
-__device__ __forceinline__ ddv dd_add(ddv a, double b) {   // a + b (TwoSum, then renormalise)
-    const double s = __dadd_rn(a.hi, b);
-    const double bb = __dsub_rn(s, a.hi);
-    const double e = __dadd_rn(__dsub_rn(a.hi, __dsub_rn(s, bb)), __dsub_rn(b, bb));
-    const double lo = __dadd_rn(a.lo, e);
-    const double hi = __dadd_rn(s, lo);
-    return ddv{hi, __dsub_rn(lo, __dsub_rn(hi, s))};
-}
-__device__ __forceinline__ ddv dd_add(ddv a, ddv b) { return dd_add(dd_add(a, b.hi), b.lo); }
-
-__device__ __forceinline__ ddv dd_wave_sum(ddv v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = dd_add(v, ddv{__shfl_xor(v.hi, o, WAVE), __shfl_xor(v.lo, o, WAVE)});
-    return v;
+// that difference flips the float mean.  Both sums are of n non-negative terms, so each lies
+// within (additions a term passes through)·2^-53 of the exact sum, relatively: (n-1)·2^-53 for
+// the CPU's loop, a few dozen ulps for the parallel tree here.  When both ends of
+// [m(1 - tol), m(1 + tol)], tol covering the two, round to the same float, that float is the
+// CPU's mean; otherwise (a fraction ~1e-5 of rows) one thread replays the CPU's loop.
+__device__ __forceinline__ double sq4(const float4 x) {   // (double)(x*x) of four elements, summed
+    double q = (double) __fmul_rn(x.x, x.x);
+    q = __dadd_rn(q, (double) __fmul_rn(x.y, x.y));
+    q = __dadd_rn(q, (double) __fmul_rn(x.z, x.z));
+    return __dadd_rn(q, (double) __fmul_rn(x.w, x.w));
 }
 
-__device__ __forceinline__ ddv dd_sq4(ddv acc, const float4 x) {   // + the four terms (double)(x*x)
-    acc = dd_add(acc, (double) __fmul_rn(x.x, x.x));
-    acc = dd_add(acc, (double) __fmul_rn(x.y, x.y));
-    acc = dd_add(acc, (double) __fmul_rn(x.z, x.z));
-    return dd_add(acc, (double) __fmul_rn(x.w, x.w));
-}
-
-// the float mean from the near-exact sum; false when the rounding is not decided
-__device__ __forceinline__ bool rms_mean_decided(ddv s, int64_t n, float & mean) {
-    const double m = __ddiv_rn(__dadd_rn(s.hi, s.lo), (double) n);
-    const double tol = (double) (n + 8) * 0x1p-53;
+// the float mean from a parallel double sum s of n terms; false when the rounding is not decided
+__device__ __forceinline__ bool rms_mean_decided(double s, int64_t n, float & mean) {
+    const double m = __ddiv_rn(s, (double) n);
+    const double tol = (double) (2 * n + 64) * 0x1p-53;   // CPU loop (n - 1) + this tree (<= n + 16) + 3 roundings
     const float f0 = (float) __dmul_rn(m, 1.0 - tol), f1 = (float) __dmul_rn(m, 1.0 + tol);
     mean = (float) m;
     return f0 == f1;
