@@ -187,6 +187,7 @@ def main():
     wbytes = gguf_synth.weight_bytes_per_token(
         gguf_synth.ModelConfig(**{**cfg.__dict__, "n_layer": a.layers or cfg.n_layer}))
 
+    gstats = la.graph_stats()
     m.close()
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
@@ -253,6 +254,7 @@ def main():
                               "llama_decode_call": round(1e3 * t_dec / a.steps, 4),
                               "llama_synchronize_call": round(1e3 * t_syn / a.steps, 4)},
             "cpu_baseline": cpu,
+            "hipgraph": dict(zip(("captures", "replays"), gstats)),
         }
         print(json.dumps(out))
     dist.close()

@@ -21,7 +21,7 @@
 //     Bits as the stand-alone k_mul_quant (k_fused.hip), one launch fewer;
 //   * residual producer / norm prologue (a mat-vec followed by ADD -> RMS_NORM -> [MUL] ->
 //     mat-vec): the producer stores x = v + res instead of v and adds its rows' sum of
-//     (double)(x*x) to eight per-XCD words; every workgroup of the consumer forms the CPU's
+//     (double)(x*x) to one of 64 words; every workgroup of the consumer forms the CPU's
 //     mean from them (quant_act.h rms_mean_decided), y = x * scale * w, and quantizes it into
 //     LDS as its activation.  The RMS_NORM launch disappears; nothing waits on a last arriver.
 #include "ops.h"
@@ -60,13 +60,18 @@ struct gemv_args {
         int * cnt;
     } tl;
     // residual producer (MODE 0, one matrix): x = v + rres[row] goes to rxsum[row] (v itself is
-    // dead), sum of (double)(x*x) to rsum[32 * (workgroup & 7)]
+    // dead), sum of (double)(x*x) to rsum[RSUM_STRIDE * (workgroup % RSUM_SHARDS)]
     const float * rres; float * rxsum; double * rsum;
     // norm prologue: the activation is quant(RMS_NORM(x) [* w]) formed in LDS at byte lds_off
     struct pro_t {
         const float * x; const float * w; const double * sum; float eps; int64_t n; int qmode; uint32_t lds_off;
     } pro;
 };
+
+// the producer's partial sums: no-return f64 atomics serialize per 128-B line at the memory
+// side (MI355X_MICROARCH.md dequeue row), so 64 shards, one line each, keep each line's count
+// of adds (workgroups / 64) small
+constexpr int RSUM_SHARDS = 64, RSUM_STRIDE = 16;   // doubles
 
 // ---- SwiGLU tail (the last workgroup of each Q8_K block) -------------------------------------------
 __device__ __forceinline__ float ld_wt(const float * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -126,7 +131,7 @@ __device__ __forceinline__ void gemv_tail(const gemv_args & p, int kg, int64_t w
 }
 
 // ---- norm prologue ---------------------------------------------------------------------------------
-// The consumer's activation, formed by every workgroup: mean from the producer's eight partial
+// The consumer's activation, formed by every workgroup: mean from the producer's 64 partial
 // sums (summed in a fixed order; decided, else the CPU's own loop over x), y = x * scale (* w),
 // quantized (Q8_K: q8K_row16, wave w lane l owns elements 16 (l & 15) .. +15 of block
 // 16 pass + 4 w + (l >> 4); Q8_0: q8_0_row16 over the same elements) into buf in the gemv_act layout.
@@ -134,9 +139,8 @@ __device__ __forceinline__ void gemv_prologue(const gemv_args & p, uint8_t * buf
     const auto & r = p.pro;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int NB = (int) (r.n / 256);
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s = __dadd_rn(s, r.sum[32 * k]);
+    static_assert(RSUM_SHARDS == WAVE, "one shard per lane");
+    const double s = wave_sum(r.sum[RSUM_STRIDE * lane]);   // a fixed tree: the same s in every workgroup
     float mean;
     if (!rms_mean_decided(s, r.n, mean)) {   // uniform: every thread holds the same s
         __shared__ float pmean;
@@ -321,14 +325,16 @@ __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_
     if constexpr (MODE == 0) {
         if (p.tl.kind) gemv_tail(p, kg, wg0, nwg, RPG);
         if (p.rres) {
-            // this workgroup's rows' sum of squares to its XCD's word (no-return atomic)
-            ss = wave_sum(ss);
-            __shared__ double rpart[4];
-            if (lane == 0) rpart[wave] = ss;
+            // this workgroup's rows' sum of squares (RPG walker lanes hold partials) to its shard
+            // (no-return atomic)
+            __shared__ double rpart[RPG];
+            if (wsub == 0 && wr < R && ws == 0) rpart[rowl0 + wr] = ss;
             __syncthreads();
             if (threadIdx.x == 0) {
-                const double tot = __dadd_rn(__dadd_rn(rpart[0], rpart[1]), __dadd_rn(rpart[2], rpart[3]));
-                __hip_atomic_fetch_add(p.rsum + 32 * (wg0 & 7), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                double tot = 0.0;
+#pragma unroll
+                for (int k = 0; k < RPG; ++k) tot = __dadd_rn(tot, rpart[k]);
+                __hip_atomic_fetch_add(p.rsum + RSUM_STRIDE * (wg0 % RSUM_SHARDS), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }

@@ -45,10 +45,10 @@ struct exec_ctx {
     // producer chain), TAIL_CNT words each on its own 4-KiB line; zeroed once, self-resetting
     static constexpr int TAIL_CNT = 256;
     int *   tail_cnt = nullptr;
-    // residual producer -> norm prologue hand-off (k_gemv.hip): per site eight per-XCD double
-    // sums (256-B apart) that the producer's workgroups add to and the consumer's read; zeroed
-    // at the end of every graph (run_nodes), so each graph starts from zero
-    static constexpr int MAX_SITES = 256, SITE_DOUBLES = 256;
+    // residual producer -> norm prologue hand-off (k_gemv.hip): per site 64 double sums (128 B
+    // apart) that the producer's workgroups add to and the consumer's read; zeroed at the end of
+    // every graph (run_nodes), so each graph starts from zero
+    static constexpr int MAX_SITES = 256, SITE_DOUBLES = 1024;
     double * rsum_buf = nullptr;
     int      nsite = 0;
     // the pending prologue: RMS_NORM chain `last` (and its data pointer) whose consumers form
