@@ -7,13 +7,18 @@ the MI355X plugin loaded.  A "step" is one single-token llama_decode (n_batch = 
 BASELINE.json configs[1] decode workload); K timed steps are bracketed by a barrier and a
 device synchronisation, the max over ranks is taken, and rank 0 prints one JSON line.
 
-Multi-GPU: the decode path of one stream does not shard (layer split is sequential,
-SURVEY.md §8(e)), so --gpus N runs N independent replicas, one process per GPU
-("replicas only", weak scaling); value = N*K / max-rank time.
+Multi-GPU (BASELINE.json configs[3]): --gpus N > 1 runs Llama-3-70B Q4_K_M
+split by layers over N devices in ONE process (libllama -sm layer; our backend is one device
+per GPU and the stage hand-off between devices is an RCCL ncclSend/ncclRecv pair,
+backend.cpp cpy_tensor_async).  Under torch.distributed.run (one process per GPU, as the
+driver launches it) rank 0 owns all N devices and the other ranks only join the barriers and
+the max; value = the single stream's tok/s ("strong": fixed work, more devices).  N = 1 is the
+8B headline workload.  --cpu runs the harness on the CPU backend (tests only).
 
-Extra objects on the line: "roofline" (the dominant kernel — the quantized mat-vec —
-timed with HIP events on the plugin's stream) and "cpu_baseline" (the reference's own
-llama-bench on the CPU backend, a bounded tg sample on the same host).
+Extra objects on the line: "roofline" (the dominant kernel — the quantized mat-vec — timed
+with HIP events on the plugin's stream; fractions against the measured STREAM-read peak and
+the 8 TB/s nominal) and "cpu_baseline" (the reference's own llama-bench on the CPU backend,
+BASELINE.md §3: physical cores of this process's CPU set, -r 5, tg128 and pp512).
 """
 from __future__ import annotations
 
@@ -28,7 +33,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-MFMA_I8_PEAK_TOPS = 2500.0   # dense int8 MFMA, no sparsity (MI355X_MICROARCH.md)
+# dense int8 MFMA, no sparsity: 2x the dense BF16 2.5 PFLOP/s (MI355X_MICROARCH.md, matrix cores)
+MFMA_I8_PEAK_TOPS = 5000.0
 # algorithmic work of one pp512 of Llama-3-8B: 2*6.98e9*512 layer matmuls +
 # output (last token) + attention
 PP512_FLOP = 7.22e12
@@ -40,18 +46,23 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--config", default="llama3-8b-q4km")
+    ap.add_argument("--config", default=None, help="default: llama3-8b-q4km at --gpus 1, llama3-70b-q4km above")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only)")
     ap.add_argument("--pp", type=int, default=512, help="prompt length for the pp figure (0 = skip)")
     ap.add_argument("--fa", type=int, default=1)
     ap.add_argument("--kv", default="f16")
+    ap.add_argument("--depth", type=int, default=0, help="KV depth before the timed steps (llama-bench -d)")
     ap.add_argument("--roofline-steps", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-gen", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = physical cores of this process's CPU set")
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--cpu", action="store_true", help="run the harness on the CPU backend (tests)")
     ap.add_argument("--model-dir", default=os.environ.get("LLAMACOG_MODEL_DIR", "/tmp/llamacog_amd_models"))
     ap.add_argument("--verbose", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config is None:
+        a.config = "llama3-70b-q4km" if a.gpus > 1 else "llama3-8b-q4km"
+    return a
 
 
 def dist_env():
@@ -63,11 +74,10 @@ def dist_env():
 
 class Dist:
     """Barrier / max-reduction over ranks (gloo on host memory; the timed work itself runs
-    on the plugin's HIP stream and is synchronised by llama_synchronize)."""
+    on the plugin's HIP streams and is synchronised by llama_synchronize)."""
 
     def __init__(self, ws: int):
         self.ws = ws
-        self.pg = None
         if ws > 1:
             import torch.distributed as dist
             dist.init_process_group("gloo")
@@ -90,31 +100,67 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(model: str, threads: int, n_gen: int, fa: int) -> dict:
+def physical_cores() -> tuple[int, str]:
+    """Physical cores of this process's CPU set (SMT siblings counted once), capped by the
+    thread budget the box grants (OMP_NUM_THREADS), and the lscpu topology for the record."""
+    cpus = sorted(os.sched_getaffinity(0))
+    cores = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            cores.add((pkg, core))
+        except OSError:
+            cores.add(("?", str(c)))
+    n = len(cores)
+    budget = os.environ.get("OMP_NUM_THREADS")
+    if budget and budget.isdigit():
+        n = min(n, int(budget))
+    topo = "?"
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = dict(l.split(":", 1) for l in out.splitlines() if ":" in l)
+        topo = (f"{kv.get('Model name', '?').strip()}: {kv.get('Socket(s)', '?').strip()} sockets x "
+                f"{kv.get('Core(s) per socket', '?').strip()} cores x {kv.get('Thread(s) per core', '?').strip()} threads; "
+                f"this process: {len(cpus)} CPUs = {len(cores)} physical cores")
+    except Exception:
+        pass
+    return max(n, 1), topo
+
+
+def cpu_baseline(model: str, threads: int, reps: int, fa: int) -> dict:
     """The reference's ggml-cpu path (refhost/build/llama-bench, score-selected CPU variant,
-    our plugin NOT loaded) on a bounded tg sample of the same model on this host."""
+    our plugin NOT loaded) on the same model: pp512 and tg128, -r reps."""
     exe = os.path.join(REPO, "refhost", "build", "llama-bench")
     env = {k: v for k, v in os.environ.items() if k != "GGML_BACKEND_PATH"}
-    cmd = [exe, "-m", model, "-p", "0", "-n", str(n_gen), "-r", "1", "-t", str(threads), "-fa", str(fa), "-o", "json"]
+    cores, topo = physical_cores()
+    threads = threads or cores
+    cmd = [exe, "-m", model, "-p", "512", "-n", "128", "-r", str(reps), "-t", str(threads), "-fa", str(fa), "-o", "json"]
     t0 = time.time()
-    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=1200)
     if out.returncode != 0:
         return {"value": None, "unit": "tok/s", "cores": threads, "kind": "reference",
                 "sample": f"llama-bench failed rc={out.returncode}: {out.stderr[-300:]}"}
     rows = json.loads(out.stdout)
-    r = rows[0]
-    return {"value": round(float(r["avg_ts"]), 3), "unit": "tok/s", "cores": threads, "kind": "reference",
-            "sample": f"reference llama-bench (ggml-cpu, {r.get('cpu_info', '?')}) tg{n_gen} x1 rep, -t {threads}, "
-                      f"-fa {fa}, same synthetic GGUF; wall {time.time() - t0:.1f}s incl. load"}
+    tg = next(r for r in rows if r.get("n_gen", 0) > 0)
+    pp = next((r for r in rows if r.get("n_prompt", 0) > 0), None)
+    return {"value": round(float(tg["avg_ts"]), 3), "unit": "tok/s", "cores": threads, "kind": "reference",
+            "tg_stddev": round(float(tg.get("stddev_ts", 0.0)), 3),
+            "pp512_tok_s": round(float(pp["avg_ts"]), 2) if pp else None,
+            "sample": f"reference llama-bench (ggml-cpu, {tg.get('cpu_info', '?')}) -p 512 -n 128 -r {reps} -t {threads} "
+                      f"-fa {fa}, same synthetic GGUF; {topo}; wall {time.time() - t0:.1f}s incl. load"}
 
 
 def main():
     a = parse()
     ws, rank, lrank = dist_env()
-    if ws > 1:
-        # one process per GPU: restrict this rank's HIP runtime (and so the plugin's
-        # device list) to its own GPU before anything touches HIP
+    split = a.gpus > 1                   # one stream, layers split over a.gpus devices
+    if ws > 1 and not split:
+        # replicas: restrict each rank's HIP runtime to its own GPU before anything touches HIP
         os.environ["HIP_VISIBLE_DEVICES"] = str(lrank)
+    worker = (rank == 0) or not split    # in split mode rank 0 owns every device
     dist = Dist(ws)
 
     import llamacog_amd as la
@@ -130,134 +176,180 @@ def main():
             print(f"[bench] wrote {path} in {time.time() - t0:.1f}s", file=sys.stderr)
     dist.barrier()
 
-    n_ctx = ((a.warmup + a.steps + max(a.pp, 0) + a.roofline_steps + 255) // 256 + 1) * 256
-    m = la.Model(path, gpu=True, n_ctx=n_ctx, flash_attn=bool(a.fa), kv_type=a.kv, n_gpus=1)
-    plugin = la.plugin_lib()
-    if a.verbose and rank == 0:
+    gpu = not a.cpu
+    n_ctx = ((a.warmup + a.steps + a.depth + max(a.pp, 0) + a.roofline_steps + 255) // 256 + 1) * 256
+    res = {}
+    if worker:
+        res = run_worker(a, la, path, gpu, n_ctx, split, dist)
+    else:
+        dist.barrier()                   # the worker's tg start
+        dist.barrier()                   # its end
+        dist.max(0.0)
+    if rank == 0:
+        emit(a, la, gguf_synth, cfg, suffix, ws, split, gpu, n_ctx, res)
+    dist.close()
+
+
+def run_worker(a, la, path, gpu, n_ctx, split, dist) -> dict:
+    r = {}
+    m = la.Model(path, gpu=gpu, n_ctx=n_ctx, flash_attn=bool(a.fa), kv_type=a.kv,
+                 n_gpus=(a.gpus if split else 1) if gpu else None, split_mode=1)
+    plugin = la.plugin_lib() if gpu else None
+    if a.verbose:
         print(la.log_tail(m.lib)[-4000:], file=sys.stderr)
 
     # pp figure (one ubatch of a.pp tokens, as llama-bench pp512)
-    pp_tps = None
+    r["pp_tps"] = None
     if a.pp > 0:
         m.clear()
         m.time_prompt(min(a.pp, 64))  # warm
         m.clear()
-        tpp = m.time_prompt(a.pp)
-        pp_tps = a.pp / tpp
+        r["pp_tps"] = a.pp / m.time_prompt(a.pp)
 
-    # tg: W untimed decode steps, then exactly K timed steps
-    m.clear()
+    # tg: W untimed decode steps (after a.depth prompt tokens), then exactly K timed steps
+    def fill():
+        m.clear()
+        if a.depth > 0:
+            m.time_prompt(a.depth)
+    fill()
     if a.warmup > 0:
         m.time_gen(a.warmup)
     dist.barrier()
     t_local = m.time_gen(a.steps)   # each step ends in llama_synchronize (device sync)
     dist.barrier()
-    t = dist.max(t_local)
-    value = ws * a.steps / t
+    r["t"] = dist.max(t_local)
+    r["t_local"] = t_local
 
-    # where a step's wall time goes: host work inside llama_decode (libllama graph build,
-    # scheduling, input upload, our graph_compute and launch) vs waiting in llama_synchronize
-    m.clear()
-    m.time_gen(4)
-    plugin.ggml_backend_mi355x_reset_timing()
-    plugin.ggml_backend_mi355x_set_graph_timing(1)
-    t_sp, t_dec, t_syn = m.time_gen_split(a.steps)
-    plugin.ggml_backend_mi355x_set_graph_timing(0)
-    g_ms, _, g_n = la.kernel_timing(plugin, 5)    # device time of each graph_compute (events around it)
-    gh_ms, _, gh_n = la.kernel_timing(plugin, 6)  # host time inside graph_compute
+    r["split"] = r["roof"] = None
+    if gpu:
+        # where a step's wall time goes: host work inside llama_decode (libllama graph build,
+        # scheduling, input upload, our graph_compute and launch) vs waiting in llama_synchronize
+        fill()
+        m.time_gen(4)
+        plugin.ggml_backend_mi355x_reset_timing()
+        plugin.ggml_backend_mi355x_set_graph_timing(1)
+        t_sp, t_dec, t_syn = m.time_gen_split(a.steps)
+        plugin.ggml_backend_mi355x_set_graph_timing(0)
+        g_ms, _, g_n = la.kernel_timing(plugin, 5)    # device time of each graph_compute (events around it)
+        gh_ms, _, gh_n = la.kernel_timing(plugin, 6)  # host time inside graph_compute
+        r["split"] = {"wall": round(1e3 * t_sp / a.steps, 4),
+                      "device_graph": round(g_ms / a.steps, 4) if g_n else None,
+                      "graph_compute_host": round(gh_ms / a.steps, 4) if gh_n else None,
+                      "llama_decode_call": round(1e3 * t_dec / a.steps, 4),
+                      "llama_synchronize_call": round(1e3 * t_syn / a.steps, 4)}
 
-    # roofline pass: HIP events around every mat-vec launch on the plugin stream
-    m.clear()
-    m.time_gen(4)
-    plugin.ggml_backend_mi355x_reset_timing()
-    plugin.ggml_backend_mi355x_set_timing(1)
-    t_rf = m.time_gen(a.roofline_steps)
-    plugin.ggml_backend_mi355x_set_timing(0)
-    mv_ms, mv_bytes, mv_n = la.kernel_timing(plugin, 0)
-    fa_ms, fa_bytes, fa_n = la.kernel_timing(plugin, 2)
-    achieved = (mv_bytes / (mv_ms * 1e-3)) / 1e9 if mv_ms > 0 else None
-    # HBM bytes per GEMV launch from the PMC pass (rocprofv3 --pmc FETCH_SIZE, x2 gfx950
-    # correction), committed with its command under profiles/ (scripts/gpu_final.sh, scripts/pmc_traffic.py)
-    traffic = None
-    if os.path.exists(TRAFFIC_FILE):
+        # roofline pass: HIP events around every mat-vec launch on the plugin streams
+        fill()
+        m.time_gen(4)
+        plugin.ggml_backend_mi355x_reset_timing()
+        plugin.ggml_backend_mi355x_set_timing(1)
+        t_rf = m.time_gen(a.roofline_steps) if a.roofline_steps > 0 else 0.0
+        plugin.ggml_backend_mi355x_set_timing(0)
+        mv_ms, mv_bytes, mv_n = la.kernel_timing(plugin, 0)
+        fa_ms, _, fa_n = la.kernel_timing(plugin, 2)
+        r["roof"] = (mv_ms, mv_bytes, mv_n, fa_ms, fa_n, t_rf)
+        r["gstats"] = la.graph_stats()
+        r["p2p"] = la.p2p_stats()
+    m.close()
+    if gpu:
+        # the measured STREAM-read ceiling of device 0 (k_stream.hip), after the model is gone
+        r["hbm_gbs"] = la.hbm_read_gbs(0)
+    r["cpu"] = None
+    if not a.no_cpu_baseline and not split and not a.cpu:
         try:
-            traffic = json.load(open(TRAFFIC_FILE)).get("gemv_bytes_per_launch")
-        except Exception:
-            traffic = None
+            r["cpu"] = cpu_baseline(path, a.cpu_threads, a.cpu_reps, a.fa)
+        except Exception as e:  # the baseline must never hide the GPU result
+            r["cpu"] = {"value": None, "unit": "tok/s", "cores": a.cpu_threads, "kind": "reference", "sample": f"error: {e}"}
+    return r
+
+
+def emit(a, la, gguf_synth, cfg, suffix, ws, split, gpu, n_ctx, r):
+    t = r["t"]
+    n_units = a.gpus if split else ws          # devices in the job
+    streams = 1 if split else ws               # independent decode streams
+    value = streams * a.steps / t
     wbytes = gguf_synth.weight_bytes_per_token(
         gguf_synth.ModelConfig(**{**cfg.__dict__, "n_layer": a.layers or cfg.n_layer}))
-
-    gstats = la.graph_stats()
-    m.close()
-    cpu = None
-    if rank == 0 and not a.no_cpu_baseline:
-        try:
-            cpu = cpu_baseline(path, a.cpu_threads, a.cpu_gen, a.fa)
-        except Exception as e:  # the baseline must never hide the GPU result
-            cpu = {"value": None, "unit": "tok/s", "cores": a.cpu_threads, "kind": "reference", "sample": f"error: {e}"}
-
-    if rank == 0:
-        out = {
-            "metric": "llama-bench tg128 + pp512 tok/s, Llama-3-8B Q4_K_M; 1/2/4/8 GPU",
-            "value": round(value, 3),
-            "unit": "tok/s",
-            "n_gpus": ws,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(1e3 * t / a.steps, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "i8",
-            "data": "synthetic",
-            "config": {
-                "workload": f"{cfg.name} ({a.config}{suffix}) tg: n_batch=1 single-token llama_decode, "
-                            f"fa={a.fa}, kv={a.kv}, n_ctx={n_ctx}; random-but-valid Q4_K/Q6_K blocks",
-                "model": a.config + suffix,
-                "global_batch": ws,
-                "seq_len": a.warmup + a.steps,
-                "parallelism": f"replicas x{ws}" if ws > 1 else "single GPU",
-            },
-            "pp_tok_s": round(pp_tps, 2) if pp_tps else None,
-            "pp_tokens": a.pp,
-            "pp_roofline": ({"bound": "mfma", "unit": "TFLOP/s", "peak": MFMA_I8_PEAK_TOPS,
-                             "achieved": round(PP512_FLOP / (a.pp / pp_tps) / 1e12, 2),
-                             "frac": round(PP512_FLOP / (a.pp / pp_tps) / 1e12 / MFMA_I8_PEAK_TOPS, 4),
-                             "note": "whole pp512 (all kernels), Llama-3-8B algorithmic FLOPs"}
-                            if (pp_tps and a.pp == 512 and a.config == "llama3-8b-q4km" and not a.layers) else None),
-            "weight_bytes_per_token": wbytes,
-            "model_bw_GBs": round(wbytes * (a.steps / t_local) / 1e9, 1),
-            "model_bw_frac_of_8TBs": round(wbytes * (a.steps / t_local) / 1e9 / HBM_PEAK_GBS, 4),
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_gemv_pipe (quantized decode GEMV, every decode MUL_MAT)",
-                "achieved": round(achieved, 1) if achieved else None,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": traffic,
-                "traffic_source": "profiles/r01/pmc_traffic.json" if traffic else None,
-                "launches": mv_n,
-                "avg_launch_us": round(1e3 * mv_ms / mv_n, 3) if mv_n else None,
-                "algorithmic_bytes_per_launch": round(mv_bytes / mv_n) if mv_n else None,
-                "measured_over_steps": a.roofline_steps,
-                "fattn_avg_us": round(1e3 * fa_ms / fa_n, 3) if fa_n else None,
-                "timed_pass_tok_s": round(a.roofline_steps / t_rf, 2),
-            },
-            # wall = one llama_decode + llama_synchronize; device_graph = GPU time of the graph
-            # (events before/after graph_compute's launches); graph_compute_host = host time in
-            # our graph_compute (signature, KV-slot table upload, hipGraph launch); the rest of the
-            # wall is libllama's host work (graph build, scheduling, input upload, logits copy)
-            "step_split_ms": {"wall": round(1e3 * t_sp / a.steps, 4),
-                              "device_graph": round(g_ms / g_n, 4) if g_n else None,
-                              "graph_compute_host": round(gh_ms / gh_n, 4) if gh_n else None,
-                              "llama_decode_call": round(1e3 * t_dec / a.steps, 4),
-                              "llama_synchronize_call": round(1e3 * t_syn / a.steps, 4)},
-            "cpu_baseline": cpu,
-            "hipgraph": dict(zip(("captures", "replays"), gstats)),
+    roof = None
+    if r.get("roof"):
+        mv_ms, mv_bytes, mv_n, fa_ms, fa_n, t_rf = r["roof"]
+        achieved = (mv_bytes / (mv_ms * 1e-3)) / 1e9 if mv_ms > 0 else None
+        hbm = r.get("hbm_gbs") or 0.0
+        # HBM bytes per GEMV launch from the PMC pass (rocprofv3 --pmc FETCH_SIZE, x2 gfx950
+        # correction), committed with its command under profiles/ (scripts/gpu_final.sh, scripts/pmc_traffic.py)
+        traffic = None
+        if os.path.exists(TRAFFIC_FILE):
+            try:
+                traffic = json.load(open(TRAFFIC_FILE)).get("gemv_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {
+            "bound": "hbm",
+            "kernel": "k_gemv_pipe (quantized decode GEMV, every decode MUL_MAT)",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "peak_measured": round(hbm, 1) if hbm > 0 else None,
+            "frac_of_measured": round(achieved / hbm, 4) if achieved and hbm > 0 else None,
+            "traffic": traffic,
+            "traffic_source": "profiles/r01/pmc_traffic.json" if traffic else None,
+            "launches": mv_n,
+            "avg_launch_us": round(1e3 * mv_ms / mv_n, 3) if mv_n else None,
+            "algorithmic_bytes_per_launch": round(mv_bytes / mv_n) if mv_n else None,
+            "measured_over_steps": a.roofline_steps,
+            "fattn_avg_us": round(1e3 * fa_ms / fa_n, 3) if fa_n else None,
+            "timed_pass_tok_s": round(a.roofline_steps / t_rf, 2) if t_rf > 0 else None,
         }
-        print(json.dumps(out))
-    dist.close()
+    pp_tps = r.get("pp_tps")
+    hbm = r.get("hbm_gbs") or 0.0
+    tok_s_stream = a.steps / r["t_local"]
+    depth0, depth1 = a.depth + a.warmup + 1, a.depth + a.warmup + a.steps
+    out = {
+        "metric": "llama-bench tg128 + pp512 tok/s, Llama-3-8B Q4_K_M; 1/2/4/8 GPU",
+        "value": round(value, 3),
+        "unit": "tok/s",
+        "n_gpus": n_units,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1e3 * t / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if split else "weak",
+        "vs_baseline": None,
+        "dtype": "i8",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{cfg.name} ({a.config}{suffix}) tg: n_batch=1 single-token llama_decode, "
+                        f"fa={a.fa}, kv={a.kv}, n_ctx={n_ctx}, KV depth {depth0}..{depth1} over the timed steps; "
+                        f"random-but-valid quant blocks" + ("; CPU backend (harness test)" if not gpu else ""),
+            "model": a.config + suffix,
+            "global_batch": streams,
+            "seq_len": depth1,
+            "parallelism": (f"layer split over {a.gpus} GPUs in one process (libllama -sm layer, RCCL send/recv "
+                            f"stage hand-off)" if split else (f"replicas x{ws}" if ws > 1 else "single GPU")),
+        },
+        "pp_tok_s": round(pp_tps, 2) if pp_tps else None,
+        "pp_tokens": a.pp,
+        "pp_roofline": ({"bound": "mfma", "unit": "TFLOP/s", "peak": MFMA_I8_PEAK_TOPS,
+                         "achieved": round(PP512_FLOP / (a.pp / pp_tps) / 1e12, 2),
+                         "frac": round(PP512_FLOP / (a.pp / pp_tps) / 1e12 / MFMA_I8_PEAK_TOPS, 4),
+                         "note": "whole pp512 (all kernels), Llama-3-8B algorithmic FLOPs, int8 dense peak"}
+                        if (pp_tps and gpu and a.pp == 512 and a.config == "llama3-8b-q4km" and not a.layers) else None),
+        "weight_bytes_per_token": wbytes,
+        "model_bw_GBs": round(wbytes * tok_s_stream / 1e9, 1),
+        "model_bw_frac_of_8TBs": round(wbytes * tok_s_stream / 1e9 / HBM_PEAK_GBS, 4),
+        "model_bw_frac_of_measured": round(wbytes * tok_s_stream / 1e9 / hbm, 4) if hbm > 0 else None,
+        "roofline": roof,
+        # wall = one llama_decode + llama_synchronize; device_graph = GPU time of the graph(s)
+        # per step (events around graph_compute); graph_compute_host = host time in our
+        # graph_compute per step (signature, KV-slot table upload, hipGraph launch); the rest of
+        # the wall is libllama's host work (graph build, scheduling, input upload, logits copy)
+        "step_split_ms": r.get("split"),
+        "cpu_baseline": r.get("cpu"),
+        "hipgraph": dict(zip(("captures", "replays"), r["gstats"])) if r.get("gstats") else None,
+        "stage_handoffs": dict(zip(("rccl", "peer"), r["p2p"])) if r.get("p2p") else None,
+    }
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

@@ -48,6 +48,16 @@ void ggml_backend_mi355x_set_graph_timing(int enable);
 void ggml_backend_mi355x_set_flags(int no_fuse, int no_graph);
 // hipGraph statistics since load: graphs captured, replays launched
 void ggml_backend_mi355x_graph_stats(long * captures, long * replays);
+// split-layer stage hand-offs since load (cpy_tensor_async between two MI355X devices): sent
+// over RCCL (ncclSend/ncclRecv, the default) / as hipMemcpyPeerAsync (GGML_MI355X_P2P=peer or
+// RCCL unavailable).  Replaces the peer-copy path of ggml-cuda.cu:2437-2490.
+void ggml_backend_mi355x_p2p_stats(long * rccl, long * peer);
+// destroys the RCCL communicators (re-created on the next cross-device copy)
+void ggml_backend_mi355x_p2p_release(void);
+// measured HBM read ceiling of a device in GB/s (STREAM-style non-temporal read of 440 MB
+// slices of a 4 GiB pool, best of three grids; llamacog_amd/csrc/k_stream.hip): the peak
+// bench.py reports its roofline fractions against beside the 8 TB/s nominal.  -1 on failure.
+double ggml_backend_mi355x_hbm_read_gbs(int device);
 
 // ---- flat kernel ABI (llamacog_amd/csrc/capi.cpp) ---------------------------------------------
 // Plain device pointers + sizes + a HIP stream (NULL = private stream, synchronised on

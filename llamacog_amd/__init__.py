@@ -56,6 +56,21 @@ def graph_stats() -> tuple[int, int]:
     return c.value, r.value
 
 
+def p2p_stats() -> tuple[int, int]:
+    """(stage hand-offs sent over RCCL send/recv, sent as hipMemcpyPeerAsync) since load."""
+    r, p = ctypes.c_long(), ctypes.c_long()
+    plugin_lib().ggml_backend_mi355x_p2p_stats(ctypes.byref(r), ctypes.byref(p))
+    return r.value, p.value
+
+
+def hbm_read_gbs(device: int = 0) -> float:
+    """Measured HBM read ceiling of a device, GB/s (k_stream.hip)."""
+    lib = plugin_lib()
+    lib.ggml_backend_mi355x_hbm_read_gbs.restype = ctypes.c_double
+    lib.ggml_backend_mi355x_hbm_read_gbs.argtypes = [ctypes.c_int]
+    return float(lib.ggml_backend_mi355x_hbm_read_gbs(device))
+
+
 def kernel_timing(lib: ctypes.CDLL, kind: int) -> tuple[float, float, int]:
     ms, by, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_long()
     lib.ggml_backend_mi355x_get_timing(kind, ctypes.byref(ms), ctypes.byref(by), ctypes.byref(n))

@@ -16,6 +16,8 @@
 #include "ops.h"
 #include "../../include/ggml-mi355x.h"
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -340,7 +342,72 @@ struct mi_backend_ctx {
     std::vector<graph_entry> graphs;   // small LRU of recently seen graphs
     uint64_t use_clock = 0;
     bool graphs_broken = false;        // capture failed once: stay eager
+    // hand-off events of cpy_tensor_async (recorded on this stream, waited on by the
+    // destination's): a ring created once instead of an event per copy
+    std::vector<hipEvent_t> xev;
+    size_t xev_next = 0;
+    hipEvent_t next_xevent() {
+        constexpr size_t RING = 16;
+        if (xev.size() < RING) {
+            hipEvent_t e;
+            MI_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            xev.push_back(e);
+            return e;
+        }
+        return xev[xev_next++ % RING];
+    }
 };
+
+// ------------------------------------------------------------------------------------------
+// split-layer hand-off over RCCL: one communicator clique over every visible
+// device (ncclCommInitAll, rank = HIP device id), created on the first cross-device copy so a
+// single-GPU process never initialises RCCL.  A stage boundary is a point-to-point
+// ncclSend (source stream) / ncclRecv (destination stream) pair in one group — the
+// collective library's xGMI transport, stream-ordered on both sides, no host sync.
+// GGML_MI355X_P2P=peer selects hipMemcpyPeerAsync + event instead (A/B and fallback).
+// ------------------------------------------------------------------------------------------
+struct mi_p2p {
+    std::mutex mtx;
+    int state = 0;                      // 0 = not tried, 1 = ready, -1 = unavailable
+    std::vector<ncclComm_t> comms;      // indexed by HIP device id
+};
+static mi_p2p g_p2p;
+static std::atomic<long> g_p2p_rccl{0}, g_p2p_peer{0};
+
+static bool p2p_use_rccl() {
+    static const bool peer = getenv("GGML_MI355X_P2P") && strcmp(getenv("GGML_MI355X_P2P"), "peer") == 0;
+    return !peer;
+}
+
+static bool p2p_comms_ready() {
+    std::lock_guard<std::mutex> lk(g_p2p.mtx);
+    if (g_p2p.state == 0) {
+        int n = 0;
+        MI_CHECK(hipGetDeviceCount(&n));
+        std::vector<int> devs(n);
+        for (int i = 0; i < n; ++i) devs[i] = i;
+        g_p2p.comms.assign(n, nullptr);
+        const ncclResult_t r = n > 1 ? ncclCommInitAll(g_p2p.comms.data(), n, devs.data()) : ncclInvalidUsage;
+        if (r == ncclSuccess) {
+            g_p2p.state = 1;
+        } else {
+            MI_LOG_WARN("mi355x: RCCL communicator init failed (%s); stage hand-off uses hipMemcpyPeerAsync\n",
+                        n > 1 ? ncclGetErrorString(r) : "one device");
+            g_p2p.comms.clear();
+            g_p2p.state = -1;
+        }
+    }
+    return g_p2p.state == 1;
+}
+
+static void p2p_destroy() {
+    std::lock_guard<std::mutex> lk(g_p2p.mtx);
+    for (ncclComm_t c : g_p2p.comms) {
+        if (c) (void) ncclCommDestroy(c);
+    }
+    g_p2p.comms.clear();
+    g_p2p.state = 0;
+}
 
 static int env_flag(const char * name) {
     const char * v = getenv(name);
@@ -409,6 +476,7 @@ static void mi_backend_free(ggml_backend_t backend) {
     MI_CHECK(hipStreamSynchronize(ctx->ex.stream));
     ctx->ex.collect_timing();
     for (auto e : ctx->ex.event_pool) (void) hipEventDestroy(e);
+    for (auto e : ctx->xev) (void) hipEventDestroy(e);
     for (auto & g : ctx->graphs) {
         if (g.exec) (void) hipGraphExecDestroy(g.exec);
     }
@@ -432,28 +500,41 @@ static void mi_backend_get_tensor_async(ggml_backend_t backend, const ggml_tenso
 
 static bool mi_backend_is_ours(ggml_backend_t backend);
 
-// Cross-device copy hook used by the scheduler for split inputs (ggml-backend.cpp:1391).
-// Same device: async D2D on the source stream; different MI355X devices: peer copy over
-// xGMI.  The destination stream waits on an event recorded after the copy.
+// Cross-device copy hook used by the scheduler for split inputs (ggml-backend.cpp:1391-1399,
+// called on the destination backend; ggml-cuda.cu:2437-2490 is the CUDA counterpart).
+//   * different MI355X devices: ncclSend on the source stream + ncclRecv on the destination
+//     stream in one group (RCCL over xGMI, see mi_p2p above), or hipMemcpyPeerAsync + event;
+//   * same device (two backend instances): async D2D on the source stream, the destination
+//     stream waits on a pooled event recorded after it.
 static bool mi_backend_cpy_tensor_async(ggml_backend_t backend_src, ggml_backend_t backend_dst, const ggml_tensor * src, ggml_tensor * dst) {
     if (!mi_backend_is_ours(backend_src) || !mi_backend_is_ours(backend_dst)) return false;
     if (!src->buffer || !dst->buffer || !mi_buf_is_ours(src->buffer) || !mi_buf_is_ours(dst->buffer)) return false;
+    if (!ggml_is_contiguous(src) || !ggml_is_contiguous(dst) || ggml_nbytes(src) != ggml_nbytes(dst)) return false;
     auto * sctx = (mi_backend_ctx *) backend_src->context;
     auto * dctx = (mi_backend_ctx *) backend_dst->context;
     const size_t n = ggml_nbytes(dst);
+    if (sctx->device != dctx->device && p2p_use_rccl() && p2p_comms_ready()) {
+        MI_CHECK(hipSetDevice(sctx->device));
+        bool ok = ncclGroupStart() == ncclSuccess;
+        ok = ok && ncclSend(src->data, n, ncclUint8, dctx->device, g_p2p.comms[sctx->device], sctx->ex.stream) == ncclSuccess;
+        ok = ok && ncclRecv(dst->data, n, ncclUint8, sctx->device, g_p2p.comms[dctx->device], dctx->ex.stream) == ncclSuccess;
+        const ncclResult_t ge = ncclGroupEnd();
+        GGML_ASSERT(ok && ge == ncclSuccess && "mi355x: RCCL send/recv of a stage hand-off failed");
+        g_p2p_rccl.fetch_add(1);
+        return true;
+    }
     MI_CHECK(hipSetDevice(sctx->device));
     if (sctx->device == dctx->device) {
         MI_CHECK(hipMemcpyAsync(dst->data, src->data, n, hipMemcpyDeviceToDevice, sctx->ex.stream));
     } else {
         MI_CHECK(hipMemcpyPeerAsync(dst->data, dctx->device, src->data, sctx->device, n, sctx->ex.stream));
+        g_p2p_peer.fetch_add(1);
     }
     if (backend_src != backend_dst) {
-        hipEvent_t ev;
-        MI_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipEvent_t ev = sctx->next_xevent();
         MI_CHECK(hipEventRecord(ev, sctx->ex.stream));
         MI_CHECK(hipSetDevice(dctx->device));
         MI_CHECK(hipStreamWaitEvent(dctx->ex.stream, ev, 0));
-        MI_CHECK(hipEventDestroy(ev));
     }
     return true;
 }
@@ -827,6 +908,13 @@ GGML_BACKEND_API void ggml_backend_mi355x_graph_stats(long * captures, long * re
 }
 
 GGML_BACKEND_API void ggml_backend_mi355x_set_graph_timing(int enable) { g_graph_timing.store(enable ? 1 : 0); }
+
+GGML_BACKEND_API void ggml_backend_mi355x_p2p_stats(long * rccl, long * peer) {
+    if (rccl) *rccl = g_p2p_rccl.load();
+    if (peer) *peer = g_p2p_peer.load();
+}
+
+GGML_BACKEND_API void ggml_backend_mi355x_p2p_release(void) { p2p_destroy(); }
 
 GGML_BACKEND_API void ggml_backend_mi355x_set_flags(int no_fuse, int no_graph) {
     g_no_fuse.store(no_fuse ? 1 : 0);

@@ -110,24 +110,27 @@ __device__ __forceinline__ void gemv_tail(const gemv_args & p, int kg, int64_t w
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __shared__ int tlist[GEMV_MAXG];
-    __shared__ int tn;
-    if (threadIdx.x == 0) {
-        int n = 0;
-        const int per = 2 * (256 / rpg);   // row groups of a Q8_K block: gate and up
-        for (int k = 0; k < kg; ++k) {
-            const int64_t g = wg0 + (int64_t) k * nwg;
+    // lane k of wave 0 reports row group k: the workgroup's returning atomics are in flight
+    // together rather than one round trip after another
+    if (threadIdx.x < GEMV_MAXG) {
+        int done = -1;
+        if ((int) threadIdx.x < kg) {
+            const int per = 2 * (256 / rpg);   // row groups of a Q8_K block: gate and up
+            const int64_t g = wg0 + (int64_t) threadIdx.x * nwg;
             const int mi = g >= p.blk0[1] ? 1 : 0;
             const int blk = (int) ((g - p.blk0[mi]) * rpg / 256);
             int * c = t.cnt + blk * TAIL_STRIDE;
             if (__hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per - 1) {
-                tlist[n++] = blk;
+                done = blk;
                 __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        tn = n;
+        tlist[threadIdx.x] = done;
     }
     __syncthreads();
-    for (int i = threadIdx.x >> 6; i < tn; i += 4) tail_swiglu(p, tlist[i], threadIdx.x & 63);
+    for (int i = threadIdx.x >> 6; i < kg; i += 4) {
+        if (tlist[i] >= 0) tail_swiglu(p, tlist[i], threadIdx.x & 63);   // wave-uniform
+    }
 }
 
 // ---- norm prologue ---------------------------------------------------------------------------------
