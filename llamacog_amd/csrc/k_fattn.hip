@@ -185,6 +185,184 @@ __global__ __launch_bounds__(256) void k_fattn_vec(const fa_args a) {
     }
 }
 
+// ---- long-context decode: GQA-packed split-K over 64-position chunks (f16 K/V, D <= 128) -------
+// One wave per (64-position chunk, KV head, query row): the G query heads that share the KV head
+// are scored together, so K and V stream from HBM once per KV head (not once per query head).
+// Lane l scores position l against all G heads (its K row in registers, Q from LDS); the
+// online-softmax terms are wave reductions (DPP rows + readlane); V goes to LDS with
+// coalesced 16-B loads issued before the scores, and lane l accumulates dims EPL*l.. for the G
+// heads, with each position's weight read from its lane as a scalar.  Partials (M, S, O) per
+// (chunk, head) merge in k_fattn_combine.  f32 throughout: the CPU's f16 VKQ rounding is not
+// reproduced (tests/test_gpu_model.py bounds the logit error at depth).
+__device__ __forceinline__ float wave_maxf(float v) {
+    v = fmaxf(v, __int_as_float(dpp<DPP_XOR1>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp<DPP_XOR2>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp<DPP_HMIRROR>(__float_as_int(v))));
+    v = fmaxf(v, __int_as_float(dpp<DPP_MIRROR>(__float_as_int(v))));
+    const float a0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float a3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fmaxf(fmaxf(a0, a1), fmaxf(a2, a3));
+}
+__device__ __forceinline__ float wave_sumf(float v) {
+    v += __int_as_float(dpp<DPP_XOR1>(__float_as_int(v)));
+    v += __int_as_float(dpp<DPP_XOR2>(__float_as_int(v)));
+    v += __int_as_float(dpp<DPP_HMIRROR>(__float_as_int(v)));
+    v += __int_as_float(dpp<DPP_MIRROR>(__float_as_int(v)));
+    const float a0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float a3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (a0 + a1) + (a2 + a3);
+}
+
+typedef __attribute__((address_space(3))) void * fa_lds_ptr_t;
+
+typedef _Float16 fa_h2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float fa_dot2(uint32_t a, uint32_t b, float c) {
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(fa_h2_t, a), __builtin_bit_cast(fa_h2_t, b), c, false);
+}
+
+// lanes: quad q4 = lane & 3 holds dims [D/4 q4, D/4 (q4+1)) of position 16 pass + (lane >> 2),
+// four passes cover the chunk's 64 positions; Q of the G heads lives in VGPRs as f16 pairs
+template <int EPL, int G>
+__global__ __launch_bounds__(64) void k_fattn_dec(const fa_args a) {
+    constexpr int D = 64 * EPL;
+    constexpr int QW = D / 8;               // dwords (f16 pairs) of a lane's quarter row
+    constexpr int PR = D * 2 / 16;          // 16-B pieces per V row
+    constexpr int RPP = 64 / PR;            // V rows per 1-KiB global_load_lds piece
+    const int lane = threadIdx.x, q4 = lane & 3, pl = lane >> 2;
+    const int64_t chunk = blockIdx.x;
+    const int64_t iq1 = blockIdx.y;
+    const int64_t hk = blockIdx.z % a.Hkv, iq3 = blockIdx.z / a.Hkv;
+    const int64_t pos0 = chunk * 64;
+    const int nvalid = (int) min((int64_t) 64, a.n_kv - pos0);
+    __shared__ __attribute__((aligned(16))) uint32_t vt[64 * D / 2];   // V tile: row-major f16 pairs
+
+    const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
+    const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
+    // V rows HBM -> LDS, asynchronous (1 KiB per wave instruction), consumed after the scores
+    {
+        const int r_in = lane / PR, col = lane % PR;
+#pragma unroll
+        for (int pc = 0; pc < 64 / RPP; ++pc) {
+            const int row = min(pc * RPP + r_in, nvalid - 1);
+            __builtin_amdgcn_global_load_lds((const void *) (vbase + (pos0 + row) * a.nbv1 + 16 * col),
+                                             (fa_lds_ptr_t) (vt + pc * 256), 16, 0, 0);
+        }
+    }
+    // K quarter rows of the four passes (QW / 4 16-B loads each)
+    uint4 kq[4][QW / 4];
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+        const int r = min(16 * ps + pl, nvalid - 1);
+        const char * krow = kbase + (pos0 + r) * a.nbk1 + (D / 2) * q4;
+#pragma unroll
+        for (int k = 0; k < QW / 4; ++k) kq[ps][k] = ld16(krow + 16 * k);
+    }
+    float mraw[4];
+    const char * mrow = a.mask ? a.mask + (iq1 % a.mask_ne1) * a.nbm1 : nullptr;
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+        const int r = 16 * ps + pl;
+        mraw[ps] = r >= nvalid ? -INFINITY : (mrow ? h2f(*(const uint16_t *) (mrow + 2 * (pos0 + r))) : 0.0f);
+    }
+    // Q of the G heads, f16-rounded like the CPU's vec_dot_type, as pairs
+    uint32_t qh[G][QW];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float * qrow = (const float *) (a.q + iq1 * a.nbq1 + (hk * G + g) * a.nbq2 + iq3 * a.nbq3) + (D / 4) * q4;
+#pragma unroll
+        for (int i = 0; i < QW / 2; ++i) {
+            const float4 f = *(const float4 *) (qrow + 4 * i);
+            qh[g][2 * i] = (uint32_t) f2h(f.x) | ((uint32_t) f2h(f.y) << 16);
+            qh[g][2 * i + 1] = (uint32_t) f2h(f.z) | ((uint32_t) f2h(f.w) << 16);
+        }
+    }
+    float p[4][G];
+    float M[G], S[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) M[g] = -INFINITY;
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < QW / 4; ++k) {
+                acc = fa_dot2(kq[ps][k].x, qh[g][4 * k], acc);
+                acc = fa_dot2(kq[ps][k].y, qh[g][4 * k + 1], acc);
+                acc = fa_dot2(kq[ps][k].z, qh[g][4 * k + 2], acc);
+                acc = fa_dot2(kq[ps][k].w, qh[g][4 * k + 3], acc);
+            }
+            acc += __int_as_float(dpp<DPP_XOR1>(__float_as_int(acc)));
+            acc += __int_as_float(dpp<DPP_XOR2>(__float_as_int(acc)));
+            const uint32_t h = (uint32_t) (hk * G + g);
+            const float slope = a.max_bias > 0.0f ? (h < a.n_head_log2 ? powf(a.m0, h + 1) : powf(a.m1, 2 * (h - a.n_head_log2) + 1)) : 1.0f;
+            float sv = acc * a.scale;
+            if (a.softcap != 0.0f) sv = a.softcap * tanhf(sv);
+            sv = mraw[ps] == -INFINITY ? -INFINITY : sv + slope * mraw[ps];
+            p[ps][g] = sv;
+            M[g] = fmaxf(M[g], sv);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        M[g] = wave_maxf(M[g]);
+        float sl = 0.0f;
+#pragma unroll
+        for (int ps = 0; ps < 4; ++ps) {
+            p[ps][g] = M[g] == -INFINITY || p[ps][g] == -INFINITY ? 0.0f : expf(p[ps][g] - M[g]);
+            sl += p[ps][g];
+        }
+        S[g] = wave_sumf(q4 == 0 ? sl : 0.0f);   // a position's weight is in all four lanes of its quad
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the V tile has landed
+    __syncthreads();
+    float o[G][EPL];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) o[g][e] = 0.0f;
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+        const int jn = min(16, nvalid - 16 * ps);
+        for (int jj = 0; jj < jn; ++jj) {
+            const int j = 16 * ps + jj;
+            float vv[EPL];
+            if constexpr (EPL == 2) {
+                const uint32_t x = vt[j * (D / 2) + lane];
+                vv[0] = h2f(x & 0xffff); vv[1] = h2f(x >> 16);
+            } else {
+                const uint32_t x = vt[j * (D / 2) + lane / 2];
+                vv[0] = h2f((lane & 1) ? (x >> 16) : (x & 0xffff));
+            }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float pj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p[ps][g]), 4 * jj));
+#pragma unroll
+                for (int e = 0; e < EPL; ++e) o[g][e] = fmaf(pj, vv[e], o[g][e]);
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int64_t h = hk * G + g;
+        if (a.nchunks == 1) {
+            float * drow = (float *) ((char *) a.dst + iq1 * a.nb1_dst * a.H + h * a.nb1_dst + iq3 * a.nb2_dst);
+            const float inv = 1.0f / S[g];
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) drow[lane * EPL + e] = o[g][e] * inv;
+        } else {
+            float * pr = a.part + (((chunk * a.n_q + iq1) * a.H + h) + iq3 * a.n_q * a.H * a.nchunks) * (D + 2);
+            if (lane == 0) { pr[0] = M[g]; pr[1] = S[g]; }
+#pragma unroll
+            for (int e = 0; e < EPL; ++e) pr[2 + lane * EPL + e] = o[g][e];
+        }
+    }
+}
+
 template <int EPL>
 __global__ __launch_bounds__(64) void k_fattn_combine(const fa_args a) {
     constexpr int D = 64 * EPL;
@@ -278,7 +456,16 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     hipEvent_t ev = nullptr;
     const double bytes = (double) (ggml_nbytes(k) + ggml_nbytes(v)) + (double) ggml_nbytes(q) + (double) ggml_nbytes(dst);
     if (ctx.timing) ctx.time_begin(TK_FATTN, bytes, ev);
-    static const bool fast = getenv("GGML_MI355X_FA_FAST") != nullptr && atoi(getenv("GGML_MI355X_FA_FAST")) != 0;
+    // the exact (CPU-order) kernel by default at every depth.  GGML_MI355X_FA_FAST=1 selects the
+    // split-K f32 kernels; GGML_MI355X_FA_EXACT_MAX=n selects them above n cache positions only.
+    // Not the default: the CPU accumulates VKQ in f16 (a rounding per position), and at depth
+    // that rounding is not small — on llama3-8b-2l-q4km at 1536 positions the f32 result's
+    // logits differ from the CPU's by 1.56 (max |diff| / max |logit|), far outside 1e-3
+    static const int fast_env = getenv("GGML_MI355X_FA_FAST") ? atoi(getenv("GGML_MI355X_FA_FAST")) : -1;
+    static const int64_t exact_max = getenv("GGML_MI355X_FA_EXACT_MAX") ? atoll(getenv("GGML_MI355X_FA_EXACT_MAX")) : INT64_MAX;
+    const bool dec_ok = a.k_type == GGML_TYPE_F16 && (a.D == 64 || a.D == 128) && a.n_q <= 8 &&
+                        (a.H / a.Hkv == 1 || a.H / a.Hkv == 2 || a.H / a.Hkv == 4 || a.H / a.Hkv == 8);
+    const bool fast = fast_env == 1 || (fast_env != 0 && dec_ok && a.n_kv > exact_max);
     a.cnt = nullptr;
     if (!fast && (a.k_type == GGML_TYPE_F16 || a.k_type == GGML_TYPE_Q8_0)) {
         // fused quantization of the output for the next MUL_MAT (decode: one row)
@@ -302,6 +489,25 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
         }
         launch_fattn_exact(ctx.stream, a, nq3);
         if (a.qmode) ctx.qcache_put(mm->src[1], a.qmode == 1, act);
+        if (ctx.timing) ctx.time_end(TK_FATTN, bytes, ev);
+        return;
+    }
+    if (dec_ok) {
+        // one wave per 64-position chunk and KV head
+        a.chunk = 64;
+        a.nchunks = (int) ceil_div(a.n_kv, 64);
+        if (a.nchunks > 1) a.part = (float *) ctx.scratch(1, sizeof(float) * a.nchunks * rows * (a.D + 2));
+        const int G = (int) (a.H / a.Hkv);
+        dim3 gd((unsigned) a.nchunks, (unsigned) a.n_q, (unsigned) (a.Hkv * nq3));
+#define DEC(E, GG) hipLaunchKernelGGL((k_fattn_dec<E, GG>), gd, dim3(64), 0, ctx.stream, a)
+        if (a.D == 128) { if (G == 1) DEC(2, 1); else if (G == 2) DEC(2, 2); else if (G == 4) DEC(2, 4); else DEC(2, 8); }
+        else            { if (G == 1) DEC(1, 1); else if (G == 2) DEC(1, 2); else if (G == 4) DEC(1, 4); else DEC(1, 8); }
+#undef DEC
+        if (a.nchunks > 1) {
+            dim3 g2((unsigned) a.n_q, (unsigned) (a.H * nq3));
+            if (a.D == 128) hipLaunchKernelGGL(k_fattn_combine<2>, g2, dim3(64), 0, ctx.stream, a);
+            else hipLaunchKernelGGL(k_fattn_combine<1>, g2, dim3(64), 0, ctx.stream, a);
+        }
         if (ctx.timing) ctx.time_end(TK_FATTN, bytes, ev);
         return;
     }
