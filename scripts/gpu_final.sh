@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd $R
-OUT=gpurun_out/round
+OUT=gpurun_out/${OUT:-r02}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; grep -E "FAILED|Error" $OUT/pytest_gpu.log | head; tail -5 $OUT/pytest_gpu.log; exit 1; }
 grep -E "passed|failed" $OUT/pytest_gpu.log | tail -1
@@ -13,10 +13,13 @@ tail -1 $OUT/smoke.log
 timeout -k 10 900 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench rc=$?"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace -o run -- python3 $R/bench.py --no-cpu-baseline > $R/$OUT/trace_bench.json 2> $R/$OUT/trace_bench.err || { echo "trace rc=$?"; tail -20 $R/$OUT/trace_bench.err; exit 1; }
+# decode-only traced run: W + K timed + (4 + K) split + (4 + R) roofline single-token decodes
+W=4; K=32; RF=8
+NTOK=$((W + K + 4 + K + 4 + RF))
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace -o run -- python3 $R/bench.py --steps $K --warmup $W --roofline-steps $RF --pp 0 --no-cpu-baseline > $R/$OUT/trace_bench.json 2> $R/$OUT/trace_bench.err || { echo "trace rc=$?"; tail -20 $R/$OUT/trace_bench.err; exit 1; }
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/$OUT/pmc -o run -- python3 $R/bench.py --steps 16 --warmup 2 --pp 0 --no-cpu-baseline --roofline-steps 0 > $R/$OUT/pmc_bench.json 2> $R/$OUT/pmc_bench.err || { echo "pmc rc=$?"; tail -20 $R/$OUT/pmc_bench.err; exit 1; }
 cd $R
-python3 scripts/kstats.py $(find $OUT/trace -name '*kernel_stats.csv' | head -1) > $OUT/kernel_stats_summary.txt
+python3 scripts/kstats.py $(find $OUT/trace -name '*kernel_stats.csv' | head -1) $NTOK > $OUT/kernel_stats_summary.txt
 cp $(find $OUT/trace -name '*kernel_stats.csv' | head -1) $OUT/kernel_stats.csv
 python3 scripts/pmc_traffic.py $(find $OUT/pmc -name '*counter_collection.csv' | head -1) $OUT/pmc_traffic.json > /dev/null
 rm -rf $OUT/trace $OUT/pmc
