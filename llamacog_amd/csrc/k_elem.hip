@@ -227,6 +227,42 @@ __global__ __launch_bounds__(64) void k_cpy_f32_q8_0(const char * __restrict__ s
     if ((lane & 7) == 0) blk->d = f2h(dd);
 }
 
+// f32 rows -> q4_0 blocks, quantize_row_q4_0_ref (ggml-quants.c, the CPU backend's from_float
+// for Q4_0, ggml-cpu/quants.c:24): the first element of largest |x| gives max, d = max / -8,
+// id = 1/d, q = min(15, (int8_t)(x*id + 8.5)) with separate f32 roundings (the reference builds
+// ggml-quants.c without FMA), elements j and j + 16 share byte j.  One thread per block.
+__global__ __launch_bounds__(64) void k_cpy_f32_q4_0(const char * __restrict__ s, t4 ts, char * __restrict__ d, t4 td,
+                                                     char * const * dslot) {
+    if (dslot) d = *dslot;
+    const int64_t r = blockIdx.y;
+    const int64_t b = (int64_t) blockIdx.x * 64 + threadIdx.x;
+    if (32 * b >= ts.ne[0]) return;
+    const int64_t i1 = r % ts.ne[1], i2 = (r / ts.ne[1]) % ts.ne[2], i3 = r / (ts.ne[1] * ts.ne[2]);
+    const char * srow = s + i1 * ts.nb[1] + i2 * ts.nb[2] + i3 * ts.nb[3];
+    const int64_t j1 = r % td.ne[1], j2 = (r / td.ne[1]) % td.ne[2], j3 = r / (td.ne[1] * td.ne[2]);
+    char * drow = d + j1 * td.nb[1] + j2 * td.nb[2] + j3 * td.nb[3];
+    float x[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) x[j] = *(const float *) (srow + (32 * b + j) * ts.nb[0]);
+    float amax = 0.0f, mx = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        if (amax < fabsf(x[j])) { amax = fabsf(x[j]); mx = x[j]; }
+    }
+    const float dd = mx / -8.0f;
+    const float id = dd != 0.0f ? 1.0f / dd : 0.0f;
+    uint8_t * blk = (uint8_t *) (drow + b * 18);
+    const uint16_t dh = f2h(dd);
+    blk[0] = (uint8_t) (dh & 0xff);
+    blk[1] = (uint8_t) (dh >> 8);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int q0 = min(15, (int) (int8_t) (int) __fadd_rn(__fmul_rn(x[j], id), 8.5f));
+        const int q1 = min(15, (int) (int8_t) (int) __fadd_rn(__fmul_rn(x[j + 16], id), 8.5f));
+        blk[2 + j] = (uint8_t) (q0 | (q1 << 4));
+    }
+}
+
 void op_cpy(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst, const ggml_tensor * node) {
     const int64_t n = ggml_nelements(src);
     if (n == 0) return;
@@ -247,6 +283,20 @@ void op_cpy(exec_ctx & ctx, const ggml_tensor * src, ggml_tensor * dst, const gg
         for (int k = 1; k < 4; ++k) { S1.ne[k] = D1.ne[k] = 1; S1.nb[k] = S.nb[0] * n; D1.nb[k] = ggml_row_size(GGML_TYPE_Q8_0, n); }
         dim3 g((unsigned) ceil_div(n, 256), 1u);
         hipLaunchKernelGGL(k_cpy_f32_q8_0, g, dim3(64), 0, ctx.stream, (const char *) src->data, S1, (char *) dst->data, D1, dslot);
+        return;
+    }
+    if (src->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_Q4_0) {
+        // contiguous both sides: one flat row (the KV-cache store); else row by row
+        t4 S1 = S, D1 = D;
+        int64_t ne0 = src->ne[0], nrows = src->ne[1] * src->ne[2] * src->ne[3];
+        if (ggml_is_contiguous(src) && ggml_is_contiguous(dst) && src->ne[0] != dst->ne[0]) {
+            ne0 = n;
+            nrows = 1;
+            S1.ne[0] = D1.ne[0] = n;
+            for (int k = 1; k < 4; ++k) { S1.ne[k] = D1.ne[k] = 1; S1.nb[k] = S.nb[0] * n; D1.nb[k] = ggml_row_size(GGML_TYPE_Q4_0, n); }
+        }
+        dim3 g((unsigned) ceil_div(ne0 / 32, 64), (unsigned) nrows);
+        hipLaunchKernelGGL(k_cpy_f32_q4_0, g, dim3(64), 0, ctx.stream, (const char *) src->data, S1, (char *) dst->data, D1, dslot);
         return;
     }
     if (src->type == GGML_TYPE_F32 && dst->type == GGML_TYPE_Q8_0) {

@@ -401,7 +401,7 @@ bool fattn_supported(const ggml_tensor * op) {
     const int64_t D = k->ne[0];
     if (D != 64 && D != 128 && D != 256) return false;
     if (k->type != v->type) return false;
-    if (k->type != GGML_TYPE_F16 && k->type != GGML_TYPE_Q8_0) return false;
+    if (k->type != GGML_TYPE_F16 && k->type != GGML_TYPE_Q8_0 && k->type != GGML_TYPE_Q4_0) return false;
     if (mask && mask->type != GGML_TYPE_F16) return false;
     if (mask && (mask->ne[2] != 1 || mask->ne[3] != 1)) return false;
     if (q->ne[2] % k->ne[2] != 0) return false;
@@ -465,9 +465,10 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     static const int64_t exact_max = getenv("GGML_MI355X_FA_EXACT_MAX") ? atoll(getenv("GGML_MI355X_FA_EXACT_MAX")) : INT64_MAX;
     const bool dec_ok = a.k_type == GGML_TYPE_F16 && (a.D == 64 || a.D == 128) && a.n_q <= 8 &&
                         (a.H / a.Hkv == 1 || a.H / a.Hkv == 2 || a.H / a.Hkv == 4 || a.H / a.Hkv == 8);
-    const bool fast = fast_env == 1 || (fast_env != 0 && dec_ok && a.n_kv > exact_max);
+    // q4_0 has no split-K kernel: always the exact one
+    const bool fast = a.k_type != GGML_TYPE_Q4_0 && (fast_env == 1 || (fast_env != 0 && dec_ok && a.n_kv > exact_max));
     a.cnt = nullptr;
-    if (!fast && (a.k_type == GGML_TYPE_F16 || a.k_type == GGML_TYPE_Q8_0)) {
+    if (!fast && (a.k_type == GGML_TYPE_F16 || a.k_type == GGML_TYPE_Q8_0 || a.k_type == GGML_TYPE_Q4_0)) {
         // fused quantization of the output for the next MUL_MAT (decode: one row)
         q8_act act;
         if (mm && a.n_q == 1 && nq3 == 1 && mmv_q_supported_type(mm->src[0]->type) &&

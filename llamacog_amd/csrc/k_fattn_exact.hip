@@ -123,8 +123,12 @@ template <int D, int CHO = 0> struct fax_cfg {
 
 // OCC = workgroups per CU the register budget allows: 1 for decode (32-64 workgroups, every
 // register for ILP), 2 for prefill (thousands of workgroups; the LDS allows two)
-template <int D, int OCC = 1, int CHO = 0, bool Q8 = false>
+// Q8: a quantized cache; Q4 (with Q8): q4_0 blocks instead of q8_0 (ggml_vec_dot_q4_0_q8_0,
+// arch/x86/quants.c:531: the same eight class chains over (nibble - 8) · q8, d = dk·dq; V
+// dequantized as (nibble - 8)·d, dequantize_row_q4_0)
+template <int D, int OCC = 1, int CHO = 0, bool Q8 = false, bool Q4 = false>
 __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
+    constexpr int KB = Q4 ? 18 : 34;   // bytes per 32-element K / V block
     using C = fax_cfg<D, CHO>;
     constexpr int CH = C::CH, U = C::U, NM = D / 16, NB = D / 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -233,14 +237,31 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
                 __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (vl + p * 512), 16, 0, 0);
             }
         } else {
-            // q8_0 blocks (34 B, 2-byte aligned): quants to vq[pos][D], scales to vd[pos][D/32]
+            // q8_0 / q4_0 blocks (2-byte aligned): quants to vq[pos][D] (q4_0: nibble - 8),
+            // scales to vd[pos][D/32]
             int8_t * vq = (int8_t *) vl;
             for (int i = tid; i < nrun * NB; i += 256) {
                 const int row = i / NB, b = i % NB;
-                const uint8_t * src = (const uint8_t *) vbase + (c0 + row) * a.nbv1 + 34 * b;
-                const uint4 lo = ld16(src + 2), hi = ld16(src + 18);
-                *(uint4 *) (vq + row * D + 32 * b) = lo;
-                *(uint4 *) (vq + row * D + 32 * b + 16) = hi;
+                const uint8_t * src = (const uint8_t *) vbase + (c0 + row) * a.nbv1 + KB * b;
+                if constexpr (Q4) {
+                    // element j < 16: low nibble of qs[j]; j >= 16: high nibble of qs[j - 16]
+                    const uint4 q = ld16(src + 2);
+                    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+                    uint32_t lo[4], hi[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        // (nibble - 8) per byte: n + 0x78 stays inside its byte (<= 135), and
+                        // flipping bit 7 turns it into n - 8 as an int8
+                        lo[k] = ((w[k] & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
+                        hi[k] = (((w[k] >> 4) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
+                    }
+                    *(uint4 *) (vq + row * D + 32 * b) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+                    *(uint4 *) (vq + row * D + 32 * b + 16) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+                } else {
+                    const uint4 lo = ld16(src + 2), hi = ld16(src + 18);
+                    *(uint4 *) (vq + row * D + 32 * b) = lo;
+                    *(uint4 *) (vq + row * D + 32 * b + 16) = hi;
+                }
                 vd[row * NB + b] = h2f(ld2(src));
             }
         }
@@ -256,7 +277,18 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
                 const uint8_t * krow = (const uint8_t *) kbase + (c0 + j) * a.nbk1;
 #pragma unroll
                 for (int b = 0; b < NB; ++b) {
-                    if (64 * p < nrun) { kb[p][b] = ld8(krow + 34 * b + 2 + 8 * qd); kd[p][b] = ld2(krow + 34 * b); }
+                    if (64 * p < nrun) {
+                        if constexpr (Q4) {
+                            // elements 8qd .. 8qd+7: qs[8 (qd & 1) ..] nibble qd >> 1, minus 8
+                            const uint2 q = ld8(krow + KB * b + 2 + 8 * (qd & 1));
+                            const int sh = 4 * (qd >> 1);
+                            kb[p][b] = make_uint2((((q.x >> sh) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u,
+                                                  (((q.y >> sh) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u);
+                        } else {
+                            kb[p][b] = ld8(krow + KB * b + 2 + 8 * qd);
+                        }
+                        kd[p][b] = ld2(krow + KB * b);
+                    }
                 }
             }
 #pragma unroll
@@ -512,6 +544,18 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     // 9.6k -> 10.6k tok/s; OCC 3/4 spill and run slower, 8.5k / 8.2k) or 256 (64 KiB)
     static const int pch = getenv("GGML_MI355X_FA_PREFILL_CH") ? atoi(getenv("GGML_MI355X_FA_PREFILL_CH")) : 128;
     const bool wide = a.n_q * a.H * nq3 > 256 && pocc >= 2;   // prefill: more workgroups than CUs
+    if (a.k_type == GGML_TYPE_Q4_0) {
+        switch (a.D) {
+            case 64:  hipLaunchKernelGGL((k_fattn_exact<64, 1, 0, true, true>), grid, dim3(256), 0, st, a); break;
+            case 128:
+                if (wide) hipLaunchKernelGGL((k_fattn_exact<128, 2, 128, true, true>), grid, dim3(256), 0, st, a);
+                else hipLaunchKernelGGL((k_fattn_exact<128, 1, 0, true, true>), grid, dim3(256), 0, st, a);
+                break;
+            case 256: hipLaunchKernelGGL((k_fattn_exact<256, 1, 0, true, true>), grid, dim3(256), 0, st, a); break;
+            default: GGML_ABORT("mi355x: FA head size %d", (int) a.D);
+        }
+        return;
+    }
     if (a.k_type == GGML_TYPE_Q8_0) {
         switch (a.D) {
             case 64:  hipLaunchKernelGGL((k_fattn_exact<64, 1, 0, true>), grid, dim3(256), 0, st, a); break;

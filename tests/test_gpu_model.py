@@ -90,6 +90,16 @@ def test_greedy_tiny_q8_0_kv_cache():
     _check(_greedy("tiny-q4km", 16, 16, True, kv="q8_0"))
 
 
+def test_greedy_tiny_q4_0_kv_cache():
+    """A q4_0 KV cache (-ctk q4_0 -ctv q4_0): the KV store quantizes with quantize_row_q4_0_ref
+    and the exact FA takes ggml_vec_dot_q4_0_q8_0's class chains, V dequantized to f32."""
+    _check(_greedy("tiny-q4km", 16, 16, True, kv="q4_0"))
+
+
+def test_greedy_llama3_8b_2layer_q4_0_kv_cache():
+    _check(_greedy("llama3-8b-2l-q4km", 64, 8, True, kv="q4_0"))
+
+
 @pytest.mark.parametrize("cfg", ["llama3-8b-2l-q4km", "tiny-q8_0", "tiny-moe-q5km"])
 def test_fused_and_graph_replay_bit_identical(cfg):
     """The fused producers (k_fused.hip) and hipGraph replay change no bit of the logits:
