@@ -320,6 +320,52 @@ static bool mi_buft_is_ours(ggml_backend_buffer_type_t buft) {
 }
 
 // ------------------------------------------------------------------------------------------
+// pinned host buffer type (device get_host_buffer_type; the role of ggml-cuda's CUDA_Host).
+// libllama puts the logits / embeddings output buffer (llama-context.cpp:1247-1253) and the
+// CPU backend's compute buffer — the token-embedding GET_ROWS output — (:211-217) in it, so the
+// per-token device<->host copies are DMA from page-locked memory instead of staged copies.
+// The buffer is an ordinary CPU buffer over hipHostMalloc'd memory.
+// ------------------------------------------------------------------------------------------
+static const char * mi_host_buft_get_name(ggml_backend_buffer_type_t) { return MI355X_NAME "_Host"; }
+
+static void mi_host_buf_free(ggml_backend_buffer_t buffer) { (void) hipHostFree(buffer->context); }
+
+static ggml_backend_buffer_t mi_host_buft_alloc(ggml_backend_buffer_type_t buft, size_t size) {
+    void * ptr = nullptr;
+    if (hipHostMalloc(&ptr, std::max<size_t>(size, 1), hipHostMallocDefault) != hipSuccess) {
+        (void) hipGetLastError();
+        MI_LOG_WARN("mi355x: hipHostMalloc of %.2f MiB failed; using pageable host memory\n", size / 1048576.0);
+        return ggml_backend_buft_alloc_buffer(ggml_backend_cpu_buffer_type(), size);
+    }
+    ggml_backend_buffer_t buf = ggml_backend_cpu_buffer_from_ptr(ptr, size);
+    buf->buft = buft;
+    buf->iface.free_buffer = mi_host_buf_free;
+    return buf;
+}
+
+static size_t mi_host_buft_get_alignment(ggml_backend_buffer_type_t) {
+    return ggml_backend_buft_get_alignment(ggml_backend_cpu_buffer_type());
+}
+
+static bool mi_host_buft_is_host(ggml_backend_buffer_type_t) { return true; }
+
+static ggml_backend_buffer_type_t mi_host_buft() {
+    static ggml_backend_buffer_type buft = {
+        /* .iface   = */ {
+            /* .get_name       = */ mi_host_buft_get_name,
+            /* .alloc_buffer   = */ mi_host_buft_alloc,
+            /* .get_alignment  = */ mi_host_buft_get_alignment,
+            /* .get_max_size   = */ nullptr,
+            /* .get_alloc_size = */ nullptr,
+            /* .is_host        = */ mi_host_buft_is_host,
+        },
+        /* .device  = */ nullptr,   // host memory belongs to no device (as CUDA_Host)
+        /* .context = */ nullptr,
+    };
+    return &buft;
+}
+
+// ------------------------------------------------------------------------------------------
 // backend (stream)
 // ------------------------------------------------------------------------------------------
 // hipGraph replay of repeated graphs (decode re-submits an identical graph every token).
@@ -721,7 +767,7 @@ static void mi_dev_get_props(ggml_backend_dev_t dev, ggml_backend_dev_props * pr
     mi_dev_get_memory(dev, &props->memory_free, &props->memory_total);
     props->caps = {
         /* .async                = */ true,
-        /* .host_buffer          = */ false,
+        /* .host_buffer          = */ !getenv("GGML_MI355X_NO_HOST_BUFFER"),
         /* .buffer_from_host_ptr = */ false,
         /* .events               = */ true,
     };
@@ -746,6 +792,11 @@ static ggml_backend_t mi_dev_init_backend(ggml_backend_dev_t dev, const char * p
 
 static ggml_backend_buffer_type_t mi_dev_get_buffer_type(ggml_backend_dev_t dev) {
     return &((mi_device_ctx *) dev->context)->buft;
+}
+
+// GGML_MI355X_NO_HOST_BUFFER=1: no pinned host buffer type (pageable copies, as round 1)
+static ggml_backend_buffer_type_t mi_dev_get_host_buffer_type(ggml_backend_dev_t) {
+    return getenv("GGML_MI355X_NO_HOST_BUFFER") ? nullptr : mi_host_buft();
 }
 
 static bool mi_dev_supports_op(ggml_backend_dev_t dev, const ggml_tensor * op) {
@@ -789,7 +840,7 @@ static const ggml_backend_device_i mi_device_iface = {
     /* .get_props            = */ mi_dev_get_props,
     /* .init_backend         = */ mi_dev_init_backend,
     /* .get_buffer_type      = */ mi_dev_get_buffer_type,
-    /* .get_host_buffer_type = */ nullptr,
+    /* .get_host_buffer_type = */ mi_dev_get_host_buffer_type,
     /* .buffer_from_host_ptr = */ nullptr,
     /* .supports_op          = */ mi_dev_supports_op,
     /* .supports_buft        = */ mi_dev_supports_buft,

@@ -434,10 +434,15 @@ static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
     int64_t grid = std::min<int64_t>(ng, g_gemv_wgs);
     if constexpr (WPR == 4 && !std::is_same<T, g_q6_K>::value) {
         // four waves per row (K = 14336, the FFN down projection): one resident round of
-        // workgroups (5 per CU) beats 2048 single-group workgroups in two rounds
-        // (Q4_K 4096 x 14336: 12.0 -> 11.2 us, scripts/probe_geom.py)
-        static const int wgs4 = getenv("GGML_MI355X_GEMV_WGS4") ? atoi(getenv("GGML_MI355X_GEMV_WGS4")) : 5 * g_num_cu;
+        // workgroups beats 2048 single-group workgroups in two rounds (Q4_K 4096 x 14336: 12.0 ->
+        // 11.2 us at 5 per CU, scripts/probe_geom.py); with the residual producer's epilogue 3 per
+        // CU (768) is faster again, 12.5 -> 11.2 us (scripts/gpu_trace_var.sh, round 2)
+        static const int wgs4 = getenv("GGML_MI355X_GEMV_WGS4") ? atoi(getenv("GGML_MI355X_GEMV_WGS4")) : 3 * g_num_cu;
         if (wgs4 > 0) grid = std::min<int64_t>(ng, wgs4);
+    }
+    if constexpr (WPR == 4 && std::is_same<T, g_q6_K>::value) {
+        static const int wgs6 = getenv("GGML_MI355X_GEMV_WGS4Q6") ? atoi(getenv("GGML_MI355X_GEMV_WGS4Q6")) : 0;
+        if (wgs6 > 0) grid = std::min<int64_t>(ng, wgs6);
     }
     if (a.pro.x) {
         // every workgroup forms the activation: one resident round (GGML_MI355X_PRO_WGS), so no
