@@ -20,6 +20,7 @@
 // MFMA tiles sharing the A fragment).  MFMA layouts (verified by tools/mfma_layout.hip): lane l
 // holds A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15]; C[row 4(l>>4)+i][col l&15].
 #include "ops.h"
+#include "qtypes.h"
 
 namespace mi355x {
 
@@ -278,6 +279,278 @@ __global__ __launch_bounds__(256, 2) void k_mmq_q4K(const mmq_args p) {
         for (int i = 0; i < 4; ++i) {
             const int64_t m = row0 + 16 * wave + 4 * h + i;
             if (m < p.M) *(float *) (drow + m * 4) = __fsub_rn(A[n][i], B[n][i]);
+        }
+    }
+}
+
+// ==== Q4_K on v_mfma_i32_16x16x64_i8 with scale-folded weights (the repacked gemm/gemv order) ========
+// The gemm's integer per sub-block pair, I_pair = sc_2k·<q_2k, y> + sc_2k+1·<q_2k+1, y>, is a
+// K = 64 dot product once each weight carries its 6-bit sub-block scale.  With sc = 8a + b
+// (a, b <= 7) the two planes qa = q·a and qb = q·b are int8 (<= 105), so
+// I_pair = 8·MFMA(qa, y) + MFMA(qb, y) exactly, and the pair's mins integer
+// m_2k·Σy_2k + m_2k+1·Σy_2k+1 is a third MFMA with the mins replicated along K — three
+// 16x16x64 instructions per pair and 16x16 outputs, and per output only the CPU's own work
+// remains on the VALU (one shift-add, two converts, the two fp32 chain FMAs).  The fold is one
+// packed 16-bit multiply per 4 weights (q·a < 256: no carry between bytes).
+// Each wave folds the 16 rows it multiplies, so the planes need no workgroup barrier: the one
+// barrier per K block is for the shared token stage (LDS-DMA, double-buffered).
+// Workgroups of one XCD take all token tiles of a row tile (the weights are read once per XCD
+// L2, not once per token tile), when the row-tile count is a multiple of 8.
+// MFMA x64 lane map (tools/mfma_probe.hip): lane l holds A[row l&15][k 16(l>>4)+j], B[k 16(l>>4)+j]
+// [col l&15], j < 16; C[row 4(l>>4)+i][col l&15].
+constexpr int MF_RS = 272;                       // plane row stride (256 + 16: 16 rows, 16 bank groups)
+constexpr int MF_PL = MQ_BM * MF_RS;             // one plane
+constexpr int MF_XD = MQ_BN * 256;               // token stage: rows [64][256] (XOR-swizzled chunks), then
+constexpr int MF_XB = MF_XD + MQ_BN * 4;         //   the token scales [64] f32
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_mul16(uint32_t x, uint32_t s2) {
+    const us2 r = __builtin_bit_cast(us2, x) * __builtin_bit_cast(us2, s2);
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+__global__ __launch_bounds__(256, 2) void k_mmq_q4Kf(const mmq_args p) {
+    __shared__ __attribute__((aligned(16))) uint8_t pa[MF_PL], pb[MF_PL];
+    __shared__ __attribute__((aligned(16))) uint8_t xst[2][MF_XB];
+    __shared__ __attribute__((aligned(16))) uint32_t wmn4[MQ_BM][8];   // mins, byte-replicated
+    __shared__ __attribute__((aligned(16))) float wd[MQ_BM], wdm[MQ_BM];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int64_t bx = blockIdx.x, by = blockIdx.y;
+    if (!p.cnt && (gridDim.x & 7) == 0) {   // XCD-major: one row tile's token tiles on one XCD
+        const int64_t id = bx + (int64_t) gridDim.x * by, j = id >> 3;
+        by = j % gridDim.y;
+        bx = (j / gridDim.y) * 8 + (id & 7);
+    }
+    const int64_t row0 = bx * MQ_BM;
+    const int64_t tok0 = by * MQ_BN;
+    const int h = lane >> 4, c16 = lane & 15;
+    const uint8_t * Wb = p.W;
+    int64_t T = p.T, col0 = 0;
+    if (p.cnt) {
+        T = p.cnt[blockIdx.z];
+        if (tok0 >= T) return;   // uniform: no barrier passed yet
+        col0 = p.off[blockIdx.z];
+        Wb = p.W + (int64_t) blockIdx.z * p.nb02;
+    }
+    const int64_t KB = p.K / 256;
+    // 0: every token of the tile takes the gemm (per-pair) order, 1: every token the gemv
+    // (per-block) order, 2: mixed (the last tile of a batch with T % 4 != 0)
+    const int mode = tok0 + MQ_BN <= p.gemm_cols ? 0 : (tok0 >= p.gemm_cols ? 1 : 2);
+    bool gemm[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) gemm[n] = tok0 + 16 * n + c16 < p.gemm_cols;
+
+    // token-side LDS-DMA sources (as k_mmq_q4K): 16 KiB of rows + 256 B of scales per block
+    const int8_t * xsrc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int c = 64 * (wave + 4 * k) + lane, t = c >> 4, part = (c & 15) ^ (t & 15);
+        xsrc[k] = p.xq + (col0 + min(tok0 + t, T - 1)) * p.K + 16 * part;
+    }
+    const float * dsrc = p.xd + (col0 + min(tok0 + lane, T - 1)) * KB;
+    auto issue_x = [&](int64_t b, int s) {
+        uint8_t * base = xst[s];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            __builtin_amdgcn_global_load_lds((const void *) (xsrc[k] + b * 256), (lds_ptr_t) (base + 1024 * (wave + 4 * k)), 16, 0, 0);
+        }
+        if (wave == 0) __builtin_amdgcn_global_load_lds((const void *) (dsrc + b), (lds_ptr_t) (base + MF_XD), 4, 0, 0);
+    };
+    // weight side: lane (row fr, pair fq) of wave w folds 64 weights of row 16w + lane/4
+    const int fr = tid >> 2, fq = tid & 3;
+    const uint8_t * wrow = Wb + min(row0 + fr, p.M - 1) * p.nb01;
+    uint4 whdr, wqa, wqb;   // header (d, dmin, scales) and the pair's 32 qs bytes
+    auto load_w = [&](int64_t b) {
+        const uint8_t * blk = wrow + b * 144;
+        whdr = ld16(blk);
+        wqa = ld16(blk + 16 + 32 * fq);
+        wqb = ld16(blk + 32 + 32 * fq);
+    };
+    auto fold_w = [&]() {
+        int sc_lo, sc_hi, m_lo, m_hi;
+        k4_scales_g(whdr.y, whdr.z, whdr.w, fq, sc_lo, sc_hi, m_lo, m_hi);
+        const uint32_t q[8] = {wqa.x, wqa.y, wqa.z, wqa.w, wqb.x, wqb.y, wqb.z, wqb.w};
+        uint32_t qa[16], qb[16];
+        // elements 0..31 of the pair: low nibbles (sub-block 2fq); 32..63: high nibbles (2fq+1)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const uint32_t sc = (uint32_t) (half ? sc_hi : sc_lo);
+            const uint32_t a2 = (sc >> 3) * 0x10001u, b2 = (sc & 7) * 0x10001u;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t nb = half ? (q[i] >> 4) & 0x0f0f0f0fu : q[i] & 0x0f0f0f0fu;
+                qa[8 * half + i] = pk_mul16(nb, a2);
+                qb[8 * half + i] = pk_mul16(nb, b2);
+            }
+        }
+        uint8_t * ap = pa + fr * MF_RS + 64 * fq;
+        uint8_t * bp = pb + fr * MF_RS + 64 * fq;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            *(uint4 *) (ap + 16 * k) = make_uint4(qa[4 * k], qa[4 * k + 1], qa[4 * k + 2], qa[4 * k + 3]);
+            *(uint4 *) (bp + 16 * k) = make_uint4(qb[4 * k], qb[4 * k + 1], qb[4 * k + 2], qb[4 * k + 3]);
+        }
+        *(uint2 *) &wmn4[fr][2 * fq] = make_uint2((uint32_t) m_lo * 0x01010101u, (uint32_t) m_hi * 0x01010101u);
+        if (fq == 0) { wd[fr] = h2f(whdr.x & 0xffff); wdm[fr] = h2f(whdr.x >> 16); }
+    };
+
+    float A[4][4], B[4][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) A[n][i] = B[n][i] = 0.0f;
+
+    const int rA = 16 * wave + c16;
+    load_w(0);
+    issue_x(0, 0);
+    fold_w();
+    for (int64_t b = 0; b < p.nblk; ++b) {
+        const int s = (int) (b & 1);
+        const int8_t * xq = (const int8_t *) xst[s];
+        const float * xd = (const float *) (xst[s] + MF_XD);
+        // stage s landed for every wave; every wave is done with stage s^1 (block b-1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const bool more = b + 1 < p.nblk;
+        if (more) {
+            load_w(b + 1);
+            issue_x(b + 1, s ^ 1);
+        }
+        // the CPU's scale products d·dy and dmin·dy of this lane's 4 rows x 4 tokens
+        const float4 dw4 = *(const float4 *) &wd[16 * wave + 4 * h], dm4 = *(const float4 *) &wdm[16 * wave + 4 * h];
+        const float dw[4] = {dw4.x, dw4.y, dw4.z, dw4.w}, dmw[4] = {dm4.x, dm4.y, dm4.z, dm4.w};
+        float sA[4][4], sB[4][4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const float dy = xd[16 * n + c16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { sA[n][i] = dw[i] * dy; sB[n][i] = dmw[i] * dy; }
+        }
+        if (mode == 0) {
+#pragma unroll 1
+            for (int k = 0; k < 4; ++k) {
+                const uint4 a1 = *(const uint4 *) (pa + rA * MF_RS + 64 * k + 16 * h);
+                const uint4 a2 = *(const uint4 *) (pb + rA * MF_RS + 64 * k + 16 * h);
+                const uint32_t mm = wmn4[rA][2 * k + (h >> 1)];
+                const v4i va = {(int) a1.x, (int) a1.y, (int) a1.z, (int) a1.w};
+                const v4i vb = {(int) a2.x, (int) a2.y, (int) a2.z, (int) a2.w};
+                const v4i vm = {(int) mm, (int) mm, (int) mm, (int) mm};
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const uint4 x = *(const uint4 *) (xq + (16 * n + c16) * 256 + 16 * ((4 * k + h) ^ c16));
+                    const v4i y = {(int) x.x, (int) x.y, (int) x.z, (int) x.w};
+                    const v4i z = {0, 0, 0, 0};
+                    const v4i ra = __builtin_amdgcn_mfma_i32_16x16x64_i8(va, y, z, 0, 0, 0);
+                    const v4i rb = __builtin_amdgcn_mfma_i32_16x16x64_i8(vb, y, z, 0, 0, 0);
+                    const v4i rm = __builtin_amdgcn_mfma_i32_16x16x64_i8(vm, y, z, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        A[n][i] = fmaf((float) (ra[i] * 8 + rb[i]), sA[n][i], A[n][i]);
+                        B[n][i] = fmaf((float) rm[i], sB[n][i], B[n][i]);
+                    }
+                }
+            }
+        } else if (mode == 1) {
+            // per-block integer sums (gemv order), accumulated in the MFMA
+            v4i ca[4], cb[4], cm[4];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) ca[n] = cb[n] = cm[n] = (v4i){0, 0, 0, 0};
+#pragma unroll 1
+            for (int k = 0; k < 4; ++k) {
+                const uint4 a1 = *(const uint4 *) (pa + rA * MF_RS + 64 * k + 16 * h);
+                const uint4 a2 = *(const uint4 *) (pb + rA * MF_RS + 64 * k + 16 * h);
+                const uint32_t mm = wmn4[rA][2 * k + (h >> 1)];
+                const v4i va = {(int) a1.x, (int) a1.y, (int) a1.z, (int) a1.w};
+                const v4i vb = {(int) a2.x, (int) a2.y, (int) a2.z, (int) a2.w};
+                const v4i vm = {(int) mm, (int) mm, (int) mm, (int) mm};
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const uint4 x = *(const uint4 *) (xq + (16 * n + c16) * 256 + 16 * ((4 * k + h) ^ c16));
+                    const v4i y = {(int) x.x, (int) x.y, (int) x.z, (int) x.w};
+                    ca[n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(va, y, ca[n], 0, 0, 0);
+                    cb[n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(vb, y, cb[n], 0, 0, 0);
+                    cm[n] = __builtin_amdgcn_mfma_i32_16x16x64_i8(vm, y, cm[n], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    A[n][i] = fmaf((float) (ca[n][i] * 8 + cb[n][i]), sA[n][i], A[n][i]);
+                    B[n][i] = fmaf((float) cm[n][i], sB[n][i], B[n][i]);
+                }
+        } else {
+            // mixed tile: per-pair chains for the gemm tokens, block integer sums for the rest
+            int ib[4][4], mb[4][4];
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) ib[n][i] = mb[n][i] = 0;
+#pragma unroll 1
+            for (int k = 0; k < 4; ++k) {
+                const uint4 a1 = *(const uint4 *) (pa + rA * MF_RS + 64 * k + 16 * h);
+                const uint4 a2 = *(const uint4 *) (pb + rA * MF_RS + 64 * k + 16 * h);
+                const uint32_t mm = wmn4[rA][2 * k + (h >> 1)];
+                const v4i va = {(int) a1.x, (int) a1.y, (int) a1.z, (int) a1.w};
+                const v4i vb = {(int) a2.x, (int) a2.y, (int) a2.z, (int) a2.w};
+                const v4i vm = {(int) mm, (int) mm, (int) mm, (int) mm};
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const uint4 x = *(const uint4 *) (xq + (16 * n + c16) * 256 + 16 * ((4 * k + h) ^ c16));
+                    const v4i y = {(int) x.x, (int) x.y, (int) x.z, (int) x.w};
+                    const v4i z = {0, 0, 0, 0};
+                    const v4i ra = __builtin_amdgcn_mfma_i32_16x16x64_i8(va, y, z, 0, 0, 0);
+                    const v4i rb = __builtin_amdgcn_mfma_i32_16x16x64_i8(vb, y, z, 0, 0, 0);
+                    const v4i rm = __builtin_amdgcn_mfma_i32_16x16x64_i8(vm, y, z, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int ip = ra[i] * 8 + rb[i];
+                        if (gemm[n]) {
+                            A[n][i] = fmaf((float) ip, sA[n][i], A[n][i]);
+                            B[n][i] = fmaf((float) rm[i], sB[n][i], B[n][i]);
+                        } else {
+                            ib[n][i] += ip;
+                            mb[n][i] += rm[i];
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                if (gemm[n]) continue;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    A[n][i] = fmaf((float) ib[n][i], sA[n][i], A[n][i]);
+                    B[n][i] = fmaf((float) mb[n][i], sB[n][i], B[n][i]);
+                }
+            }
+        }
+        if (more) {
+            // this wave's plane rows for block b+1 (only this wave reads them; a wave's LDS
+            // accesses complete in order, so the reads above finish first)
+            asm volatile("" ::: "memory");
+            fold_w();
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const int64_t t = tok0 + 16 * n + c16;
+        if (t >= T) continue;
+        char * drow = (char *) p.dst + t * p.nb1;
+        if (p.cnt) {
+            const int pair = p.list[col0 + t];
+            drow = (char *) p.dst + (pair % p.n_used) * p.nb1 + (pair / p.n_used) * p.nb2;
+        }
+        const int64_t m0 = row0 + 16 * wave + 4 * h;
+        if (m0 + 3 < p.M) {
+            *(float4 *) (drow + m0 * 4) = make_float4(__fsub_rn(A[n][0], B[n][0]), __fsub_rn(A[n][1], B[n][1]),
+                                                      __fsub_rn(A[n][2], B[n][2]), __fsub_rn(A[n][3], B[n][3]));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (m0 + i < p.M) *(float *) (drow + (m0 + i) * 4) = __fsub_rn(A[n][i], B[n][i]);
         }
     }
 }
@@ -575,7 +848,13 @@ static void launch_cls(hipStream_t st, const dim3 & grid, const mmq_args & p) {
 
 static void launch_mmq(hipStream_t st, ggml_type t, const dim3 & grid, const mmq_args & p) {
     switch (t) {
-        case GGML_TYPE_Q4_K: hipLaunchKernelGGL(k_mmq_q4K<mq_q4_K>, grid, dim3(256), 0, st, p); break;
+        case GGML_TYPE_Q4_K: {
+            // GGML_MI355X_MMQ_FOLD=0: the 16x16x32 tile with VALU scales (k_mmq_q4K)
+            static const bool fold = !getenv("GGML_MI355X_MMQ_FOLD") || atoi(getenv("GGML_MI355X_MMQ_FOLD")) != 0;
+            if (fold) hipLaunchKernelGGL(k_mmq_q4Kf, grid, dim3(256), 0, st, p);
+            else hipLaunchKernelGGL(k_mmq_q4K<mq_q4_K>, grid, dim3(256), 0, st, p);
+            break;
+        }
         case GGML_TYPE_Q5_K: launch_cls<mc_q5_K>(st, grid, p); break;
         case GGML_TYPE_Q6_K: launch_cls<mc_q6_K>(st, grid, p); break;
         default: GGML_ABORT("mi355x: mmq type");
