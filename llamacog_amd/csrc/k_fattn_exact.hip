@@ -534,6 +534,292 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
     }
 }
 
+// ==== prefill: a block of query rows x the G query heads of one KV head per workgroup ========
+// Same arithmetic as k_fattn_exact (the AVX-512 f16 dot order, the prefix-max coefficients, the
+// f16 VKQ recurrence with the CPU's roundings), arranged for a batch of queries: the 16 (query
+// row, head) pairs of a workgroup share every K and V row it stages, so the cache is read from
+// L2 once per 16 pairs instead of once per pair, and each thread carries 8 independent f16
+// chains (2 dims x 4 pairs) instead of one.  Wave w owns pairs 4w..4w+3 through all three
+// phases (scores, coefficients, recurrence), so the only workgroup barrier per 64-position
+// chunk is the one that publishes the next K / V / mask stage (double-buffered, LDS-DMA).
+// K rows are XOR-swizzled in LDS (16-byte chunk c of row r in slot c ^ 2(r & 3)) so the four
+// rows a phase-1 instruction touches sit in different banks.
+constexpr int PF_CH = 64, PF_P = 16, PF_U = 8;
+
+// y = f16(fma(v_hi, vs, y)): f16_mad on the high half of v
+__device__ __forceinline__ uint32_t f16_mad_hi(uint32_t vbits, float vs, uint32_t ybits) {
+    float t;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(t) : "v"(vbits), "v"(vs), "v"(ybits));
+    uint32_t r;
+    asm("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
+// dot_f16_avx512_q4 with the f16 -> f32 conversions folded into v_fma_mix_f32 (exact: the
+// conversion is exact and the fma rounds once; the first product is fma(k, q, -0) = k·q
+// rounded, as _mm512_mul_ps)
+template <int SEL>
+__device__ __forceinline__ float mixfma(uint32_t kbits, float q, float acc) {
+    float r;
+    if constexpr (SEL == 0) asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(kbits), "v"(q), "v"(acc));
+    else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(kbits), "v"(q), "v"(acc));
+    return r;
+}
+
+__device__ __forceinline__ float dot_f16_mix_d128(const uint2 (&kh)[8], const float (&qf)[8][4], float nz) {
+    float w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float acc[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const uint32_t k0 = c < 2 ? kh[jj].x : kh[jj].y, k1 = c < 2 ? kh[4 + jj].x : kh[4 + jj].y;
+            float t = (c & 1) ? mixfma<1>(k0, qf[jj][c], nz) : mixfma<0>(k0, qf[jj][c], nz);
+            acc[jj] = (c & 1) ? mixfma<1>(k1, qf[4 + jj][c], t) : mixfma<0>(k1, qf[4 + jj][c], t);
+        }
+        w[c] = __fadd_rn(__fadd_rn(acc[0], acc[2]), __fadd_rn(acc[1], acc[3]));
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = __fadd_rn(w[c], quad_from_plus2(w[c]));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = __fadd_rn(w[c], quad_from_plus1(w[c]));
+    return __fadd_rn(__fadd_rn(w[0], w[2]), __fadd_rn(w[1], w[3]));
+}
+
+template <int G>
+__global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
+    constexpr int D = 128, NM = D / 16, QB = PF_P / G;
+    __shared__ __attribute__((aligned(16))) uint16_t kl[2][PF_CH * D];
+    __shared__ __attribute__((aligned(16))) uint16_t vl[2][PF_CH * D];
+    __shared__ __attribute__((aligned(16))) uint16_t ml[2][QB * PF_CH];   // mask values (f16)
+    __shared__ __attribute__((aligned(16))) float sc[PF_CH * PF_P];       // scores -> vs, [pos][pair]
+    __shared__ __attribute__((aligned(16))) float cm[PF_CH * PF_P];       // ms, [pos][pair]
+    __shared__ int wend[4];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // longest causal prefixes first
+    const int64_t q0 = (int64_t) (gridDim.x - 1 - blockIdx.x) * QB;
+    const int64_t hk = blockIdx.y % a.Hkv, iq3 = blockIdx.y / a.Hkv;
+    const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
+    const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
+    auto qrow_of = [&](int p) { return min(q0 + p / G, a.n_q - 1); };
+    auto head_of = [&](int p) { return hk * G + p % G; };
+    auto slope_of = [&](int p) -> float {
+        if (a.max_bias <= 0.0f) return 1.0f;
+        const uint32_t h = (uint32_t) head_of(p);
+        return (float) (h < a.n_head_log2 ? pow((double) a.m0, (double) (h + 1))
+                                          : pow((double) a.m1, (double) (2 * (h - a.n_head_log2) + 1)));
+    };
+
+    // ---- the cache positions any of the QB query rows attends: [0, nend) --------------------
+    int64_t nend = a.n_kv;
+    if (a.mask) {
+        int last = -1;
+        for (int qi = 0; qi < QB; ++qi) {
+            const uint16_t * mr = (const uint16_t *) (a.mask + (min(q0 + qi, a.n_q - 1) % a.mask_ne1) * a.nbm1);
+            for (int64_t j0 = 0; j0 < a.n_kv; j0 += 256) {
+                const int64_t j = j0 + tid;
+                const bool live = j < a.n_kv && mr[j] != 0xfc00;   // f16 -inf
+                const unsigned long long b = __ballot(live);
+                if (b) last = max(last, (int) (j0 + 64 * wave + 63 - __clzll(b)));
+            }
+        }
+        if (lane == 0) wend[wave] = last;
+        __syncthreads();
+        nend = max(max(wend[0], wend[1]), max(wend[2], wend[3])) + 1;
+    }
+    const int nchunk = (int) ((nend + PF_CH - 1) / PF_CH);
+
+    // ---- staging: K (swizzled) and V rows of a chunk by LDS-DMA, its mask through registers -----
+    auto issue_kv = [&](int c, int s) {
+        const int64_t c0 = (int64_t) c * PF_CH;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = wave + 4 * k;                       // 1 KiB piece: rows 4i .. 4i+3
+            const int r = 4 * i + (lane >> 4), cs = lane & 15;
+            const int64_t row = min(c0 + r, a.n_kv - 1);
+            __builtin_amdgcn_global_load_lds((const void *) (kbase + row * a.nbk1 + 16 * (cs ^ (2 * (r & 3)))),
+                                             (lds_ptr_t) (kl[s] + 512 * i), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (vbase + row * a.nbv1 + 16 * cs),
+                                             (lds_ptr_t) (vl[s] + 512 * i), 16, 0, 0);
+        }
+    };
+    constexpr int MPT = (QB * PF_CH + 255) / 256;   // mask values per thread
+    uint16_t mreg[MPT];
+    auto load_mask = [&](int c) {
+        const int64_t c0 = (int64_t) c * PF_CH;
+#pragma unroll
+        for (int k = 0; k < MPT; ++k) {
+            const int e = tid + 256 * k, qi = e / PF_CH, j = e % PF_CH;
+            uint16_t v = 0xfc00;
+            if (e < QB * PF_CH && c0 + j < a.n_kv) {
+                v = 0;
+                if (a.mask) v = *(const uint16_t *) (a.mask + (min(q0 + qi, a.n_q - 1) % a.mask_ne1) * a.nbm1 + 2 * (c0 + j));
+            }
+            mreg[k] = v;
+        }
+    };
+    auto store_mask = [&](int s) {
+#pragma unroll
+        for (int k = 0; k < MPT; ++k) {
+            const int e = tid + 256 * k;
+            if (e < QB * PF_CH) ml[s][e] = mreg[k];
+        }
+    };
+
+    // ---- phase-1 role: quad qi = lane / 4 scores pair 4w + (qi & 3) at positions 4r + qi / 4 --
+    const int qd = lane & 3, qi = lane >> 2;
+    const int p1 = 4 * wave + (qi & 3), r1 = qi >> 2;
+    float qf[NM][4];
+    {
+        const float * qr = (const float *) (a.q + qrow_of(p1) * a.nbq1 + head_of(p1) * a.nbq2 + iq3 * a.nbq3);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const float4 t = *(const float4 *) (qr + 16 * m + 4 * qd);
+            qf[m][0] = f16r(t.x); qf[m][1] = f16r(t.y); qf[m][2] = f16r(t.z); qf[m][3] = f16r(t.w);
+        }
+    }
+    const float slope1 = slope_of(p1);
+    float nz = -0.0f;
+    asm volatile("" : "+v"(nz));
+    // ---- phase-2/3 state of the wave's 4 pairs --------------------------------------------------
+    float mc[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};   // running max (uniform)
+    uint32_t y[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};          // f16 bits, dims 2 lane, 2 lane + 1
+    float S[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float slope2[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) slope2[i] = slope_of(4 * wave + i);
+
+    if (nchunk > 0) {
+        issue_kv(0, 0);
+        load_mask(0);
+        store_mask(0);
+    }
+    for (int c = 0; c < nchunk; ++c) {
+        const int s = c & 1;
+        const int64_t c0 = (int64_t) c * PF_CH;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // stage s (K, V, mask) is in; every wave is done with stage s^1
+        const bool more = c + 1 < nchunk;
+        if (more) {
+            issue_kv(c + 1, s ^ 1);
+            load_mask(c + 1);
+        }
+        const uint16_t * ks = kl[s];
+        const uint16_t * ms = ml[s];
+        // ---- phase 1: scores of the wave's 4 pairs x 64 positions --------------------------
+#pragma unroll 2
+        for (int r = 0; r < PF_CH / 4; ++r) {
+            const int j = 4 * r + r1;
+            uint2 kh[NM];
+#pragma unroll
+            for (int m = 0; m < NM; ++m)
+                kh[m] = *(const uint2 *) ((const char *) ks + j * 256 + 16 * ((2 * m + (qd >> 1)) ^ (2 * (j & 3))) + 8 * (qd & 1));
+            const float w = dot_f16_mix_d128(kh, qf, nz);
+            if (qd == 0) {
+                float sv = __fmul_rn(w, a.scale);
+                if (a.softcap != 0.0f) sv = __fmul_rn(a.softcap, tanhf(sv));
+                sc[j * PF_P + p1] = __fadd_rn(sv, __fmul_rn(slope1, h2f(ms[(p1 / G) * PF_CH + j])));
+            }
+        }
+        asm volatile("" ::: "memory");
+        // ---- phase 2: per pair, the prefix max and the (ms, vs) coefficient of every position -
+        // per pair: positions that update the running max / that are masked (uniform)
+        uint64_t upd[4], dead[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = 4 * wave + i, j = lane;
+            const bool live = c0 + j < nend && ms[(p / G) * PF_CH + j] != 0xfc00;
+            const float sj = live ? sc[j * PF_P + p] : -INFINITY;
+            float sm = sj;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const float t = __shfl_up(sm, o, WAVE);
+                if (lane >= o) sm = fmaxf(sm, t);
+            }
+            float M = mc[i];
+            const float ex = __shfl_up(sm, 1, WAVE);
+            if (lane > 0) M = fmaxf(M, ex);
+            float vs, mv;
+            if (!live) { mv = 1.0f; vs = 0.0f; }
+            else if (sj > M) { mv = M == -INFINITY ? 0.0f : expf_cr(M - sj); vs = 1.0f; }
+            else { mv = 1.0f; vs = expf_cr(sj - M); }
+            cm[j * PF_P + p] = mv;
+            sc[j * PF_P + p] = vs;
+            upd[i] = __ballot(live && sj > M);
+            dead[i] = __ballot(!live);
+            mc[i] = fmaxf(mc[i], __shfl(sm, 63, WAVE));
+        }
+        asm volatile("" ::: "memory");
+        // ---- phase 3: the f16 recurrence, 2 dims x 4 pairs per lane (V from LDS) ------------
+        {
+            const int nrun = (int) min((int64_t) PF_CH, nend - c0);
+            const uint32_t * vrow = (const uint32_t *) vl[s] + lane;   // dims 2 lane, 2 lane + 1
+            const float * scw = sc + 4 * wave;
+            const float * cmw = cm + 4 * wave;
+            for (int j0 = 0; j0 < nrun; j0 += PF_U) {
+                uint32_t vv[PF_U];
+                float4 vs[PF_U];
+#pragma unroll
+                for (int u = 0; u < PF_U; ++u) {
+                    vv[u] = vrow[(j0 + u) * (D / 2)];
+                    vs[u] = *(const float4 *) (scw + (j0 + u) * PF_P);
+                }
+                const uint64_t ev = (upd[0] | upd[1] | upd[2] | upd[3] | dead[0] | dead[1] | dead[2] | dead[3]) >> j0;
+                if ((ev & ((1ull << PF_U) - 1)) == 0) {
+#pragma unroll
+                    for (int u = 0; u < PF_U; ++u) {
+                        const float v4[4] = {vs[u].x, vs[u].y, vs[u].z, vs[u].w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            y[i][0] = f16_mad(vv[u], v4[i], y[i][0]);
+                            y[i][1] = f16_mad_hi(vv[u], v4[i], y[i][1]);
+                            S[i] = __fadd_rn(S[i], v4[i]);   // not contracted on the CPU
+                        }
+                    }
+                } else {
+                    // the same steps, except: a masked position keeps the state (-0 must
+                    // survive); a running-max update first rescales, y = f16(y*ms), S = S*ms —
+                    // the CPU's vec_scale_f16 (ops.cpp:7120-7160).  Uniform branches per event.
+#pragma unroll
+                    for (int u = 0; u < PF_U; ++u) {
+                        const int j = j0 + u;
+                        const float v4[4] = {vs[u].x, vs[u].y, vs[u].z, vs[u].w};
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            if ((dead[i] >> j) & 1) continue;
+                            if ((upd[i] >> j) & 1) {
+                                const float w = cmw[j * PF_P + i];
+#pragma unroll
+                                for (int e = 0; e < 2; ++e) {
+                                    float t = __fmul_rn(h2f((uint16_t) y[i][e]), w);
+                                    asm("" : "+v"(t));   // two roundings, as f16r
+                                    y[i][e] = (uint32_t) f2h(t);
+                                }
+                                S[i] = __fmul_rn(S[i], w);
+                            }
+                            y[i][0] = f16_mad(vv[u], v4[i], y[i][0]);
+                            y[i][1] = f16_mad_hi(vv[u], v4[i], y[i][1]);
+                            S[i] = __fadd_rn(S[i], v4[i]);
+                        }
+                    }
+                }
+            }
+        }
+        if (more) store_mask(s ^ 1);   // published by the next chunk's barrier
+    }
+    // ---- output O = y / S --------------------------------------------------------------------
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = 4 * wave + i;
+        const int64_t iq = q0 + p / G;
+        if (iq >= a.n_q) continue;
+        float * drow = (float *) ((char *) a.dst + iq * a.nb1_dst * a.H + head_of(p) * a.nb1_dst + iq3 * a.nb2_dst);
+        const float rs = 1.0f / S[i];
+        *(float2 *) (drow + 2 * lane) = make_float2(__fmul_rn(h2f((uint16_t) y[i][0]), rs), __fmul_rn(h2f((uint16_t) y[i][1]), rs));
+    }
+}
+
 void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     GGML_ASSERT(a0.H % a0.Hkv == 0);
     fa_args a = a0;
@@ -565,6 +851,21 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
                 break;
             case 256: hipLaunchKernelGGL((k_fattn_exact<256, 1, 0, true>), grid, dim3(256), 0, st, a); break;
             default: GGML_ABORT("mi355x: FA head size %d", (int) a.D);
+        }
+        return;
+    }
+    // prefill, f16 cache, D = 128: query blocks x the GQA group (GGML_MI355X_FA_PF=0: one
+    // workgroup per query row and head)
+    static const bool pf_on = !getenv("GGML_MI355X_FA_PF") || atoi(getenv("GGML_MI355X_FA_PF")) != 0;
+    const int64_t G = a.H / a.Hkv;
+    if (pf_on && a.D == 128 && a.n_q >= 16 && a.qmode == 0 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) {
+        const dim3 g((unsigned) ceil_div(a.n_q, (int64_t) PF_P / G), (unsigned) (a.Hkv * nq3));
+        switch (G) {
+            case 1:  hipLaunchKernelGGL(k_fattn_pf<1>, g, dim3(256), 0, st, a); break;
+            case 2:  hipLaunchKernelGGL(k_fattn_pf<2>, g, dim3(256), 0, st, a); break;
+            case 4:  hipLaunchKernelGGL(k_fattn_pf<4>, g, dim3(256), 0, st, a); break;
+            case 8:  hipLaunchKernelGGL(k_fattn_pf<8>, g, dim3(256), 0, st, a); break;
+            default: hipLaunchKernelGGL(k_fattn_pf<16>, g, dim3(256), 0, st, a); break;
         }
         return;
     }
