@@ -488,6 +488,8 @@ __global__ __launch_bounds__(256) void k_pattern_read(const uint8_t * __restrict
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+namespace mi355x { void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst); }
+
 extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t b, int iters) {
     scoped_ctx sc(nullptr);
     hipEvent_t e0, e1;
@@ -536,6 +538,17 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
                                (const v4u_t *) (buf + (c % copies) * bytes), bytes / 16, o);
             ++c;
         };
+    } else if (which == 300 || which == 301) {
+        // prefill MUL_MAT: Q4_K (300) / Q6_K (301) weights [K=4096][M=a] x b f32 tokens
+        const ggml_type wt = which == 300 ? GGML_TYPE_Q4_K : GGML_TYPE_Q6_K;
+        const int64_t Kd = 4096, M = a, T = b;
+        static ggml_tensor Wm, Xm, Dm;
+        const int64_t new_[4] = {Kd, M, 1, 1}, nex[4] = {Kd, T, 1, 1}, ned[4] = {M, T, 1, 1};
+        init_tensor(Wm, wt, new_, dalloc(ggml_row_size(wt, Kd) * M, 0x11));
+        init_tensor(Xm, GGML_TYPE_F32, nex, dalloc(Kd * T * 4, 0x3c));
+        init_tensor(Dm, GGML_TYPE_F32, ned, dalloc(M * T * 4, 0));
+        Dm.op = GGML_OP_MUL_MAT; Dm.src[0] = &Wm; Dm.src[1] = &Xm;
+        run = [&] { mul_mat_q(sc.ex, &Dm); };
     } else if (which == 0) {
         const int64_t D = 128, H = 32, Hkv = 8, n_kv = a;
         float * q = (float *) dalloc(D * H * 4, 0x3c);
