@@ -526,6 +526,22 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
             else           hipLaunchKernelGGL(k_pattern_read<1>, grid, dim3(256), 0, sc.ex.stream, p, nrows, o);
             ++c;
         };
+    } else if (which == 300 || which == 301) {
+        // prefill MUL_MAT: Q4_K (300) / Q6_K (301) weights [K=4096][M=a] x b f32 tokens
+        const ggml_type wt = which == 300 ? GGML_TYPE_Q4_K : GGML_TYPE_Q6_K;
+        const int64_t Kd = 4096, M = a, T = b;
+        static ggml_tensor Wm, Xm, Dm;
+        const int64_t new_[4] = {Kd, M, 1, 1}, nex[4] = {Kd, T, 1, 1}, ned[4] = {M, T, 1, 1};
+        init_tensor(Wm, wt, new_, dalloc(ggml_row_size(wt, Kd) * M, 0x11));
+        init_tensor(Xm, GGML_TYPE_F32, nex, dalloc(Kd * T * 4, 0x3c));
+        init_tensor(Dm, GGML_TYPE_F32, ned, dalloc(M * T * 4, 0));
+        Dm.op = GGML_OP_MUL_MAT; Dm.src[0] = &Wm; Dm.src[1] = &Xm;
+        run = [&] { mul_mat_q(sc.ex, &Dm); };
+        run();
+        MI_CHECK(hipStreamSynchronize(sc.ex.stream));
+        float chk[4];
+        MI_CHECK(hipMemcpy(chk, (const char *) Dm.data + (M * T / 2) * 4, sizeof(chk), hipMemcpyDeviceToHost));
+        fprintf(stderr, "mmq probe M=%lld T=%lld: dst[mid] %g %g %g %g\n", (long long) M, (long long) T, chk[0], chk[1], chk[2], chk[3]);
     } else if (which >= 100) {
         // streaming read of a bytes per launch over b rotating copies, grid = which - 100 (x64)
         const int64_t bytes = a, copies = std::max<int64_t>(1, b);
@@ -538,17 +554,6 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
                                (const v4u_t *) (buf + (c % copies) * bytes), bytes / 16, o);
             ++c;
         };
-    } else if (which == 300 || which == 301) {
-        // prefill MUL_MAT: Q4_K (300) / Q6_K (301) weights [K=4096][M=a] x b f32 tokens
-        const ggml_type wt = which == 300 ? GGML_TYPE_Q4_K : GGML_TYPE_Q6_K;
-        const int64_t Kd = 4096, M = a, T = b;
-        static ggml_tensor Wm, Xm, Dm;
-        const int64_t new_[4] = {Kd, M, 1, 1}, nex[4] = {Kd, T, 1, 1}, ned[4] = {M, T, 1, 1};
-        init_tensor(Wm, wt, new_, dalloc(ggml_row_size(wt, Kd) * M, 0x11));
-        init_tensor(Xm, GGML_TYPE_F32, nex, dalloc(Kd * T * 4, 0x3c));
-        init_tensor(Dm, GGML_TYPE_F32, ned, dalloc(M * T * 4, 0));
-        Dm.op = GGML_OP_MUL_MAT; Dm.src[0] = &Wm; Dm.src[1] = &Xm;
-        run = [&] { mul_mat_q(sc.ex, &Dm); };
     } else if (which == 0) {
         const int64_t D = 128, H = 32, Hkv = 8, n_kv = a;
         float * q = (float *) dalloc(D * H * 4, 0x3c);
@@ -609,6 +614,10 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
     MI_CHECK(hipEventDestroy(e0));
     MI_CHECK(hipEventDestroy(e1));
     MI_CHECK(hipStreamSynchronize(sc.ex.stream));
+    {
+        const hipError_t err = hipGetLastError();
+        if (err != hipSuccess) fprintf(stderr, "mi355x_bench_op %d: %s\n", which, hipGetErrorString(err));
+    }
     if (prof) {
         unsigned long long h[6];
         MI_CHECK(hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost));

@@ -1,5 +1,5 @@
-// k_mmq.hip — batched (prefill) Q4_K MUL_MAT on MFMA (v_mfma_i32_16x16x32_i8), in the CPU
-// backend's exact float order.
+// k_mmq.hip — batched (prefill) quantized MUL_MAT / MUL_MAT_ID on MFMA, in the CPU backend's
+// exact float order.
 //
 // libllama keeps Q4_K weights with M % 8 == 0 in the CPU_REPACK buffer; for a batch the CPU
 // runs ggml_gemm_q4_K_8x8_q8_K (arch/x86/repack.cpp:1771) on the tokens in whole groups of
@@ -10,280 +10,20 @@
 // CPU's Q8_K (the gemm's 4x8 quantizer differs only in the sign of equal-magnitude maxima,
 // which flips qs, d and bsums together and leaves every product unchanged; qtypes.h).
 //
-// The integer dot of a 32-element chunk of 16 weight rows x 16 tokens is one MFMA; the 6-bit
-// sub-block scales multiply the int32 results in VALU (24-bit multiplies: |MFMA result| <=
-// 32*15*127 < 2^23), pairs and mins are exact integers, and every float step is the CPU's.
-//
-// Tiling (MI355X): a 256-thread workgroup owns 64 weight rows x 64 tokens; per 256-element K
-// block the 64 rows' quant blocks and the 64 tokens' Q8_K rows are staged in LDS (two stages:
-// block b+1 loads while block b computes), each wave computes 16 rows x 64 tokens (four 16x16
-// MFMA tiles sharing the A fragment).  MFMA layouts (verified by tools/mfma_layout.hip): lane l
-// holds A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15]; C[row 4(l>>4)+i][col l&15].
-#include "ops.h"
-#include "qtypes.h"
-#include <type_traits>
+// Tiles: Q4_K MUL_MAT runs the f16-operand tile (k_mmq_f16.hip); Q4_K MUL_MAT_ID (expert-sorted
+// pairs, all gemv order) and GGML_MI355X_MMQ_F16=0 run the int8 scale-folded tile below
+// (v_mfma_i32_16x16x64_i8); Q6_K / Q5_K run the class-exact tile (the vec_dot order).
+// MFMA layouts (tools/mfma_layout.hip, tools/mfma_probe.hip): 16x16x32 i8 / f16 lane l holds
+// A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15]; 16x16x64 i8 k 16(l>>4)+j;
+// C[row 4(l>>4)+i][col l&15].
+#include "mmq.h"
 
 namespace mi355x {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef float v4f __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void * lds_ptr_t;
-
 constexpr int MQ_BM = 64, MQ_BN = 64;
 
-// Q4_K weight block: per-row sub-scales and mins, and the A fragment of 32-element chunk c
-// (0..7), k = 8h .. 8h+7 (h = lane>>4)
-struct mq_q4_K {
-    static constexpr int BLK = 144, NSC = 8;
-    __device__ static void unpack(const uint8_t * b, int * sc, int * mn, float & d, float & dmin) {
-        d = h2f(ld2(b)); dmin = h2f(ld2(b + 2));
-        const uint8_t * q = b + 4;
-        for (int j = 0; j < 8; ++j) {
-            int s, m;
-            scale_min_k4(j, q, s, m);
-            sc[j] = s; mn[j] = m;
-        }
-    }
-    __device__ static long afrag(const uint8_t * b, int c, int h) {
-        // chunk c = 2g + hi: qs[32g + k] low (hi = 0) or high nibbles
-        const uint2 v = ld8(b + 16 + 32 * (c >> 1) + 8 * h);
-        const int sh = 4 * (c & 1);
-        const uint32_t lo = (v.x >> sh) & 0x0f0f0f0f, hi = (v.y >> sh) & 0x0f0f0f0f;
-        return (long) lo | ((long) hi << 32);
-    }
-};
 
-struct mmq_args {
-    const uint8_t * W; int64_t nb01; int64_t M; int64_t K; int64_t nblk;
-    const int8_t * xq; const float * xd; const int16_t * xs;   // Q8_K SoA: [T][K], [T][K/256], [T][K/16]
-    int64_t T;
-    int64_t gemm_cols;          // tokens below this take the gemm (per-pair) order, the rest the gemv order
-    float * dst; int64_t nb1;   // dst[t * nb1 + m*4]
-    // MUL_MAT_ID (expert-sorted, k_mmv.hip k_moe_sort): blockIdx.z = expert, its cnt[z] tokens are
-    // activation columns off[z] .. off[z] + cnt[z] - 1, column j is pair list[j] = e + n_used * t and
-    // lands at dst + e * nb1 + t * nb2; nullptr cnt = a plain MUL_MAT
-    const int32_t * cnt; const int32_t * off; const int32_t * list; int64_t n_used; int64_t nb02; int64_t nb2;
-};
 
-// Staging: the loads of K block b+1 are in flight while block b computes: the Q8_K token rows,
-// their scales d and bsums go HBM -> LDS by global_load_lds into the other of two stages, the
-// weight blocks go to registers and are written to that stage after the MFMA work.  One
-// s_waitcnt + barrier per block then finds the next stage landed.
-// The token tile is XOR-swizzled in LDS: the 16-byte chunk k of token row t sits in slot
-// k ^ (t & 15), so the 16 lanes of an MFMA B fragment (rows t = 16n + c16, same chunk) read 16
-// different bank groups instead of one (rows are 256 B = one bank period apart).  The swizzle
-// is applied on the source side of the LDS-DMA (each lane picks which chunk it fetches).
-template <class W> struct mq_stage {
-    static constexpr int RS = (W::BLK + 15) / 16 * 16;
-    static constexpr int XQ = MQ_BM * RS;            // token rows [64][256] after the weight tile
-    static constexpr int XD = XQ + MQ_BN * 256;      // token scales [64] f32
-    static constexpr int XS = XD + MQ_BN * 4;        // token bsums [64][16] i16
-    static constexpr int BYTES = XS + MQ_BN * 32;
-    static constexpr int RC = RS / 16;               // 16-byte chunks per weight row
-    static constexpr int NWR = (MQ_BM * RC + 255) / 256;   // weight chunks per thread
-};
-
-// two workgroups per CU (two stages of ~56 KB LDS each)
-template <class W>
-__global__ __launch_bounds__(256, 2) void k_mmq_q4K(const mmq_args p) {
-    using S = mq_stage<W>;
-    constexpr int RS = S::RS;
-    __shared__ __attribute__((aligned(16))) uint8_t st[2][S::BYTES];
-    __shared__ int wsc[MQ_BM][W::NSC];
-    __shared__ __attribute__((aligned(8))) int wmn[MQ_BM][8];
-    __shared__ float wd[MQ_BM], wdm[MQ_BM];
-    __shared__ __attribute__((aligned(8))) int xs[MQ_BN][8];   // Q8_K sums per 32-element chunk
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t row0 = (int64_t) blockIdx.x * MQ_BM;
-    const int64_t tok0 = (int64_t) blockIdx.y * MQ_BN;
-    const int h = lane >> 4, c16 = lane & 15;
-    const uint8_t * Wb = p.W;
-    int64_t T = p.T, col0 = 0;
-    if (p.cnt) {
-        T = p.cnt[blockIdx.z];
-        if (tok0 >= T) return;   // uniform: no barrier passed yet
-        col0 = p.off[blockIdx.z];
-        Wb = p.W + (int64_t) blockIdx.z * p.nb02;
-    }
-    const int64_t KB = p.K / 256;
-    // per token tile n: does this lane's token take the gemm (per-pair) order?
-    bool gemm[4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) gemm[n] = tok0 + 16 * n + c16 < p.gemm_cols;
-
-    // per-thread source pointers of block 0 (block b adds b * 256 / b / b * 16 / b * BLK)
-    const int8_t * xsrc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {   // token rows: instruction i = wave + 4k of 16
-        const int c = 64 * (wave + 4 * k) + lane, t = c >> 4, part = (c & 15) ^ (t & 15);   // LDS slot (t, c & 15) holds chunk (c & 15) ^ (t & 15)
-        xsrc[k] = p.xq + (col0 + min(tok0 + t, T - 1)) * p.K + 16 * part;
-    }
-    const float * dsrc = p.xd + (col0 + min(tok0 + lane, T - 1)) * KB;
-    const int16_t * ssrc;
-    {
-        const int c = 64 * (wave == 2 ? 1 : 0) + lane, t = c >> 1, half = c & 1;
-        ssrc = p.xs + (col0 + min(tok0 + t, T - 1)) * (p.K / 16) + 8 * half;
-    }
-    const uint8_t * wsrc[S::NWR];
-#pragma unroll
-    for (int j = 0; j < S::NWR; ++j) {
-        const int c = min(tid + 256 * j, MQ_BM * S::RC - 1);
-        const int r = c / S::RC, k = c % S::RC;
-        wsrc[j] = Wb + min(row0 + r, p.M - 1) * p.nb01 + 16 * k;
-    }
-    // token-side loads of block b into stage s (LDS-DMA: 1 KiB, or 256 B, per wave instruction)
-    auto issue_x = [&](int64_t b, int s) {
-        uint8_t * base = st[s];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            __builtin_amdgcn_global_load_lds((const void *) (xsrc[k] + b * 256), (lds_ptr_t) (base + S::XQ + 1024 * (wave + 4 * k)), 16, 0, 0);
-        }
-        if (wave == 0) {   // scales: one 4-byte load per token
-            __builtin_amdgcn_global_load_lds((const void *) (dsrc + b), (lds_ptr_t) (base + S::XD), 4, 0, 0);
-        } else if (wave <= 2) {   // bsums: 32 B per token, two instructions
-            __builtin_amdgcn_global_load_lds((const void *) (ssrc + b * 16), (lds_ptr_t) (base + S::XS + 1024 * (wave - 1)), 16, 0, 0);
-        }
-    };
-    uint4 wr[S::NWR];
-    auto load_w = [&](int64_t b) {
-#pragma unroll
-        for (int j = 0; j < S::NWR; ++j) {
-            if (tid + 256 * j < MQ_BM * S::RC) wr[j] = ld16(wsrc[j] + b * W::BLK);
-        }
-    };
-    auto store_w = [&](int s) {
-#pragma unroll
-        for (int j = 0; j < S::NWR; ++j) {
-            const int c = tid + 256 * j;
-            if (c < MQ_BM * S::RC) *(uint4 *) (st[s] + c * 16) = wr[j];   // row r, chunk k at r * RS + 16 k = 16 c
-        }
-    };
-
-    // the CPU's two fp32 chains per output (qtypes.h g_q4_K_p)
-    float A[4][4], B[4][4];
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) A[n][i] = B[n][i] = 0.0f;
-
-    issue_x(0, 0);
-    load_w(0);
-    store_w(0);
-    for (int64_t b = 0; b < p.nblk; ++b) {
-        const int s = (int) (b & 1);
-        const uint8_t * wq = st[s];
-        const int8_t * xq = (const int8_t *) (st[s] + S::XQ);
-        const float * xd = (const float *) (st[s] + S::XD);
-        // stage s has landed for every wave, and block b-1's reads of stage s^1 are done
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const bool more = b + 1 < p.nblk;
-        if (more) {
-            issue_x(b + 1, s ^ 1);
-            load_w(b + 1);
-        }
-        // ---- per-row scales and per-token chunk sums of block b ----------------------------
-        if (tid < MQ_BM) {
-            int sc[16], mn[8];
-            float d, dmin;
-            W::unpack(wq + tid * RS, sc, mn, d, dmin);
-#pragma unroll
-            for (int j = 0; j < W::NSC; ++j) wsc[tid][j] = sc[j];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) wmn[tid][j] = mn[j];
-            wd[tid] = d; wdm[tid] = dmin;
-        } else if (tid < MQ_BM + MQ_BN) {
-            const int t = tid - MQ_BM;
-            const int16_t * s16 = (const int16_t *) (st[s] + S::XS) + 16 * t;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) xs[t][j] = s16[2 * j] + s16[2 * j + 1];
-        }
-        __syncthreads();
-        // scale products d·dy and dmin·dy of this lane's 4 rows x 4 tokens, as the CPU forms them
-        float dw[4], dmw[4], dy[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { dw[i] = wd[16 * wave + 4 * h + i]; dmw[i] = wdm[16 * wave + 4 * h + i]; }
-#pragma unroll
-        for (int n = 0; n < 4; ++n) dy[n] = xd[16 * n + c16];
-        int ib[4][4], mb[4][4];   // block sums of the gemv (tail) tokens
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ib[n][i] = mb[n][i] = 0;
-        const int rA = 16 * wave + c16;
-#pragma unroll 1
-        for (int k = 0; k < 4; ++k) {   // sub-block pairs
-            int ip[4][4];
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) ip[n][i] = 0;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int c = 2 * k + u;
-                const long a = W::afrag(wq + rA * RS, c, h);
-                int scv[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) scv[i] = wsc[16 * wave + 4 * h + i][c];
-#pragma unroll
-                for (int n = 0; n < 4; ++n) {
-                    const long bf = *(const long *) (xq + (16 * n + c16) * 256 + 16 * ((2 * c + (h >> 1)) ^ c16) + 8 * (h & 1));
-                    v4i r = {0, 0, 0, 0};
-                    r = __builtin_amdgcn_mfma_i32_16x16x32_i8(a, bf, r, 0, 0, 0);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) ip[n][i] += __mul24(r[i], scv[i]);
-                }
-            }
-            // the pair's mins integer m_2k·bsum_2k + m_2k+1·bsum_2k+1 (exact)
-            int2 mr[4], xt[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) mr[i] = *(const int2 *) &wmn[16 * wave + 4 * h + i][2 * k];
-#pragma unroll
-            for (int n = 0; n < 4; ++n) xt[n] = *(const int2 *) &xs[16 * n + c16][2 * k];
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int mn = __mul24(mr[i].x, xt[n].x) + __mul24(mr[i].y, xt[n].y);
-                    if (gemm[n]) {
-                        A[n][i] = fmaf((float) ip[n][i], dw[i] * dy[n], A[n][i]);
-                        B[n][i] = fmaf((float) mn, dmw[i] * dy[n], B[n][i]);
-                    } else {
-                        ib[n][i] += ip[n][i];
-                        mb[n][i] += mn;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            if (gemm[n]) continue;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                A[n][i] = fmaf((float) ib[n][i], dw[i] * dy[n], A[n][i]);
-                B[n][i] = fmaf((float) mb[n][i], dmw[i] * dy[n], B[n][i]);
-            }
-        }
-        // block b+1's weights into the other stage (its readers, block b-1, passed the barrier)
-        if (more) store_w(s ^ 1);
-    }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const int64_t t = tok0 + 16 * n + c16;
-        if (t >= T) continue;
-        char * drow = (char *) p.dst + t * p.nb1;
-        if (p.cnt) {
-            const int pair = p.list[col0 + t];
-            drow = (char *) p.dst + (pair % p.n_used) * p.nb1 + (pair / p.n_used) * p.nb2;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t m = row0 + 16 * wave + 4 * h + i;
-            if (m < p.M) *(float *) (drow + m * 4) = __fsub_rn(A[n][i], B[n][i]);
-        }
-    }
-}
 
 // ==== Q4_K on v_mfma_i32_16x16x64_i8 with scale-folded weights (the repacked gemm/gemv order) ========
 // The gemm's integer per sub-block pair, I_pair = sc_2k·<q_2k, y> + sc_2k+1·<q_2k+1, y>, is a
@@ -557,248 +297,6 @@ __global__ __launch_bounds__(256, 2) void k_mmq_q4Kf(const mmq_args p) {
     }
 }
 
-// ==== Q4_K on f16 MFMA: exact integers in f32 accumulators (the repacked gemm/gemv order) ======
-// The scale-folded weight w' = sc·q <= 945 and the Q8_K value y in [-128, 127] are exact f16, every
-// product (<= 120960) and every partial sum of a sub-block pair (<= 64·120960 < 2^23) is an exact
-// f32 integer, so v_mfma_f32_16x16x32_f16 returns the pair's integer I_pair as a float with no
-// rounding in any summation order — the CPU's (float) I_pair — and the VALU is left with the two
-// chain FMAs per output.  The mins integer of a pair is one v_mfma_f32_16x16x16_f16 over the 16
-// sums of 16 Q8_K values (|sum| <= 2048: exact f16) with the sums outside the pair zeroed.
-// 64 rows x 64 tokens per workgroup of 4 waves (two workgroups per CU); wave w multiplies the 64
-// rows with tokens 16w .. +15.  The folded weight planes are the only LDS data (double-buffered: the fold of
-// block b+1 overlaps block b, one barrier per block; 16-byte chunk c of row r in slot c ^ (r & 15)
-// so every ds_read_b128 lane group hits distinct banks); each wave streams its 16 tokens' Q8_K
-// bytes straight into registers one block ahead and widens them to f16 there
-// ((0x6400 | (y ^ 0x80)) - 1152 = y, exact).
-constexpr int MH_BM = 64, MH_BN = 64;
-
-typedef _Float16 mh8 __attribute__((ext_vector_type(8)));
-typedef _Float16 mh4 __attribute__((ext_vector_type(4)));
-typedef _Float16 mh2 __attribute__((ext_vector_type(2)));
-
-struct mh_tok {   // one K block of a lane's token: bytes 64pp + 16h .. +15 per pair, the 16-sums of
-    uint4 x[4];   // slots 4h .. 4h+3, d
-    uint2 s;
-    float d;
-};
-
-// 8 int8 (two words) -> 8 f16, exact
-__device__ __forceinline__ mh8 i8x8_f16(uint32_t w0, uint32_t w1) {
-    const mh2 off = {(_Float16) -1152.0f, (_Float16) -1152.0f};
-    const uint32_t u[2] = {w0 ^ 0x80808080u, w1 ^ 0x80808080u};
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        o[2 * k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(mh2, __builtin_amdgcn_perm(0x64646464u, u[k], 0x04010400u)) + off);
-        o[2 * k + 1] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(mh2, __builtin_amdgcn_perm(0x64646464u, u[k], 0x04030402u)) + off);
-    }
-    const uint4 r = make_uint4(o[0], o[1], o[2], o[3]);
-    return __builtin_bit_cast(mh8, r);
-}
-
-__global__ __launch_bounds__(256, 2) void k_mmq_q4Kh(const mmq_args p) {
-    __shared__ __attribute__((aligned(16))) uint8_t wpl[2][MH_BM * 512];
-    __shared__ __attribute__((aligned(16))) uint32_t wmn[2][MH_BM][4];   // f16 (m_2p, m_2p+1) per pair
-    __shared__ __attribute__((aligned(16))) float wd[2][MH_BM], wdm[2][MH_BM];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int64_t bx = blockIdx.x, by = blockIdx.y;
-    if ((gridDim.x & 7) == 0) {   // XCD-major: one row tile's token tiles on one XCD
-        const int64_t id = bx + (int64_t) gridDim.x * by, j = id >> 3;
-        by = j % gridDim.y;
-        bx = (j / gridDim.y) * 8 + (id & 7);
-    }
-    const int64_t row0 = bx * MH_BM, tok0 = by * MH_BN, T = p.T;
-    const int h = lane >> 4, c16 = lane & 15;
-    const int tg = wave, rg = 0;
-    const int64_t KB = p.K / 256;
-    const int64_t tok = tok0 + 16 * tg + c16;                // this lane's token
-    const bool gemm = tok < p.gemm_cols;
-    const bool allg = tok0 + 16 * tg + 15 < p.gemm_cols;     // uniform: the wave's 16 tokens all gemm-order
-
-    // token side: straight to registers
-    const int64_t tl = min(tok, T - 1);
-    const int8_t * xrow = p.xq + tl * p.K + 16 * h;
-    const int16_t * srow = p.xs + tl * (p.K / 16) + 4 * h;
-    const float * drow_ = p.xd + tl * KB;
-    auto load_x = [&](int64_t b, mh_tok & o) __attribute__((always_inline)) {
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) o.x[pp] = *(const uint4 *) (xrow + b * 256 + 64 * pp);
-        o.s = *(const uint2 *) (srow + b * 16);
-        o.d = drow_[b];
-    };
-    // weight side: thread (row fr, pair fq) folds 64 weights into f16
-    const int fr = tid >> 2, fq = tid & 3;
-    const uint8_t * wrow = p.W + min(row0 + fr, p.M - 1) * p.nb01;
-    uint4 whdr, wqa, wqb;
-    auto load_w = [&](int64_t b) __attribute__((always_inline)) {
-        const uint8_t * blk = wrow + b * 144;
-        whdr = ld16(blk);
-        wqa = ld16(blk + 16 + 32 * fq);
-        wqb = ld16(blk + 32 + 32 * fq);
-    };
-    auto fold_w = [&](int buf) __attribute__((always_inline)) {
-        int sc_lo, sc_hi, m_lo, m_hi;
-        k4_scales_g(whdr.y, whdr.z, whdr.w, fq, sc_lo, sc_hi, m_lo, m_hi);
-        const uint32_t q[8] = {wqa.x, wqa.y, wqa.z, wqa.w, wqb.x, wqb.y, wqb.z, wqb.w};
-        uint8_t * dp = wpl[buf] + fr * 512;
-        // (1024 + q)·sc - 1024·sc = q·sc, one rounding of an exact f16 value; chunk 8fq + k
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int half = k >> 2;
-            const _Float16 sc = (_Float16) (half ? sc_hi : sc_lo);
-            const mh2 s2 = {sc, sc}, n2 = {(_Float16) -1024.0f * sc, (_Float16) -1024.0f * sc};
-            uint32_t o[4];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const uint32_t w = q[2 * (k & 3) + u];
-                const uint32_t nb = half ? (w >> 4) & 0x0f0f0f0fu : w & 0x0f0f0f0fu;
-                const mh2 lo = __builtin_bit_cast(mh2, __builtin_amdgcn_perm(0x64646464u, nb, 0x04010400u));
-                const mh2 hi = __builtin_bit_cast(mh2, __builtin_amdgcn_perm(0x64646464u, nb, 0x04030402u));
-                o[2 * u] = __builtin_bit_cast(uint32_t, __builtin_elementwise_fma(lo, s2, n2));
-                o[2 * u + 1] = __builtin_bit_cast(uint32_t, __builtin_elementwise_fma(hi, s2, n2));
-            }
-            *(uint4 *) (dp + 16 * ((8 * fq + k) ^ (fr & 15))) = make_uint4(o[0], o[1], o[2], o[3]);
-        }
-        const mh2 mm = {(_Float16) m_lo, (_Float16) m_hi};
-        wmn[buf][fr][fq] = __builtin_bit_cast(uint32_t, mm);
-        if (fq == 0) { wd[buf][fr] = h2f(whdr.x & 0xffff); wdm[buf][fr] = h2f(whdr.x >> 16); }
-    };
-
-    float A[4][4], B[4][4];   // [row tile][row 4h + i]
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) A[r][i] = B[r][i] = 0.0f;
-
-    auto compute = [&](int buf, const mh_tok & x, auto allg_c) __attribute__((always_inline)) {
-        constexpr bool ALLG = decltype(allg_c)::value;
-        const uint8_t * pl = wpl[buf];
-        // the token's block as f16 fragments, and its 16-sums (|sum| <= 2048: exact f16) — per
-        // pair pp only slots 4pp .. 4pp+3, held by lanes h == pp
-        mh8 bf[4][2];
-        mh4 bz[4];
-        {
-            const mh4 sf = {(_Float16) (int16_t) (x.s.x & 0xffff), (_Float16) (int16_t) (x.s.x >> 16),
-                            (_Float16) (int16_t) (x.s.y & 0xffff), (_Float16) (int16_t) (x.s.y >> 16)};
-#pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-                bf[pp][0] = i8x8_f16(x.x[pp].x, x.x[pp].y);
-                bf[pp][1] = i8x8_f16(x.x[pp].z, x.x[pp].w);
-                bz[pp] = h == pp ? sf : (mh4){0, 0, 0, 0};
-            }
-        }
-        // row tile r's LDS operands (A fragments, d / dmin, mins) are read while tile r-1 computes
-        mh8 af[2][4][2];
-        float4 dwv[2], dmv[2];
-        uint32_t wmv[2];
-        auto lda = [&](int r, int sl) __attribute__((always_inline)) {
-            const int rb = 64 * rg + 16 * r;
-            const uint8_t * ar = pl + (rb + c16) * 512;
-#pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-                af[sl][pp][0] = *(const mh8 *) (ar + 16 * ((8 * pp + 2 * h) ^ c16));
-                af[sl][pp][1] = *(const mh8 *) (ar + 16 * ((8 * pp + 2 * h + 1) ^ c16));
-            }
-            dwv[sl] = *(const float4 *) &wd[buf][rb + 4 * h];
-            dmv[sl] = *(const float4 *) &wdm[buf][rb + 4 * h];
-            wmv[sl] = wmn[buf][rb + c16][h];
-        };
-        lda(0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int sl = r & 1;
-            if (r < 3) lda(r + 1, sl ^ 1);
-            __builtin_amdgcn_sched_barrier(0);   // the next tile's reads are in flight; bounded live ranges
-            // the CPU's scale products d·dy, dmin·dy of rows rb + 4h + i
-            const float sA[4] = {dwv[sl].x * x.d, dwv[sl].y * x.d, dwv[sl].z * x.d, dwv[sl].w * x.d};
-            const float sB[4] = {dmv[sl].x * x.d, dmv[sl].y * x.d, dmv[sl].z * x.d, dmv[sl].w * x.d};
-            // mins operand of row rb + c16: slots 4h .. 4h+3 are sub-blocks 2h, 2h, 2h+1, 2h+1
-            const uint32_t w = wmv[sl];
-            const mh4 mA = __builtin_bit_cast(mh4, make_uint2(__builtin_amdgcn_perm(w, w, 0x01000100u), __builtin_amdgcn_perm(w, w, 0x03020302u)));
-            int ib[4], mb[4];   // gemv-order sums (exact ints: a block's I can pass 2^24)
-            if constexpr (!ALLG) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) ib[i] = mb[i] = 0;
-            }
-#pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-                const v4f z = {0.f, 0.f, 0.f, 0.f};
-                v4f I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][pp][0], bf[pp][0], z, 0, 0, 0);
-                I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][pp][1], bf[pp][1], I, 0, 0, 0);
-                const v4f Im = __builtin_amdgcn_mfma_f32_16x16x16f16(mA, bz[pp], z, 0, 0, 0);
-                if constexpr (ALLG) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        A[r][i] = fmaf(I[i], sA[i], A[r][i]);
-                        B[r][i] = fmaf(Im[i], sB[i], B[r][i]);
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        if (gemm) {
-                            A[r][i] = fmaf(I[i], sA[i], A[r][i]);
-                            B[r][i] = fmaf(Im[i], sB[i], B[r][i]);
-                        } else {
-                            ib[i] += (int) I[i];
-                            mb[i] += (int) Im[i];
-                        }
-                    }
-                }
-            }
-            if constexpr (!ALLG) {
-                if (!gemm) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        A[r][i] = fmaf((float) ib[i], sA[i], A[r][i]);
-                        B[r][i] = fmaf((float) mb[i], sB[i], B[r][i]);
-                    }
-                }
-            }
-        }
-    };
-
-    mh_tok xa, xb;
-    load_w(0);
-    load_x(0, xa);
-    fold_w(0);
-    load_w(min((int64_t) 1, p.nblk - 1));
-    // block b: planes[b & 1] were folded during block b-1; the fold of b+1 (planes[(b+1) & 1],
-    // last read in block b-1) and the token loads of b+1 overlap block b's MFMAs
-    // (no branches around the loads: the last blocks re-load the final block, so the memory
-    // counter waits stay exact instead of draining every load at each block)
-    auto step = [&](int64_t b, mh_tok & cur, mh_tok & nxt, auto allg_c) __attribute__((always_inline)) {
-        __syncthreads();
-        load_x(min(b + 1, p.nblk - 1), nxt);
-        fold_w((int) ((b + 1) & 1));
-        load_w(min(b + 2, p.nblk - 1));
-        compute((int) (b & 1), cur, allg_c);
-    };
-    auto run = [&](auto allg_c) __attribute__((always_inline)) {
-        for (int64_t b = 0; b < p.nblk; ++b) {
-            step(b, xa, xb, allg_c);
-            xa = xb;
-        }
-    };
-    if (allg) run(std::integral_constant<bool, true>());
-    else run(std::integral_constant<bool, false>());
-    if (tok < T) {
-        char * drow = (char *) p.dst + tok * p.nb1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t m0 = row0 + 64 * rg + 16 * r + 4 * h;
-            if (m0 + 3 < p.M) {
-                *(float4 *) (drow + m0 * 4) = make_float4(__fsub_rn(A[r][0], B[r][0]), __fsub_rn(A[r][1], B[r][1]),
-                                                          __fsub_rn(A[r][2], B[r][2]), __fsub_rn(A[r][3], B[r][3]));
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (m0 + i < p.M) *(float *) (drow + (m0 + i) * 4) = __fsub_rn(A[r][i], B[r][i]);
-            }
-        }
-    }
-}
-
 // ==== class-exact prefill tile for Q6_K / Q5_K (the vec_dot order, qtypes.h) ====================
 // The CPU's vec_dot keeps, per 256-block, eight integer "class" sums (class c = bytes 4c..4c+3
 // of every 32-element chunk) and runs eight fp32 chains acc[c] = fma(dy·d, cls_b[c], acc[c])
@@ -900,8 +398,6 @@ struct mc_q5_K {
         for (int s = 0; s < 8; ++s) { int sc; scmin(r, s, sc, mn[s]); }
     }
 };
-
-typedef float v4f __attribute__((ext_vector_type(4)));
 
 // 512 threads: wave w computes rows 16 (w & 3) .. +15 of the 64-row tile for tokens 32 (w >> 2) ..
 // +31 (two 16-token MFMA tiles): 8 x 2 x 4 = 64 chain registers per lane
@@ -1092,13 +588,7 @@ static void launch_cls(hipStream_t st, const dim3 & grid, const mmq_args & p) {
 
 static void launch_mmq(hipStream_t st, ggml_type t, const dim3 & grid, const mmq_args & p) {
     switch (t) {
-        case GGML_TYPE_Q4_K: {
-            // GGML_MI355X_MMQ_FOLD=0: the 16x16x32 tile with VALU scales (k_mmq_q4K)
-            static const bool fold = !getenv("GGML_MI355X_MMQ_FOLD") || atoi(getenv("GGML_MI355X_MMQ_FOLD")) != 0;
-            if (fold) hipLaunchKernelGGL(k_mmq_q4Kf, grid, dim3(256), 0, st, p);
-            else hipLaunchKernelGGL(k_mmq_q4K<mq_q4_K>, grid, dim3(256), 0, st, p);
-            break;
-        }
+        case GGML_TYPE_Q4_K: hipLaunchKernelGGL(k_mmq_q4Kf, grid, dim3(256), 0, st, p); break;
         case GGML_TYPE_Q5_K: launch_cls<mc_q5_K>(st, grid, p); break;
         case GGML_TYPE_Q6_K: launch_cls<mc_q6_K>(st, grid, p); break;
         default: GGML_ABORT("mi355x: mmq type");
@@ -1139,8 +629,9 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
     // Q4_K: the f16-operand tile (GGML_MI355X_MMQ_F16=0: the int8 one)
     static const bool f16_on = !getenv("GGML_MI355X_MMQ_F16") || atoi(getenv("GGML_MI355X_MMQ_F16")) != 0;
     if (w->type == GGML_TYPE_Q4_K && f16_on) {
-        const dim3 grid((unsigned) ceil_div(p.M, MH_BM), (unsigned) ceil_div(p.T, MH_BN));
-        hipLaunchKernelGGL(k_mmq_q4Kh, grid, dim3(256), 0, ctx.stream, p);
+        // GGML_MI355X_MMQ_NW=8: 128-token workgroups of 8 waves (the fold is shared by twice the tokens)
+        static const int nw = getenv("GGML_MI355X_MMQ_NW") ? atoi(getenv("GGML_MI355X_MMQ_NW")) : 4;
+        launch_mmq_q4Kh(ctx.stream, p, nw);
     } else {
         const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(p.T, MQ_BN));
         launch_mmq(ctx.stream, w->type, grid, p);

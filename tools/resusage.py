@@ -7,7 +7,7 @@ import sys
 
 src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
-cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-munsafe-fp-atomics", "-ffp-contract=off", *(["-fno-slp-vectorize"] if "k_mmq" in sys.argv[1] else []),
+cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-munsafe-fp-atomics", "-ffp-contract=off", *(["-fno-slp-vectorize"] if "k_mmq_f16" in sys.argv[1] else []),
        "-DGGML_BACKEND_SHARED", "-DGGML_BACKEND_BUILD", "-DGGML_SHARED", "-DGGML_BACKEND_DL", "-DNDEBUG",
        "-I/root/reference/ggml/include", "-I/root/reference/ggml/src", "-Illamacog_amd/csrc", "--offload-device-only",
        "-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", "/tmp/_resusage.o"]
