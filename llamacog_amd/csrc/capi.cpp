@@ -542,6 +542,53 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
         float chk[4];
         MI_CHECK(hipMemcpy(chk, (const char *) Dm.data + (M * T / 2) * 4, sizeof(chk), hipMemcpyDeviceToHost));
         fprintf(stderr, "mmq probe M=%lld T=%lld: dst[mid] %g %g %g %g\n", (long long) M, (long long) T, chk[0], chk[1], chk[2], chk[3]);
+    } else if (which == 302) {
+        // prefill flash attention: D = 128, 32 query heads over 8 KV heads, a query rows = a cache
+        // rows with the causal mask, random data (phase cycles of workgroup (0, 0) when b != 0)
+        const int64_t D = 128, H = 32, Hkv = 8, nq = a, n_kv = a;
+        std::vector<float> hq(D * H * nq);
+        std::vector<uint16_t> hk(D * Hkv * n_kv), hv(D * Hkv * n_kv), hm(n_kv * nq);
+        uint32_t st = 12345;
+        auto rnd = [&]() { st = st * 1664525u + 1013904223u; return ((st >> 8) & 0xffff) / 65536.0f - 0.5f; };
+        for (auto & x : hq) x = rnd();
+        auto f16b = [](float f) { const _Float16 h = (_Float16) f; uint16_t u; memcpy(&u, &h, 2); return u; };
+        for (auto & x : hk) x = f16b(rnd());
+        for (auto & x : hv) x = f16b(rnd());
+        for (int64_t i = 0; i < nq; ++i)
+            for (int64_t j = 0; j < n_kv; ++j) hm[i * n_kv + j] = j <= i ? 0 : 0xFC00;
+        float * q = (float *) dalloc(hq.size() * 4, 0);
+        void * k = dalloc(hk.size() * 2, 0);
+        void * v = dalloc(hv.size() * 2, 0);
+        uint16_t * m = (uint16_t *) dalloc(hm.size() * 2, 0);
+        MI_CHECK(hipMemcpy(q, hq.data(), hq.size() * 4, hipMemcpyHostToDevice));
+        MI_CHECK(hipMemcpy(k, hk.data(), hk.size() * 2, hipMemcpyHostToDevice));
+        MI_CHECK(hipMemcpy(v, hv.data(), hv.size() * 2, hipMemcpyHostToDevice));
+        MI_CHECK(hipMemcpy(m, hm.data(), hm.size() * 2, hipMemcpyHostToDevice));
+        float * out = (float *) dalloc(D * H * nq * 4, 0);
+        const int64_t neq[4] = {D, nq, H, 1};
+        init_tensor(Q, GGML_TYPE_F32, neq, q);
+        std::swap(Q.nb[1], Q.nb[2]);   // [D, nq, H] view of rows laid out [nq][H][D]
+        Q.nb[1] = D * H * 4; Q.nb[2] = D * 4; Q.nb[3] = D * H * nq * 4;
+        const int64_t nek[4] = {D, n_kv, Hkv, 1};
+        init_tensor(K, GGML_TYPE_F16, nek, k);
+        K.nb[1] = D * Hkv * 2; K.nb[2] = D * 2; K.nb[3] = D * Hkv * n_kv * 2;
+        init_tensor(V, GGML_TYPE_F16, nek, v);
+        V.nb[1] = D * Hkv * 2; V.nb[2] = D * 2; V.nb[3] = D * Hkv * n_kv * 2;
+        const int64_t nem[4] = {n_kv, nq, 1, 1}, neo[4] = {D, H, nq, 1};
+        init_tensor(Mk, GGML_TYPE_F16, nem, m);
+        init_tensor(O, GGML_TYPE_F32, neo, out);
+        O.op = GGML_OP_FLASH_ATTN_EXT;
+        O.src[0] = &Q; O.src[1] = &K; O.src[2] = &V; O.src[3] = &Mk;
+        const float scale = 0.088f, zero = 0.0f;
+        memcpy(O.op_params, &scale, 4);
+        memcpy(O.op_params + 1, &zero, 4);
+        memcpy(O.op_params + 2, &zero, 4);
+        if (b) {
+            MI_CHECK(hipMalloc(&prof, 6 * sizeof(unsigned long long)));
+            MI_CHECK(hipMemset(prof, 0, 6 * sizeof(unsigned long long)));
+            g_fa_prof = prof;
+        }
+        run = [&] { op_flash_attn(sc.ex, &O); };
     } else if (which >= 100) {
         // streaming read of a bytes per launch over b rotating copies, grid = which - 100 (x64)
         const int64_t bytes = a, copies = std::max<int64_t>(1, b);
@@ -622,6 +669,8 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
         unsigned long long h[6];
         MI_CHECK(hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost));
         const char * nm[6] = {"A(mask)", "0(V issue)", "1(scores)", "2(softmax coef)", "3(wait V)", "3(recurrence)"};
+        const char * nmp[6] = {"barrier+wait", "1(scores)", "2(coef)", "3(recurrence)", "chunks", "-"};
+        if (which == 302) for (int i = 0; i < 6; ++i) nm[i] = nmp[i];
         fprintf(stderr, "FA phases (s_memtime ticks per launch, wg 0):");
         for (int i = 0; i < 6; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double) h[i] / (iters + 3));
         fprintf(stderr, "\n");

@@ -586,6 +586,22 @@ __device__ __forceinline__ float dot_f16_mix_d128(const uint2 (&kh)[8], const fl
     return __fadd_rn(__fadd_rn(w[0], w[2]), __fadd_rn(w[1], w[3]));
 }
 
+// wave-wide inclusive max-scan by DPP (rows by row_shr 1/2/4/8, then row_bcast:15 / :31 —
+// GFX9 DPP), and the exclusive shift by one lane (wave_shr:1); absent sources read -inf
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp_ninf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp((int) 0xff800000u, __float_as_int(v), CTRL, ROWS, 0xf, false));
+}
+__device__ __forceinline__ float wave_scan_max(float x) {
+    x = fmaxf(x, dpp_ninf<0x111>(x));
+    x = fmaxf(x, dpp_ninf<0x112>(x));
+    x = fmaxf(x, dpp_ninf<0x114>(x));
+    x = fmaxf(x, dpp_ninf<0x118>(x));
+    x = fmaxf(x, dpp_ninf<0x142, 0xa>(x));
+    x = fmaxf(x, dpp_ninf<0x143, 0xc>(x));
+    return x;
+}
+
 template <int G>
 __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
     constexpr int D = 128, NM = D / 16, QB = PF_P / G;
@@ -629,6 +645,12 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
         nend = max(max(wend[0], wend[1]), max(wend[2], wend[3])) + 1;
     }
     const int nchunk = (int) ((nend + PF_CH - 1) / PF_CH);
+    // microbenchmark hook: per-phase s_memtime cycles of workgroup (0, 0) wave 0 (capi.cpp op 302)
+    const bool prof = a.prof && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0;
+    unsigned long long tp = prof ? __builtin_amdgcn_s_memtime() : 0, pc[6] = {0, 0, 0, 0, 0, 0};
+    auto mark = [&](int i) {
+        if (prof) { const unsigned long long t = __builtin_amdgcn_s_memtime(); pc[i] += t - tp; tp = t; }
+    };
 
     // ---- staging: K (swizzled) and V rows of a chunk by LDS-DMA, its mask through registers -----
     auto issue_kv = [&](int c, int s) {
@@ -705,6 +727,7 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
             issue_kv(c + 1, s ^ 1);
             load_mask(c + 1);
         }
+        mark(0);
         const uint16_t * ks = kl[s];
         const uint16_t * ms = ml[s];
         // ---- phase 1: scores of the wave's 4 pairs x 64 positions --------------------------
@@ -723,6 +746,7 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
             }
         }
         asm volatile("" ::: "memory");
+        mark(1);
         // ---- phase 2: per pair, the prefix max and the (ms, vs) coefficient of every position -
         // per pair: positions that update the running max / that are masked (uniform)
         uint64_t upd[4], dead[4];
@@ -731,15 +755,8 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
             const int p = 4 * wave + i, j = lane;
             const bool live = c0 + j < nend && ms[(p / G) * PF_CH + j] != 0xfc00;
             const float sj = live ? sc[j * PF_P + p] : -INFINITY;
-            float sm = sj;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const float t = __shfl_up(sm, o, WAVE);
-                if (lane >= o) sm = fmaxf(sm, t);
-            }
-            float M = mc[i];
-            const float ex = __shfl_up(sm, 1, WAVE);
-            if (lane > 0) M = fmaxf(M, ex);
+            const float sm = wave_scan_max(sj);
+            const float M = fmaxf(mc[i], dpp_ninf<0x138>(sm));   // max over every position before j
             float vs, mv;
             if (!live) { mv = 1.0f; vs = 0.0f; }
             else if (sj > M) { mv = M == -INFINITY ? 0.0f : expf_cr(M - sj); vs = 1.0f; }
@@ -748,23 +765,26 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
             sc[j * PF_P + p] = vs;
             upd[i] = __ballot(live && sj > M);
             dead[i] = __ballot(!live);
-            mc[i] = fmaxf(mc[i], __shfl(sm, 63, WAVE));
+            mc[i] = fmaxf(mc[i], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), 63)));
         }
         asm volatile("" ::: "memory");
+        mark(2);
         // ---- phase 3: the f16 recurrence, 2 dims x 4 pairs per lane (V from LDS) ------------
         {
             const int nrun = (int) min((int64_t) PF_CH, nend - c0);
             const uint32_t * vrow = (const uint32_t *) vl[s] + lane;   // dims 2 lane, 2 lane + 1
             const float * scw = sc + 4 * wave;
             const float * cmw = cm + 4 * wave;
-            for (int j0 = 0; j0 < nrun; j0 += PF_U) {
-                uint32_t vv[PF_U];
-                float4 vs[PF_U];
+            // batch j0's V values and coefficients are read while batch j0 - U computes (a read
+            // past the chunk end lands in other LDS data and is never used)
+            auto ldb = [&](int j0, uint32_t (&vv)[PF_U], float4 (&vs)[PF_U]) __attribute__((always_inline)) {
 #pragma unroll
                 for (int u = 0; u < PF_U; ++u) {
                     vv[u] = vrow[(j0 + u) * (D / 2)];
                     vs[u] = *(const float4 *) (scw + (j0 + u) * PF_P);
                 }
+            };
+            auto run = [&](int j0, const uint32_t (&vv)[PF_U], const float4 (&vs)[PF_U]) __attribute__((always_inline)) {
                 const uint64_t ev = (upd[0] | upd[1] | upd[2] | upd[3] | dead[0] | dead[1] | dead[2] | dead[3]) >> j0;
                 if ((ev & ((1ull << PF_U) - 1)) == 0) {
 #pragma unroll
@@ -804,9 +824,24 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
                         }
                     }
                 }
+            };
+            uint32_t va[PF_U], vb[PF_U];
+            float4 sa[PF_U], sb[PF_U];
+            ldb(0, va, sa);
+            for (int j0 = 0; j0 < nrun; j0 += 2 * PF_U) {
+                ldb(j0 + PF_U, vb, sb);
+                run(j0, va, sa);
+                if (j0 + PF_U >= nrun) break;
+                ldb(j0 + 2 * PF_U, va, sa);
+                run(j0 + PF_U, vb, sb);
             }
         }
         if (more) store_mask(s ^ 1);   // published by the next chunk's barrier
+        mark(3);
+    }
+    if (prof) {
+        for (int i = 0; i < 4; ++i) a.prof[i] += pc[i];
+        a.prof[4] += (unsigned long long) nchunk;
     }
     // ---- output O = y / S --------------------------------------------------------------------
 #pragma unroll
