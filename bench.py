@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--config", default=None, help="default: llama3-8b-q4km at --gpus 1, llama3-70b-q4km above")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only)")
     ap.add_argument("--pp", type=int, default=512, help="prompt length for the pp figure (0 = skip)")
+    ap.add_argument("--pp-reps", type=int, default=3, help="timed pp runs after the warmup run (mean tok/s)")
     ap.add_argument("--fa", type=int, default=1)
     ap.add_argument("--kv", default="f16")
     ap.add_argument("--depth", type=int, default=0, help="KV depth before the timed steps (llama-bench -d)")
@@ -198,13 +199,17 @@ def run_worker(a, la, path, gpu, n_ctx, split, dist) -> dict:
     if a.verbose:
         print(la.log_tail(m.lib)[-4000:], file=sys.stderr)
 
-    # pp figure (one ubatch of a.pp tokens, as llama-bench pp512)
+    # pp figure (one ubatch of a.pp tokens, as llama-bench pp512: one warmup prompt of the same
+    # length, tools/llama-bench/llama-bench.cpp:1933-1945, then the mean of --pp-reps runs' tok/s)
     r["pp_tps"] = None
     if a.pp > 0:
         m.clear()
-        m.time_prompt(min(a.pp, 64))  # warm
-        m.clear()
-        r["pp_tps"] = a.pp / m.time_prompt(a.pp)
+        m.time_prompt(a.pp)  # warm
+        tps = []
+        for _ in range(max(1, a.pp_reps)):
+            m.clear()
+            tps.append(a.pp / m.time_prompt(a.pp))
+        r["pp_tps"] = sum(tps) / len(tps)
 
     # tg: W untimed decode steps (after a.depth prompt tokens), then exactly K timed steps
     def fill():
