@@ -513,8 +513,45 @@ struct rope_job {
 
 struct rope_jobs { rope_job j[2]; int njobs; };
 
+// cos/sin of every rope pair at the positions of ntok tokens ([token][pair]), once per graph:
+// rope_cs, the arithmetic of the ROPE kernel, so fused (k_gemv.hip epilogue) and table-driven
+// ROPE kernels produce the same bits; every layer's ROPE nodes read it (the sinf / cosf of the
+// CPU's libm are ~100 instructions each)
+__global__ __launch_bounds__(256) void k_rope_table(const rope_params rp, const int32_t * __restrict__ pos,
+                                                    const float * __restrict__ ff, int64_t ntok, float2 * __restrict__ tab) {
+    const int np = rp.n_dims / 2;
+    for (int64_t e = (int64_t) blockIdx.x * 256 + threadIdx.x; e < ntok * np; e += (int64_t) gridDim.x * 256) {
+        const int64_t t = e / np;
+        const int ip = (int) (e % np);
+        float c, sn;
+        rope_cs(rp, (float) pos[t], ip, ff, c, sn);
+        tab[e] = make_float2(c, sn);
+    }
+}
+
+// the table for a ROPE node's parameters and position tensor, launched on first use in the
+// graph (run_nodes clears the key: positions change every graph, a capture replays the
+// launch); slot 3 of the scratch arena holds it
+const float2 * rope_table(exec_ctx & ctx, const ggml_tensor * r, const rope_params & rp, const int32_t * pos,
+                          const float * ff, int64_t ntok) {
+    if (ctx.rt_table && ctx.rt_pos == pos && ctx.rt_ff == ff && ctx.rt_ntok == ntok &&
+        memcmp(ctx.rt_params, r->op_params, sizeof(ctx.rt_params)) == 0) {
+        return ctx.rt_table;
+    }
+    const int64_t n = ntok * (rp.n_dims / 2);
+    float2 * tab = (float2 *) ctx.scratch(3, sizeof(float2) * std::max<int64_t>(n, 256));
+    hipLaunchKernelGGL(k_rope_table, dim3((unsigned) std::min<int64_t>(ceil_div(n, 256), 1024)), dim3(256), 0, ctx.stream,
+                       rp, pos, ff, ntok, tab);
+    ctx.rt_table = tab;
+    ctx.rt_ntok = ntok;
+    ctx.rt_pos = pos;
+    ctx.rt_ff = ff;
+    memcpy(ctx.rt_params, r->op_params, sizeof(ctx.rt_params));
+    return tab;
+}
+
 __global__ __launch_bounds__(256) void k_rope(const rope_jobs J, const int32_t * __restrict__ pos,
-                                              const float * __restrict__ ff, rope_params rp) {
+                                              const float * __restrict__ ff, rope_params rp, const float2 * __restrict__ tab) {
     int64_t r = blockIdx.x;  // row over (i1 head, i2 token, i3) of job 0, then job 1
     const int jb = (J.njobs > 1 && r >= J.j[0].nrows) ? 1 : 0;
     if (jb) r -= J.j[0].nrows;
@@ -534,7 +571,12 @@ __global__ __launch_bounds__(256) void k_rope(const rope_jobs J, const int32_t *
         float o0, o1;
         if (i0 < rp.n_dims) {
             float c, s;
-            rope_cs(rp, p, ip, ff, c, s);
+            if (tab) {
+                const float2 cs = tab[i2 * (rp.n_dims / 2) + ip];
+                c = cs.x; s = cs.y;
+            } else {
+                rope_cs(rp, p, ip, ff, c, s);
+            }
             if (neox) { a0 = ip; a1 = ip + rp.n_dims / 2; }
             else      { a0 = i0; a1 = i0 + 1; }
             const float x0 = *(const float *) (xr + a0 * tx.nb[0]);
@@ -597,8 +639,13 @@ void op_rope_multi(exec_ctx & ctx, ggml_tensor * const * nodes, int n, void * co
     const ggml_tensor * pos = nodes[0]->src[1];
     const ggml_tensor * ff  = nodes[0]->src[2];
     const unsigned thr = nodes[0]->src[0]->ne[0] / 2 >= 256 ? 256 : 64;
+    // positions indexed by i2 only (the llama layout: [dims, heads, tokens]); a table of
+    // pos->ne[0] tokens shared by every ROPE node of the graph
+    const bool tabbed = pos->ne[0] == nodes[0]->src[0]->ne[2] && nodes[0]->src[0]->ne[3] == 1;
+    const float2 * tab = tabbed ? rope_table(ctx, nodes[0], rp, (const int32_t *) pos->data, ff ? (const float *) ff->data : nullptr,
+                                             pos->ne[0]) : nullptr;
     hipLaunchKernelGGL(k_rope, dim3((unsigned) rows), dim3(thr), 0, ctx.stream, J, (const int32_t *) pos->data,
-                       ff ? (const float *) ff->data : nullptr, rp);
+                       ff ? (const float *) ff->data : nullptr, rp, tab);
 }
 
 void op_rope(exec_ctx & ctx, ggml_tensor * dst) {

@@ -372,33 +372,6 @@ __global__ __launch_bounds__(256) void k_gemv_pipe2(const gemv_args p1, const in
     else gemv_pipe_body<T2, R2, WPR, 1>(p2, ng2, (int64_t) blockIdx.x - nwg1, (int64_t) gridDim.x - nwg1, xr);
 }
 
-// cos/sin of every rope pair at the token's position (one token), once per graph: rope_cs,
-// the arithmetic of the stand-alone ROPE kernel, so the fused epilogue's bits do not change.
-__global__ __launch_bounds__(256) void k_rope_table(const rope_params rp, const int32_t * __restrict__ pos,
-                                                    const float * __restrict__ ff, float2 * __restrict__ tab) {
-    for (int ip = threadIdx.x; ip < rp.n_dims / 2; ip += blockDim.x) {
-        float c, sn;
-        rope_cs(rp, (float) pos[0], ip, ff, c, sn);
-        tab[ip] = make_float2(c, sn);
-    }
-}
-
-// the table for a ROPE node's parameters and position tensor, launched on first use in the
-// graph (run_nodes clears the key: positions change every graph, the capture replays the
-// launch); slot 3 of the scratch arena holds it
-static const float2 * rope_table(exec_ctx & ctx, const ggml_tensor * r, const rope_params & rp, const int32_t * pos,
-                                 const float * ff) {
-    if (ctx.rt_table && ctx.rt_pos == pos && ctx.rt_ff == ff && memcmp(ctx.rt_params, r->op_params, sizeof(ctx.rt_params)) == 0) {
-        return ctx.rt_table;
-    }
-    float2 * tab = (float2 *) ctx.scratch(3, sizeof(float2) * GEMV_ROPE_MAXPAIRS);
-    hipLaunchKernelGGL(k_rope_table, dim3(1), dim3(256), 0, ctx.stream, rp, pos, ff, tab);
-    ctx.rt_table = tab;
-    ctx.rt_pos = pos;
-    ctx.rt_ff = ff;
-    memcpy(ctx.rt_params, r->op_params, sizeof(ctx.rt_params));
-    return tab;
-}
 
 // ---- host ----------------------------------------------------------------------------------------
 // kernel-timing mode: the GEMV kernel itself is launched with start/stop events
@@ -631,7 +604,7 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
     if (a.need_pairs) {
         GGML_ASSERT(a.rp.n_dims <= 2 * GEMV_ROPE_MAXPAIRS);
         for (int i = 0; i < nmat; ++i) {
-            if (epi->rope[i]) { a.rtab_g = rope_table(ctx, epi->rope[i], a.rp, a.rope_pos, a.rope_ff); break; }
+            if (epi->rope[i]) { a.rtab_g = rope_table(ctx, epi->rope[i], a.rp, a.rope_pos, a.rope_ff, 1); break; }
         }
     }
     a.A = {act.qs, act.d, act.s};

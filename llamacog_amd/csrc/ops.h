@@ -79,9 +79,10 @@ struct exec_ctx {
     q8_act              qc_act;
     void qcache_clear() { qc_tensor = nullptr; qc_data = nullptr; }
 
-    // per-graph RoPE cos/sin table (k_gemv.hip rope_table): every layer's fused Q/K rope
+    // per-graph RoPE cos/sin table (k_elem.hip rope_table): every layer's fused Q/K rope
     // epilogue reads the same table of the token's position, built once per graph
     const float2 *  rt_table = nullptr;
+    int64_t         rt_ntok = 0;
     const void *    rt_pos = nullptr;
     const void *    rt_ff = nullptr;
     int32_t         rt_params[15] = {};

@@ -47,4 +47,10 @@ __device__ __forceinline__ void rope_rotate(float x0, float x1, float c, float s
     o1 = fmaf(x0, s, __fmul_rn(x1, c));
 }
 
+struct exec_ctx;
+// the graph's cos/sin table [ntok][n_dims/2] of a ROPE node's positions (k_elem.hip), built on
+// first use and shared by the graph's ROPE kernels and fused GEMV rope epilogues
+const float2 * rope_table(exec_ctx & ctx, const ggml_tensor * r, const rope_params & rp, const int32_t * pos,
+                          const float * ff, int64_t ntok);
+
 }  // namespace mi355x
