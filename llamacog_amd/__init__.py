@@ -14,7 +14,8 @@ import os
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "llamacog_amd")
-PLUGIN = os.path.join(PKG, "libggml-mi355x.so")
+# MI355X_PLUGIN: an A/B build of the plugin (scripts/gpu_iter.sh variants); default the in-tree one
+PLUGIN = os.environ.get("MI355X_PLUGIN") or os.path.join(PKG, "libggml-mi355x.so")
 LLB = os.path.join(PKG, "libllb.so")
 REFHOST = os.path.join(REPO, "refhost", "build")
 

@@ -810,9 +810,22 @@ static bool mi_dev_supports_buft(ggml_backend_dev_t dev, ggml_backend_buffer_typ
 
 // mirror of the CUDA heuristic (ggml-cuda.cu:3326-3347): offload big-batch ops whose
 // weights live in host memory
+// the batch an op carries, as the scheduler's offload test measures it (the CUDA backend's
+// per-op rule, ggml-cuda.cu:3326-3338): the token count of a mat-mul, the token dimension ne[2]
+// of MUL_MAT_ID (ne[1] is the expert slots) and ROPE (ne[1] is the heads), the rows otherwise;
+// GET_ROWS (the embedding) is never offloaded
+static int64_t mi_op_batch(const ggml_tensor * op) {
+    switch (op->op) {
+        case GGML_OP_GET_ROWS: return 0;
+        case GGML_OP_MUL_MAT: return op->ne[1];
+        case GGML_OP_MUL_MAT_ID: case GGML_OP_ROPE: case GGML_OP_ROPE_BACK: return op->ne[2];
+        default: return ggml_nrows(op);
+    }
+}
+
 static bool mi_dev_offload_op(ggml_backend_dev_t, const ggml_tensor * op) {
     const int min_batch = 32;
-    return op->ne[1] >= min_batch && op->op != GGML_OP_GET_ROWS;
+    return mi_op_batch(op) >= min_batch;
 }
 
 static ggml_backend_event_t mi_dev_event_new(ggml_backend_dev_t dev) {

@@ -67,9 +67,31 @@ __device__ __forceinline__ void k4_scales_g(uint32_t s0, uint32_t s1, uint32_t s
 
 // weight loads: streamed once per token
 typedef unsigned int gv4u __attribute__((ext_vector_type(4)));
+// Weight loads.  Decode reads every weight byte once per token, so the loads can be
+// non-temporal (MI355X_MICROARCH.md nt-weights row: -5..10 % per decode layer); MI_WNT=0 builds
+// the default-policy loads for A/B.
+#ifndef MI_WNT
+#define MI_WNT 1
+#endif
+#if MI_WNT
+typedef gv4u gv4u_u __attribute__((aligned(1)));
+typedef unsigned int gv2u __attribute__((ext_vector_type(2)));
+typedef gv2u gv2u_u __attribute__((aligned(1)));
+typedef uint16_t u16_u __attribute__((aligned(1)));
+__device__ __forceinline__ uint4 wld16(const uint8_t * p) {
+    const gv4u v = __builtin_nontemporal_load((const gv4u_u *) p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 wld8(const uint8_t * p) {
+    const gv2u v = __builtin_nontemporal_load((const gv2u_u *) p);
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint32_t wld2(const uint8_t * p) { return __builtin_nontemporal_load((const u16_u *) p); }
+#else
 __device__ __forceinline__ uint4 wld16(const uint8_t * p) { return ld16(p); }
 __device__ __forceinline__ uint2 wld8(const uint8_t * p) { return ld8(p); }
 __device__ __forceinline__ uint32_t wld2(const uint8_t * p) { return ld2(p); }
+#endif
 
 // the Q8_K / Q8_0 activation (quant_act.h layout): qs, d, and the 16-sums (Q8_K) / 32-sums (Q8_0)
 struct gemv_act { const int8_t * qs; const float * d; const int16_t * s; };
