@@ -52,6 +52,10 @@ void ggml_backend_mi355x_graph_stats(long * captures, long * replays);
 // over RCCL (ncclSend/ncclRecv, the default) / as hipMemcpyPeerAsync (GGML_MI355X_P2P=peer or
 // RCCL unavailable).  Replaces the peer-copy path of ggml-cuda.cu:2437-2490.
 void ggml_backend_mi355x_p2p_stats(long * rccl, long * peer);
+// the same plus the hand-offs between two ggml devices on ONE GPU (two backends, or the virtual
+// devices of GGML_MI355X_VDEV) that went as an async device-to-device copy (d2d); with
+// GGML_MI355X_P2P=rccl those go as an RCCL self send/recv and count under rccl
+void ggml_backend_mi355x_handoff_stats(long * rccl, long * peer, long * d2d);
 // destroys the RCCL communicators (re-created on the next cross-device copy)
 void ggml_backend_mi355x_p2p_release(void);
 // measured HBM read ceiling of a device in GB/s (STREAM-style non-temporal read of 440 MB

@@ -64,6 +64,13 @@ def p2p_stats() -> tuple[int, int]:
     return r.value, p.value
 
 
+def handoff_stats() -> tuple[int, int, int]:
+    """(stage hand-offs over RCCL, as hipMemcpyPeerAsync, as a same-GPU async copy) since load."""
+    r, p, d = ctypes.c_long(), ctypes.c_long(), ctypes.c_long()
+    plugin_lib().ggml_backend_mi355x_handoff_stats(ctypes.byref(r), ctypes.byref(p), ctypes.byref(d))
+    return r.value, p.value, d.value
+
+
 def hbm_read_gbs(device: int = 0) -> float:
     """Measured HBM read ceiling of a device, GB/s (k_stream.hip)."""
     lib = plugin_lib()
@@ -118,6 +125,8 @@ def llb(echo_log: bool = False, with_plugin: bool = True) -> ctypes.CDLL:
     lib.llb_greedy.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.c_int,
                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float)]
     lib.llb_log.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.llb_greedy_threads.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
+                                       ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float)]
     plugin = _require(PLUGIN, "MI355X backend plugin").encode() if with_plugin else None
     n = lib.llb_load_backends(REFHOST.encode(), plugin, 1 if echo_log else 0)
     # n < 0: the plugin did not register (ggml_backend_score() == 0, i.e. no gfx950 GPU
@@ -218,6 +227,20 @@ class Model:
         if self.lib.llb_decode(self.h, p, len(tokens)) != 0:
             raise RuntimeError("llama_decode failed")
         return np.ctypeslib.as_array(self.lib.llb_logits(self.h), shape=(self.n_vocab,)).copy()
+
+    def greedy_threads(self, n_contexts: int, prompt: list[int], n_gen: int):
+        """n_contexts extra contexts of this model greedy-decode `prompt` concurrently, one thread
+        each (tests/test-thread-safety.cpp's pattern); returns ids [c][n_gen], logits [c][n_gen][V]"""
+        import numpy as np
+        p = (ctypes.c_int32 * len(prompt))(*prompt)
+        ids = np.zeros((n_contexts, n_gen), dtype=np.int32)
+        logits = np.zeros((n_contexts, n_gen, self.n_vocab), dtype=np.float32)
+        r = self.lib.llb_greedy_threads(self.h, n_contexts, p, len(prompt), n_gen,
+                                        ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                        logits.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        if r != 0:
+            raise RuntimeError(f"threaded greedy decode failed ({r})")
+        return ids, logits
 
     def greedy(self, prompt: list[int], n_gen: int, want_logits: bool = True):
         import numpy as np

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <mutex>
 #include <string>
@@ -50,6 +51,7 @@ void * exec_ctx::scratch(int slot, size_t bytes) {
     nsz = (nsz + (1 << 20) - 1) & ~size_t((1 << 20) - 1);
     if (slot_ptr[slot]) {
         MI_CHECK(hipStreamSynchronize(stream));
+        wait_no_capture();   // another context's capture may be open (thread safety)
         MI_CHECK(hipFree(slot_ptr[slot]));
     }
     MI_CHECK(hipMalloc(&slot_ptr[slot], nsz));
@@ -80,16 +82,18 @@ bool exec_ctx::prepare_dyn(ggml_cgraph * g) {
     if (!dyn_dev) {
         MI_CHECK(hipMalloc((void **) &dyn_dev, DYN_CAP * sizeof(void *)));
         dyn_cap = DYN_CAP;
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < DYN_RING; ++k) {
             MI_CHECK(hipHostMalloc((void **) &dyn_pin[k], DYN_CAP * sizeof(void *), hipHostMallocDefault));
             MI_CHECK(hipEventCreateWithFlags(&dyn_ev[k], hipEventDisableTiming));
             MI_CHECK(hipEventRecord(dyn_ev[k], stream));
         }
     }
     // stage through pinned memory: the copy runs asynchronously on the stream, so the buffer it
-    // reads is only refilled once the copy that last used it has completed
+    // reads is only refilled once the copy that last used it has completed.  A ring of DYN_RING
+    // buffers: the host blocks only when it runs DYN_RING graphs ahead of the device (the
+    // scheduler's pipeline keeps up to n_copies = 4 graphs in flight per backend)
     const int k = dyn_flip;
-    dyn_flip ^= 1;
+    dyn_flip = (dyn_flip + 1) % DYN_RING;
     MI_CHECK(hipEventSynchronize(dyn_ev[k]));
     memcpy(dyn_pin[k], dyn_host.data(), dyn_host.size() * sizeof(void *));
     MI_CHECK(hipMemcpyAsync(dyn_dev, dyn_pin[k], dyn_host.size() * sizeof(void *), hipMemcpyHostToDevice, stream));
@@ -106,7 +110,7 @@ void exec_ctx::free_scratch() {
     if (dyn_dev) (void) hipFree(dyn_dev);
     dyn_dev = nullptr;
     dyn_cap = 0;
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < DYN_RING; ++k) {
         if (dyn_pin[k]) (void) hipHostFree(dyn_pin[k]);
         if (dyn_ev[k]) (void) hipEventDestroy(dyn_ev[k]);
         dyn_pin[k] = nullptr;
@@ -349,7 +353,13 @@ static size_t mi_host_buft_get_alignment(ggml_backend_buffer_type_t) {
 
 static bool mi_host_buft_is_host(ggml_backend_buffer_type_t) { return true; }
 
+static size_t mi_reg_get_device_count(ggml_backend_reg_t reg);
+static ggml_backend_dev_t mi_reg_get_device(ggml_backend_reg_t reg, size_t index);
+
 static ggml_backend_buffer_type_t mi_host_buft() {
+    // .device = the registry's first device, as CUDA_Host (ggml-cuda.cu:1145): with mmap on,
+    // libllama then keeps CPU-resident weights in the mmap'd CPU buffer instead of copying them
+    // into page-locked memory (src/llama-model.cpp:1742-1750)
     static ggml_backend_buffer_type buft = {
         /* .iface   = */ {
             /* .get_name       = */ mi_host_buft_get_name,
@@ -359,7 +369,7 @@ static ggml_backend_buffer_type_t mi_host_buft() {
             /* .get_alloc_size = */ nullptr,
             /* .is_host        = */ mi_host_buft_is_host,
         },
-        /* .device  = */ nullptr,   // host memory belongs to no device (as CUDA_Host)
+        /* .device  = */ mi_reg_get_device_count(mi_reg()) > 0 ? mi_reg_get_device(mi_reg(), 0) : nullptr,
         /* .context = */ nullptr,
     };
     return &buft;
@@ -412,38 +422,122 @@ struct mi_backend_ctx {
 // collective library's xGMI transport, stream-ordered on both sides, no host sync.
 // GGML_MI355X_P2P=peer selects hipMemcpyPeerAsync + event instead (A/B and fallback).
 // ------------------------------------------------------------------------------------------
+// The clique covers the HIP devices that own a backend when the first hand-off happens (rank =
+// position in `devs`), not every visible GPU.  Any RCCL error disables RCCL for the process and
+// the hand-off falls back to hipMemcpyPeerAsync: a failed collective never aborts the decode.
+// GGML_MI355X_P2P: unset = RCCL between distinct GPUs; "peer" = hipMemcpyPeerAsync only;
+// "rccl" = RCCL also between two ggml devices on ONE GPU (virtual devices, GGML_MI355X_VDEV):
+// a one-rank communicator and a self send/recv, so the RCCL path runs on a single-GPU box.
 struct mi_p2p {
     std::mutex mtx;
     int state = 0;                      // 0 = not tried, 1 = ready, -1 = unavailable
-    std::vector<ncclComm_t> comms;      // indexed by HIP device id
+    std::vector<int> devs;              // HIP device id of each rank
+    std::vector<ncclComm_t> comms;      // by rank
+    std::vector<int> self_dev;          // one-rank communicators of the forced same-GPU mode
+    std::vector<ncclComm_t> self_comm;
 };
 static mi_p2p g_p2p;
-static std::atomic<long> g_p2p_rccl{0}, g_p2p_peer{0};
+static std::atomic<long> g_p2p_rccl{0}, g_p2p_peer{0}, g_p2p_d2d{0};
+// HIP devices that own at least one backend (mi_dev_init_backend)
+static std::mutex g_bdev_mtx;
+static std::vector<int> g_bdevs;
 
-static bool p2p_use_rccl() {
-    static const bool peer = getenv("GGML_MI355X_P2P") && strcmp(getenv("GGML_MI355X_P2P"), "peer") == 0;
-    return !peer;
+enum p2p_mode { P2P_RCCL, P2P_PEER, P2P_RCCL_ALL };
+static p2p_mode p2p_mode_env() {
+    const char * v = getenv("GGML_MI355X_P2P");
+    if (v && strcmp(v, "peer") == 0) return P2P_PEER;
+    if (v && strcmp(v, "rccl") == 0) return P2P_RCCL_ALL;
+    return P2P_RCCL;
 }
 
-static bool p2p_comms_ready() {
+static void p2p_disable(const char * what, ncclResult_t r) {
+    MI_LOG_WARN("mi355x: RCCL %s failed (%s); stage hand-offs use hipMemcpyPeerAsync from now on\n", what,
+                ncclGetErrorString(r));
+    g_p2p.state = -1;
+}
+
+// rank of HIP device `dev` in the clique (built on first use), or -1
+static int p2p_rank(int dev) {
     std::lock_guard<std::mutex> lk(g_p2p.mtx);
     if (g_p2p.state == 0) {
-        int n = 0;
-        MI_CHECK(hipGetDeviceCount(&n));
-        std::vector<int> devs(n);
-        for (int i = 0; i < n; ++i) devs[i] = i;
+        {
+            std::lock_guard<std::mutex> lb(g_bdev_mtx);
+            g_p2p.devs = g_bdevs;
+        }
+        std::sort(g_p2p.devs.begin(), g_p2p.devs.end());
+        const int n = (int) g_p2p.devs.size();
         g_p2p.comms.assign(n, nullptr);
-        const ncclResult_t r = n > 1 ? ncclCommInitAll(g_p2p.comms.data(), n, devs.data()) : ncclInvalidUsage;
+        const ncclResult_t r = n > 1 ? ncclCommInitAll(g_p2p.comms.data(), n, g_p2p.devs.data()) : ncclInvalidUsage;
         if (r == ncclSuccess) {
             g_p2p.state = 1;
         } else {
-            MI_LOG_WARN("mi355x: RCCL communicator init failed (%s); stage hand-off uses hipMemcpyPeerAsync\n",
-                        n > 1 ? ncclGetErrorString(r) : "one device");
+            MI_LOG_WARN("mi355x: RCCL communicator init over %d devices failed (%s); stage hand-off uses hipMemcpyPeerAsync\n",
+                        n, n > 1 ? ncclGetErrorString(r) : "one device");
             g_p2p.comms.clear();
             g_p2p.state = -1;
         }
     }
-    return g_p2p.state == 1;
+    if (g_p2p.state != 1) return -1;
+    for (size_t k = 0; k < g_p2p.devs.size(); ++k) {
+        if (g_p2p.devs[k] == dev) return (int) k;
+    }
+    return -1;
+}
+
+// one ncclSend (source stream) + ncclRecv (destination stream) in a group; false = not sent
+static bool p2p_send_recv(const void * src, int sdev, hipStream_t ss, void * dst, int ddev, hipStream_t ds, size_t n) {
+    const int rs = p2p_rank(sdev), rd = p2p_rank(ddev);
+    if (rs < 0 || rd < 0) return false;
+    std::lock_guard<std::mutex> lk(g_p2p.mtx);
+    if (g_p2p.state != 1) return false;
+    MI_CHECK(hipSetDevice(sdev));
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) {
+        ncclResult_t a = ncclSend(src, n, ncclUint8, rd, g_p2p.comms[rs], ss);
+        ncclResult_t b = a == ncclSuccess ? ncclRecv(dst, n, ncclUint8, rs, g_p2p.comms[rd], ds) : a;
+        r = ncclGroupEnd();
+        if (r == ncclSuccess) r = b;
+    }
+    if (r != ncclSuccess) {
+        p2p_disable("send/recv", r);
+        return false;
+    }
+    g_p2p_rccl.fetch_add(1);
+    return true;
+}
+
+// forced RCCL between two ggml devices on one GPU: self send/recv of a one-rank communicator,
+// both on the source stream (the caller makes the destination stream wait)
+static bool p2p_self(const void * src, void * dst, int dev, hipStream_t ss, size_t n) {
+    std::lock_guard<std::mutex> lk(g_p2p.mtx);
+    if (g_p2p.state < 0) return false;
+    ncclComm_t comm = nullptr;
+    for (size_t k = 0; k < g_p2p.self_dev.size(); ++k) {
+        if (g_p2p.self_dev[k] == dev) comm = g_p2p.self_comm[k];
+    }
+    if (!comm) {
+        const ncclResult_t r = ncclCommInitAll(&comm, 1, &dev);
+        if (r != ncclSuccess) {
+            p2p_disable("one-rank communicator init", r);
+            return false;
+        }
+        g_p2p.self_dev.push_back(dev);
+        g_p2p.self_comm.push_back(comm);
+    }
+    MI_CHECK(hipSetDevice(dev));
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) {
+        ncclResult_t a = ncclSend(src, n, ncclUint8, 0, comm, ss);
+        ncclResult_t b = a == ncclSuccess ? ncclRecv(dst, n, ncclUint8, 0, comm, ss) : a;
+        r = ncclGroupEnd();
+        if (r == ncclSuccess) r = b;
+    }
+    if (r != ncclSuccess) {
+        p2p_disable("self send/recv", r);
+        return false;
+    }
+    g_p2p_rccl.fetch_add(1);
+    return true;
 }
 
 static void p2p_destroy() {
@@ -451,7 +545,13 @@ static void p2p_destroy() {
     for (ncclComm_t c : g_p2p.comms) {
         if (c) (void) ncclCommDestroy(c);
     }
+    for (ncclComm_t c : g_p2p.self_comm) {
+        if (c) (void) ncclCommDestroy(c);
+    }
     g_p2p.comms.clear();
+    g_p2p.devs.clear();
+    g_p2p.self_comm.clear();
+    g_p2p.self_dev.clear();
     g_p2p.state = 0;
 }
 
@@ -460,6 +560,26 @@ static int env_flag(const char * name) {
     return v && atoi(v) != 0 ? 1 : 0;
 }
 static std::atomic<long> g_graph_captures{0}, g_graph_replays{0};
+// Captures in flight in any thread (the role of ggml-cuda.cu:516-541's lock): freeing a stream,
+// an event or device memory while another thread's stream is being captured is not safe on the
+// HIP runtime, so backend teardown and scratch reallocation wait until no capture is open.
+static std::mutex g_capture_mtx;
+static std::condition_variable g_capture_cv;
+static int g_captures_open = 0;
+namespace mi355x {
+void wait_no_capture() {
+    std::unique_lock<std::mutex> lk(g_capture_mtx);
+    g_capture_cv.wait(lk, [] { return g_captures_open == 0; });
+}
+}
+static void capture_open() {
+    std::lock_guard<std::mutex> lk(g_capture_mtx);
+    ++g_captures_open;
+}
+static void capture_close() {
+    std::lock_guard<std::mutex> lk(g_capture_mtx);
+    if (--g_captures_open == 0) g_capture_cv.notify_all();
+}
 static std::atomic<int> g_no_fuse{env_flag("GGML_MI355X_NO_FUSE")};
 // rocprofv3 --kernel-trace (ROCm 7.2) segfaults the profiled process when it traces the
 // kernels of a replayed hipGraph; under kernel tracing the same kernels are launched
@@ -518,6 +638,7 @@ static const char * mi_backend_get_name(ggml_backend_t backend) {
 
 static void mi_backend_free(ggml_backend_t backend) {
     auto * ctx = (mi_backend_ctx *) backend->context;
+    wait_no_capture();
     MI_CHECK(hipSetDevice(ctx->device));
     MI_CHECK(hipStreamSynchronize(ctx->ex.stream));
     ctx->ex.collect_timing();
@@ -550,8 +671,9 @@ static bool mi_backend_is_ours(ggml_backend_t backend);
 // called on the destination backend; ggml-cuda.cu:2437-2490 is the CUDA counterpart).
 //   * different MI355X devices: ncclSend on the source stream + ncclRecv on the destination
 //     stream in one group (RCCL over xGMI, see mi_p2p above), or hipMemcpyPeerAsync + event;
-//   * same device (two backend instances): async D2D on the source stream, the destination
-//     stream waits on a pooled event recorded after it.
+//   * same GPU (two backend instances, or two virtual devices): async D2D on the source stream
+//     (or RCCL self send/recv under GGML_MI355X_P2P=rccl), the destination stream waits on a
+//     pooled event recorded after it.
 static bool mi_backend_cpy_tensor_async(ggml_backend_t backend_src, ggml_backend_t backend_dst, const ggml_tensor * src, ggml_tensor * dst) {
     if (!mi_backend_is_ours(backend_src) || !mi_backend_is_ours(backend_dst)) return false;
     if (!src->buffer || !dst->buffer || !mi_buf_is_ours(src->buffer) || !mi_buf_is_ours(dst->buffer)) return false;
@@ -559,19 +681,17 @@ static bool mi_backend_cpy_tensor_async(ggml_backend_t backend_src, ggml_backend
     auto * sctx = (mi_backend_ctx *) backend_src->context;
     auto * dctx = (mi_backend_ctx *) backend_dst->context;
     const size_t n = ggml_nbytes(dst);
-    if (sctx->device != dctx->device && p2p_use_rccl() && p2p_comms_ready()) {
-        MI_CHECK(hipSetDevice(sctx->device));
-        bool ok = ncclGroupStart() == ncclSuccess;
-        ok = ok && ncclSend(src->data, n, ncclUint8, dctx->device, g_p2p.comms[sctx->device], sctx->ex.stream) == ncclSuccess;
-        ok = ok && ncclRecv(dst->data, n, ncclUint8, sctx->device, g_p2p.comms[dctx->device], dctx->ex.stream) == ncclSuccess;
-        const ncclResult_t ge = ncclGroupEnd();
-        GGML_ASSERT(ok && ge == ncclSuccess && "mi355x: RCCL send/recv of a stage hand-off failed");
-        g_p2p_rccl.fetch_add(1);
+    static const p2p_mode mode = p2p_mode_env();
+    if (sctx->device != dctx->device && mode != P2P_PEER &&
+        p2p_send_recv(src->data, sctx->device, sctx->ex.stream, dst->data, dctx->device, dctx->ex.stream, n)) {
         return true;
     }
     MI_CHECK(hipSetDevice(sctx->device));
     if (sctx->device == dctx->device) {
-        MI_CHECK(hipMemcpyAsync(dst->data, src->data, n, hipMemcpyDeviceToDevice, sctx->ex.stream));
+        if (!(mode == P2P_RCCL_ALL && backend_src != backend_dst && p2p_self(src->data, dst->data, sctx->device, sctx->ex.stream, n))) {
+            MI_CHECK(hipMemcpyAsync(dst->data, src->data, n, hipMemcpyDeviceToDevice, sctx->ex.stream));
+            g_p2p_d2d.fetch_add(1);
+        }
     } else {
         MI_CHECK(hipMemcpyPeerAsync(dst->data, dctx->device, src->data, sctx->device, n, sctx->ex.stream));
         g_p2p_peer.fetch_add(1);
@@ -654,9 +774,11 @@ static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
 
     hipGraph_t g = nullptr;
     ctx->ex.capturing = true;
+    capture_open();
     MI_CHECK(hipStreamBeginCapture(ctx->ex.stream, hipStreamCaptureModeRelaxed));
     run_nodes(ctx->ex, cgraph);
     const hipError_t cerr = hipStreamEndCapture(ctx->ex.stream, &g);
+    capture_close();
     ctx->ex.capturing = false;
     if (cerr != hipSuccess || g == nullptr ||
         hipGraphInstantiate(&e->exec, g, nullptr, nullptr, 0) != hipSuccess) {
@@ -782,6 +904,10 @@ static ggml_backend_t mi_dev_init_backend(ggml_backend_dev_t dev, const char * p
     ctx->name = dctx->name;
     ctx->ex.device = dctx->device;
     MI_CHECK(hipStreamCreateWithFlags(&ctx->ex.stream, hipStreamNonBlocking));
+    {
+        std::lock_guard<std::mutex> lk(g_bdev_mtx);
+        if (std::find(g_bdevs.begin(), g_bdevs.end(), dctx->device) == g_bdevs.end()) g_bdevs.push_back(dctx->device);
+    }
     return new ggml_backend{
         /* .guid    = */ mi_guid(),
         /* .iface   = */ mi_backend_iface,
@@ -912,20 +1038,28 @@ static ggml_backend_reg_t mi_reg() {
             (void) hipGetLastError();
             n = 0;
         }
-        ctx->dev_ctx.reserve(n);
-        ctx->devices.reserve(n);
-        for (int i = 0; i < n; ++i) {
+        // GGML_MI355X_VDEV=k (k > 1): k ggml devices over HIP device 0 — libllama's multi-device
+        // paths (layer split with the scheduler's pipeline copies and cpy_tensor_async hand-offs,
+        // row split) then run on a one-GPU box; each virtual device has its own buffers and streams
+        const int vdev = getenv("GGML_MI355X_VDEV") ? atoi(getenv("GGML_MI355X_VDEV")) : 0;
+        const int nd = (vdev > 1 && n >= 1) ? vdev : n;
+        ctx->dev_ctx.reserve(nd);
+        ctx->devices.reserve(nd);
+        for (int i = 0; i < nd; ++i) {
+            const int hip = nd != n ? 0 : i;
             hipDeviceProp_t prop;
-            MI_CHECK(hipGetDeviceProperties(&prop, i));
+            MI_CHECK(hipGetDeviceProperties(&prop, hip));
             auto * d = new mi_device_ctx;
-            d->device = i;
+            d->device = hip;
             d->name = std::string(MI355X_NAME) + std::to_string(i);
             d->arch = prop.gcnArchName;
-            d->description = std::string(prop.name) + " (" + d->arch + ", " + std::to_string(prop.multiProcessorCount) + " CUs)";
+            d->description = std::string(prop.name) + " (" + d->arch + ", " + std::to_string(prop.multiProcessorCount) + " CUs" +
+                             (nd != n ? ", virtual device " + std::to_string(i) + " of HIP device 0)" : ")");
             d->total_mem = prop.totalGlobalMem;
             d->buft = {mi_buft_iface, nullptr, d};
             ctx->dev_ctx.push_back(d);
         }
+        n = nd;
         for (int i = 0; i < n; ++i) {
             ctx->devices.push_back({mi_device_iface, &reg, ctx->dev_ctx[i]});
             ctx->dev_ctx[i]->buft.device = &ctx->devices[i];
@@ -976,6 +1110,12 @@ GGML_BACKEND_API void ggml_backend_mi355x_set_graph_timing(int enable) { g_graph
 GGML_BACKEND_API void ggml_backend_mi355x_p2p_stats(long * rccl, long * peer) {
     if (rccl) *rccl = g_p2p_rccl.load();
     if (peer) *peer = g_p2p_peer.load();
+}
+
+GGML_BACKEND_API void ggml_backend_mi355x_handoff_stats(long * rccl, long * peer, long * d2d) {
+    if (rccl) *rccl = g_p2p_rccl.load();
+    if (peer) *peer = g_p2p_peer.load();
+    if (d2d) *d2d = g_p2p_d2d.load();
 }
 
 GGML_BACKEND_API void ggml_backend_mi355x_p2p_release(void) { p2p_destroy(); }

@@ -53,7 +53,10 @@ static bool cpy_supported(const ggml_tensor * src, const ggml_tensor * dst) {
     if (s == GGML_TYPE_I32 && d == GGML_TYPE_I32) return true;
     if (s == GGML_TYPE_F32 && (d == GGML_TYPE_Q8_0 || d == GGML_TYPE_Q4_0)) {
         // the KV-cache store: src Kcur [D, H, T] into a contiguous [H*D, T] view of the cache
-        if (ggml_is_contiguous(src) && ggml_is_contiguous(dst)) return ggml_nelements(src) % 32 == 0;
+        // (flat rows: op_cpy quantizes the element stream in 32-blocks).  With equal row lengths
+        // op_cpy goes row by row, so each row must hold whole blocks (the CPU's dup-to-quant
+        // asserts the same)
+        if (ggml_is_contiguous(src) && ggml_is_contiguous(dst) && src->ne[0] != dst->ne[0]) return ggml_nelements(src) % 32 == 0;
         return src->ne[0] == dst->ne[0] && src->ne[0] % 32 == 0 && dst->nb[0] == ggml_type_size(d) &&
                ggml_nrows(src) == ggml_nrows(dst);
     }

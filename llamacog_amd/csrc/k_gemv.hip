@@ -26,6 +26,7 @@
 //     LDS as its activation.  The RMS_NORM launch disappears; nothing waits on a last arriver.
 #include "ops.h"
 #include <hip/hip_ext.h>
+#include <mutex>
 #include "rope.h"
 #include "qtypes.h"
 #include "quant_act.h"
@@ -104,6 +105,12 @@ __device__ __forceinline__ void tail_swiglu(const gemv_args & p, int blk, int la
 // hand-off row); the report that completes a block's count makes this workgroup run that block.
 // Returning atomics on one word serialize at the memory side (~88 per us, MI355X_MICROARCH.md
 // dequeue row) and words of one line share that limit, so each counter owns a 4-KiB line.
+// Ordering: this is the first row of MI355X_MICROARCH.md's measured hand-off table (sc1 stores,
+// every storing wave's vmcnt(0) wait, a workgroup barrier, then one lane's agent-scope atomic add
+// per counter; the last adder — told by the returned value — and only after that return, loads
+// the bytes with sc1 loads after a workgroup barrier).  An acq_rel add would instead put an L2
+// write-back + invalidate (≈1.7–3.5 us per workgroup, the fence rows there) into every launch;
+// the form kept here is the measured-valid one the guide prescribes for write-through payloads.
 constexpr int TAIL_STRIDE = 1024;   // ints between counter words
 __device__ __forceinline__ void gemv_tail(const gemv_args & p, int kg, int64_t wg0, int64_t nwg, int rpg) {
     const auto & t = p.tl;
@@ -381,16 +388,17 @@ static thread_local hipEvent_t t_ev_beg = nullptr, t_ev_end = nullptr;
 
 static int g_gemv_wgs = -1;    // GGML_MI355X_GEMV_WGS: persistent grid size
 static int g_num_cu = 0;
+static std::once_flag g_gemv_once;   // several contexts may launch from several threads
 
 static void gemv_init() {
-    if (g_gemv_wgs < 0) g_gemv_wgs = getenv("GGML_MI355X_GEMV_WGS") ? atoi(getenv("GGML_MI355X_GEMV_WGS")) : 2048;
-    if (!g_num_cu) {
+    std::call_once(g_gemv_once, [] {
+        g_gemv_wgs = getenv("GGML_MI355X_GEMV_WGS") ? atoi(getenv("GGML_MI355X_GEMV_WGS")) : 2048;
         int dev = 0;
         hipDeviceProp_t prop;
         MI_CHECK(hipGetDevice(&dev));
         MI_CHECK(hipGetDeviceProperties(&prop, dev));
         g_num_cu = prop.multiProcessorCount;
-    }
+    });
 }
 
 static int64_t set_groups(gemv_args & a, int nmat, int rpg) {

@@ -104,10 +104,11 @@ struct exec_ctx {
     std::vector<void *>              dyn_host;    // their destination pointers
     void **                          dyn_dev = nullptr;
     size_t                           dyn_cap = 0;
-    // pinned staging of the table upload, double-buffered: buffer k is rewritten only after
-    // the copy that last read it has completed (dyn_ev[k])
-    void **                          dyn_pin[2] = {nullptr, nullptr};
-    hipEvent_t                       dyn_ev[2] = {nullptr, nullptr};
+    // pinned staging of the table upload, a ring: buffer k is rewritten only after the copy
+    // that last read it has completed (dyn_ev[k])
+    static constexpr int             DYN_RING = 8;
+    void **                          dyn_pin[DYN_RING] = {};
+    hipEvent_t                       dyn_ev[DYN_RING] = {};
     int                              dyn_flip = 0;
     bool prepare_dyn(ggml_cgraph * g);            // scan + upload; false = table too small (backend.cpp)
     void * const * dyn_slot(const ggml_tensor * cpy) const {
@@ -147,6 +148,8 @@ enum timed_kind { TK_MMV = 0, TK_MMQ = 1, TK_FATTN = 2, TK_OTHER = 3, TK_GRAPH =
 // bit-for-bit in tests/test_gpu_model.py)
 bool fusion_enabled();
 bool graphs_enabled();
+// blocks while any thread has a hipGraph capture open (backend.cpp)
+void wait_no_capture();
 
 // supports / dispatch
 bool op_supported(const ggml_tensor * op);

@@ -55,6 +55,10 @@ class ModelConfig:
     n_expert: int = 0
     n_expert_used: int = 0
     size_label: str = ""  # llama model type inference uses n_layer; kept for docs
+    # the 70B rule of llama_tensor_get_type (src/llama-quant.cpp: LLM_TYPE_70B, 8 heads share each
+    # attn_v: Q4_K -> Q5_K); a real 70B is recognised by its 80 layers, the 2-layer parity model
+    # of the same shapes sets it explicitly
+    v_q5k_70b: bool = False
 
     @property
     def head_dim(self) -> int:
@@ -68,7 +72,11 @@ CONFIGS = {
     # configs[1], configs[2]: Llama-3-8B Q4_K_M
     "llama3-8b-q4km": ModelConfig("Llama-3-8B-synthetic", 4096, 32, 32, 8, 14336, 128256, "q4_k_m"),
     # configs[3]: Llama-3-70B Q4_K_M
-    "llama3-70b-q4km": ModelConfig("Llama-3-70B-synthetic", 8192, 80, 64, 8, 28672, 128256, "q4_k_m"),
+    "llama3-70b-q4km": ModelConfig("Llama-3-70B-synthetic", 8192, 80, 64, 8, 28672, 128256, "q4_k_m", v_q5k_70b=True),
+    # fast parity model: full Llama-3-70B layer shapes (8192 / 28672, 64 / 8 heads, Q5_K / Q6_K
+    # attn_v), 2 layers: layer 0 the Q4_K / Q5_K mix, layer 1 the use_more_bits Q6_K one
+    "llama3-70b-2l-q4km": ModelConfig("Llama-3-70B-2layer-synthetic", 8192, 2, 64, 8, 28672, 128256, "q4_k_m",
+                                      v_q5k_70b=True),
     # configs[4]: Mixtral-8x7B Q5_K_M
     "mixtral-8x7b-q5km": ModelConfig("Mixtral-8x7B-synthetic", 4096, 32, 32, 8, 14336, 32000, "q5_k_m",
                                      n_ctx_train=32768, rope_base=1000000.0, n_expert=8, n_expert_used=2),
@@ -106,7 +114,7 @@ def tensor_types(cfg: ModelConfig) -> list[tuple[str, list[int], int]]:
     if E % 256 != 0 and base in (Q4_K, Q5_K, Q6_K):
         base, out_t, emb_t = Q8_0, Q8_0, Q8_0
     out = [("token_embd.weight", [E, V], emb_t), ("output_norm.weight", [E], F32), ("output.weight", [E, V], out_t)]
-    is70b = L == 80
+    is70b = L == 80 or cfg.v_q5k_70b
     for i in range(L):
         more = use_more_bits(i, L)
         if ft in ("q4_k_m", "q5_k_m"):

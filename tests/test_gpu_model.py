@@ -86,6 +86,103 @@ def test_greedy_llama3_8b_2layer_prompt512():
     _check(_greedy("llama3-8b-2l-q4km", 512, 8, True))
 
 
+def test_greedy_llama3_70b_2layer_q4km():
+    """Llama-3-70B layer shapes (BASELINE.json configs[3]): n_embd 8192, FFN 28672, 64 / 8 heads,
+    attn_v Q5_K (layer 0, the 70B rule) and Q6_K (layer 1), ffn_down Q4_K and Q6_K at K = 28672
+    (wider than the pipelined GEMV's 256 tasks: the batched mat-vec path), the 28672-wide SwiGLU
+    product; bit-identical to the CPU backend."""
+    _check(_greedy("llama3-70b-2l-q4km", 32, 16, True))
+
+
+def test_greedy_llama3_70b_2layer_prompt512():
+    """The same 70B-shaped model with a 512-token prompt: the MFMA prefill tiles at M = 28672 /
+    K = 8192 and K = 28672, the prefill flash attention with 64 query heads, then decode."""
+    _check(_greedy("llama3-70b-2l-q4km", 512, 8, True))
+
+
+_VDEV_RUN = """
+import sys, json
+import numpy as np
+sys.path.insert(0, {repo!r})
+import llamacog_amd as la
+from llamacog_amd import gguf_synth as gs
+path = gs.ensure({cfg!r})
+prompt = [1] + np.random.default_rng(7).integers(300, gs.CONFIGS[{cfg!r}].n_vocab, {n_prompt} - 1).tolist()
+lib = la.llb()
+names = [n for _, n, _ in la.devices(lib)]
+m = la.Model(path, gpu=True, n_ctx=512, n_gpus=2, split_mode={split_mode})
+ids, lg = m.greedy(prompt, {n_gen})
+log = la.log_tail(m.lib, 1 << 20)
+m.close()
+np.save({out!r}, lg)
+print(json.dumps({{"devices": names, "handoffs": la.handoff_stats(),
+                   "pipeline": [l for l in log.splitlines() if "pipeline parallelism" in l or "graph splits" in l][-3:]}}))
+"""
+
+
+def _vdev_greedy(tmp_path, cfg, n_prompt, n_gen, split_mode=1, p2p=None):
+    """greedy decode over two VIRTUAL MI355X devices of the one GPU (GGML_MI355X_VDEV=2, read at
+    registration, so in a child process) vs the CPU backend in this process"""
+    env = dict(os.environ, GGML_MI355X_VDEV="2")
+    env.pop("GGML_MI355X_P2P", None)
+    if p2p:
+        env["GGML_MI355X_P2P"] = p2p
+    f = str(tmp_path / "lg.npy")
+    code = _VDEV_RUN.format(repo=la.REPO, cfg=cfg, n_prompt=n_prompt, n_gen=n_gen, split_mode=split_mode, out=f)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    info = __import__("json").loads(r.stdout.strip().splitlines()[-1])
+    lg_g = np.load(f)
+    path = gs.ensure(cfg)
+    prompt = [1] + np.random.default_rng(7).integers(300, gs.CONFIGS[cfg].n_vocab, n_prompt - 1).tolist()
+    m = la.Model(path, gpu=False, n_ctx=512, n_threads=16)
+    ids_c, lg_c = m.greedy(prompt, n_gen)
+    m.close()
+    ids_g = lg_g.argmax(axis=1)
+    _check({True: (ids_g, lg_g), False: (ids_c, lg_c)})
+    return info
+
+
+@pytest.mark.parametrize("cfg", ["tiny-q4km", "llama3-8b-2l-q4km"])
+def test_greedy_layer_split_virtual_devices_bit_identical(cfg, tmp_path):
+    """libllama's -sm layer pipeline (BASELINE.json configs[3]'s partition) over two ggml devices
+    on this one GPU: contiguous layer ranges per device, the scheduler's n_copies = 4 pipeline
+    with events, and every stage boundary through our cpy_tensor_async (same-GPU async copy +
+    pooled event).  Logits bit-identical to the CPU backend; hand-offs counted."""
+    info = _vdev_greedy(tmp_path, cfg, 16, 16)
+    assert "MI355X0" in info["devices"] and "MI355X1" in info["devices"], info
+    rccl, peer, d2d = info["handoffs"]
+    assert d2d > 0 and rccl == 0 and peer == 0, info
+    assert any("pipeline parallelism enabled" in l for l in info["pipeline"]), info
+
+
+def test_greedy_layer_split_virtual_devices_rccl(tmp_path):
+    """The same split with GGML_MI355X_P2P=rccl: every same-GPU stage hand-off goes through RCCL
+    (a one-rank communicator, ncclSend + ncclRecv to self in one group on the source stream), so
+    the RCCL transport runs on a one-GPU box; bit-identical logits."""
+    info = _vdev_greedy(tmp_path, "tiny-q4km", 16, 16, p2p="rccl")
+    rccl, peer, d2d = info["handoffs"]
+    assert rccl > 0 and d2d == 0, info
+
+
+@pytest.mark.parametrize("cfg", ["tiny-q4km", "llama3-8b-2l-q4km"])
+def test_concurrent_contexts_bit_identical(cfg):
+    """tests/test-thread-safety.cpp's pattern: several contexts of one model on MI355X0, each
+    decoding in its own thread at the same time (own backend, stream, scratch arena and captured
+    hipGraphs; process-wide state — the registry, RCCL clique, timing accumulators — behind
+    mutexes or atomics).  Every context's logits equal the serial CPU backend's bit for bit."""
+    path = gs.ensure(cfg)
+    prompt = [1] + np.random.default_rng(11).integers(300, gs.CONFIGS[cfg].n_vocab, 23).tolist()
+    m = la.Model(path, gpu=True, n_ctx=256)
+    ids_t, lg_t = m.greedy_threads(3, prompt, 12)
+    m.close()
+    c = la.Model(path, gpu=False, n_ctx=256, n_threads=16)
+    ids_c, lg_c = c.greedy(prompt, 12)
+    c.close()
+    for k in range(ids_t.shape[0]):
+        _check({True: (ids_t[k], lg_t[k]), False: (ids_c, lg_c)})
+
+
 def test_greedy_tiny_q8_0_kv_cache():
     """A q8_0 KV cache (-ctk q8_0 -ctv q8_0) with flash attention."""
     _check(_greedy("tiny-q4km", 16, 16, True, kv="q8_0"))

@@ -15,8 +15,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -47,6 +49,7 @@ struct llb {
     const llama_vocab * vocab = nullptr;
     int n_vocab = 0;
     int n_batch = 0;
+    llama_context_params cparams;
     std::vector<ggml_backend_dev_t> devs;
 };
 
@@ -137,6 +140,7 @@ void * llb_open(const char * path, unsigned long long gpu_mask, int n_gpu_layers
         cp.cb_eval = dump_cb;
         cp.cb_eval_user_data = h;
     }
+    h->cparams = cp;
     h->ctx = llama_init_from_model(h->model, cp);
     if (!h->ctx) { llama_model_free(h->model); delete h; return nullptr; }
     h->vocab = llama_model_get_vocab(h->model);
@@ -233,6 +237,46 @@ int llb_greedy(void * hp, const int32_t * prompt, int n_prompt, int n_gen, int32
         if (s + 1 < n_gen && llb_decode(hp, &t, 1) != 0) return -2;
     }
     return 0;
+}
+
+// tests/test-thread-safety.cpp's pattern (several contexts of one model, each decoding in its own
+// thread at the same time): n_contexts extra contexts on h's model, each greedy-decodes the same
+// prompt concurrently; ids [c][n_gen], logits [c][n_gen][n_vocab].  Returns 0, or -(1 + c) for
+// the first context that failed
+int llb_greedy_threads(void * hp, int n_contexts, const int32_t * prompt, int n_prompt, int n_gen, int32_t * out_ids,
+                       float * out_logits) {
+    auto * h = (llb *) hp;
+    std::vector<llama_context *> ctxs(n_contexts, nullptr);
+    for (int c = 0; c < n_contexts; ++c) {
+        ctxs[c] = llama_init_from_model(h->model, h->cparams);
+        if (!ctxs[c]) {
+            for (auto * x : ctxs) if (x) llama_free(x);
+            return -(1 + c);
+        }
+    }
+    std::atomic<int> failed{0};
+    std::vector<std::thread> th;
+    for (int c = 0; c < n_contexts; ++c) {
+        th.emplace_back([&, c]() {
+            llama_context * ctx = ctxs[c];
+            std::vector<int32_t> p(prompt, prompt + n_prompt);
+            if (llama_decode(ctx, llama_batch_get_one(p.data(), n_prompt)) != 0) { failed = 1 + c; return; }
+            for (int s = 0; s < n_gen; ++s) {
+                llama_synchronize(ctx);
+                const float * lg = llama_get_logits_ith(ctx, -1);
+                float * dst = out_logits + ((size_t) c * n_gen + s) * h->n_vocab;
+                memcpy(dst, lg, sizeof(float) * h->n_vocab);
+                int best = 0;
+                for (int i = 1; i < h->n_vocab; ++i) if (lg[i] > lg[best]) best = i;
+                out_ids[(size_t) c * n_gen + s] = best;
+                int32_t t = best;
+                if (s + 1 < n_gen && llama_decode(ctx, llama_batch_get_one(&t, 1)) != 0) { failed = 1 + c; return; }
+            }
+        });
+    }
+    for (auto & t : th) t.join();
+    for (auto * x : ctxs) llama_free(x);
+    return failed ? -failed.load() : 0;
 }
 
 // copy (a tail of) the captured log; returns its full length
