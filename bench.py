@@ -7,13 +7,15 @@ the MI355X plugin loaded.  A "step" is one single-token llama_decode (n_batch = 
 BASELINE.json configs[1] decode workload); K timed steps are bracketed by a barrier and a
 device synchronisation, the max over ranks is taken, and rank 0 prints one JSON line.
 
-Multi-GPU (BASELINE.json configs[3]): --gpus N > 1 runs Llama-3-70B Q4_K_M
-split by layers over N devices in ONE process (libllama -sm layer; our backend is one device
-per GPU and the stage hand-off between devices is an RCCL ncclSend/ncclRecv pair,
-backend.cpp cpy_tensor_async).  Under torch.distributed.run (one process per GPU, as the
-driver launches it) rank 0 owns all N devices and the other ranks only join the barriers and
-the max; value = the single stream's tok/s ("strong": fixed work, more devices).  N = 1 is the
-8B headline workload.  --cpu runs the harness on the CPU backend (tests only).
+Multi-GPU.  `value` is the same workload at every N: under
+torch.distributed.run (one process per GPU, as the driver launches it) every rank decodes its
+own Llama-3-8B replica on its own GPU, and value = N streams x K steps / the slowest rank's time
+("weak": fixed work per GPU).  Beside it, `split_series` is BASELINE.json configs[3] at the same
+N: Llama-3-70B Q4_K_M split by layers over the N GPUs in ONE process (libllama -sm layer, the
+scheduler's pipeline copies, stage hand-offs through backend.cpp cpy_tensor_async = RCCL
+ncclSend/ncclRecv between GPUs), run by rank 0 in a child process that sees every GPU while the
+other ranks wait at a barrier; N = 1 gives the 70B's one-GPU point of the same series.
+--cpu runs the harness on the CPU backend (tests only).
 
 Extra objects on the line: "roofline" (the dominant kernel — the quantized mat-vec — timed
 with HIP events on the plugin's stream; fractions against the measured STREAM-read peak and
@@ -46,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--config", default=None, help="default: llama3-8b-q4km at --gpus 1, llama3-70b-q4km above")
+    ap.add_argument("--config", default="llama3-8b-q4km")
     ap.add_argument("--layers", type=int, default=None, help="override layer count (debug only)")
     ap.add_argument("--pp", type=int, default=512, help="prompt length for the pp figure (0 = skip)")
     ap.add_argument("--pp-reps", type=int, default=3, help="timed pp runs after the warmup run (mean tok/s)")
@@ -60,10 +62,12 @@ def parse():
     ap.add_argument("--cpu", action="store_true", help="run the harness on the CPU backend (tests)")
     ap.add_argument("--model-dir", default=os.environ.get("LLAMACOG_MODEL_DIR", "/tmp/llamacog_amd_models"))
     ap.add_argument("--verbose", action="store_true")
-    a = ap.parse_args()
-    if a.config is None:
-        a.config = "llama3-70b-q4km" if a.gpus > 1 else "llama3-8b-q4km"
-    return a
+    ap.add_argument("--no-split-series", action="store_true", help="skip the 70B layer-split series")
+    ap.add_argument("--split-config", default="llama3-70b-q4km")
+    ap.add_argument("--split-steps", type=int, default=32)
+    ap.add_argument("--split-warmup", type=int, default=4)
+    ap.add_argument("--split-only", action="store_true", help=argparse.SUPPRESS)   # the series' child process
+    return ap.parse_args()
 
 
 def dist_env():
@@ -156,12 +160,13 @@ def cpu_baseline(model: str, threads: int, reps: int, fa: int) -> dict:
 
 def main():
     a = parse()
+    if a.split_only:
+        return split_only(a)
     ws, rank, lrank = dist_env()
-    split = a.gpus > 1                   # one stream, layers split over a.gpus devices
-    if ws > 1 and not split:
+    visible = os.environ.get("HIP_VISIBLE_DEVICES")   # the job's GPUs (the split series' child sees all)
+    if ws > 1:
         # replicas: restrict each rank's HIP runtime to its own GPU before anything touches HIP
-        os.environ["HIP_VISIBLE_DEVICES"] = str(lrank)
-    worker = (rank == 0) or not split    # in split mode rank 0 owns every device
+        os.environ["HIP_VISIBLE_DEVICES"] = visible.split(",")[lrank] if visible else str(lrank)
     dist = Dist(ws)
 
     import llamacog_amd as la
@@ -179,22 +184,72 @@ def main():
 
     gpu = not a.cpu
     n_ctx = ((a.warmup + a.steps + a.depth + max(a.pp, 0) + a.roofline_steps + 255) // 256 + 1) * 256
-    res = {}
-    if worker:
-        res = run_worker(a, la, path, gpu, n_ctx, split, dist)
-    else:
-        dist.barrier()                   # the worker's tg start
-        dist.barrier()                   # its end
-        dist.max(0.0)
+    res = run_worker(a, la, path, gpu, n_ctx, dist)
+    # the 70B layer-split series at this N: rank 0's child process over every GPU of the job
+    dist.barrier()
+    if rank == 0 and not a.no_split_series:
+        res["split_series"] = split_child(a, max(a.gpus, ws), visible)
+    dist.barrier()
     if rank == 0:
-        emit(a, la, gguf_synth, cfg, suffix, ws, split, gpu, n_ctx, res)
+        emit(a, la, gguf_synth, cfg, suffix, ws, gpu, n_ctx, res)
     dist.close()
 
 
-def run_worker(a, la, path, gpu, n_ctx, split, dist) -> dict:
-    r = {}
+def split_child(a, n: int, visible) -> dict:
+    """runs bench.py --split-only in a child process (all of the job's GPUs visible, no rank
+    environment) and returns its JSON object"""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                            "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK", "ROLE_RANK")}
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    if visible:
+        env["HIP_VISIBLE_DEVICES"] = visible
+    cmd = [sys.executable, os.path.abspath(__file__), "--split-only", "--gpus", str(n), "--config", a.split_config,
+           "--steps", str(a.split_steps), "--warmup", str(a.split_warmup), "--model-dir", a.model_dir, "--fa", str(a.fa),
+           "--kv", a.kv] + (["--cpu"] if a.cpu else [])
+    t0 = time.time()
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=1800, env=env)
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    if out.returncode != 0 or not lines:
+        return {"error": f"rc={out.returncode}: {out.stderr[-400:]}"}
+    d = json.loads(lines[-1])
+    d["wall_s"] = round(time.time() - t0, 1)
+    return d
+
+
+def split_only(a):
+    """the split series' child: the layer split of a.config over a.gpus devices in this process"""
+    import llamacog_amd as la
+    from llamacog_amd import gguf_synth
+    path = os.path.join(a.model_dir, f"{a.config}-s0.gguf")
+    t0 = time.time()
+    if not os.path.exists(path):
+        gguf_synth.ensure(a.config, path, seed=0)
+    t_write = time.time() - t0
+    gpu = not a.cpu
+    n_ctx = ((a.warmup + a.steps + 255) // 256 + 1) * 256
     m = la.Model(path, gpu=gpu, n_ctx=n_ctx, flash_attn=bool(a.fa), kv_type=a.kv,
-                 n_gpus=(a.gpus if split else 1) if gpu else None, split_mode=1)
+                 n_gpus=a.gpus if gpu else None, split_mode=1)
+    devs = [n for _, n, t in la.devices(m.lib) if n.startswith("MI355X")][:a.gpus] if gpu else ["CPU"]
+    h0 = la.handoff_stats() if gpu else (0, 0, 0)
+    if a.warmup > 0:
+        m.time_gen(a.warmup)
+    t = m.time_gen(a.steps)
+    h1 = la.handoff_stats() if gpu else (0, 0, 0)
+    m.close()
+    cfg = gguf_synth.CONFIGS[a.config]
+    print(json.dumps({
+        "model": a.config, "n_devices": len(devs), "devices": devs, "steps": a.steps, "warmup": a.warmup,
+        "tg_tok_s": round(a.steps / t, 3), "ms_per_token": round(1e3 * t / a.steps, 4),
+        "weight_bytes_per_token": gguf_synth.weight_bytes_per_token(cfg),
+        "stage_handoffs": dict(zip(("rccl", "peer", "d2d"), (h1[i] - h0[i] for i in range(3)))),
+        "gguf_write_s": round(t_write, 1),
+        "partition": f"libllama -sm layer over {len(devs)} device(s): contiguous layer ranges, output on the last",
+    }))
+
+
+def run_worker(a, la, path, gpu, n_ctx, dist) -> dict:
+    r = {}
+    m = la.Model(path, gpu=gpu, n_ctx=n_ctx, flash_attn=bool(a.fa), kv_type=a.kv, n_gpus=1 if gpu else None)
     plugin = la.plugin_lib() if gpu else None
     if a.verbose:
         print(la.log_tail(m.lib)[-4000:], file=sys.stderr)
@@ -254,13 +309,12 @@ def run_worker(a, la, path, gpu, n_ctx, split, dist) -> dict:
         fa_ms, _, fa_n = la.kernel_timing(plugin, 2)
         r["roof"] = (mv_ms, mv_bytes, mv_n, fa_ms, fa_n, t_rf)
         r["gstats"] = la.graph_stats()
-        r["p2p"] = la.p2p_stats()
     m.close()
     if gpu:
         # the measured STREAM-read ceiling of device 0 (k_stream.hip), after the model is gone
         r["hbm_gbs"] = la.hbm_read_gbs(0)
     r["cpu"] = None
-    if not a.no_cpu_baseline and not split and not a.cpu:
+    if not a.no_cpu_baseline and not a.cpu and int(os.environ.get("RANK", "0")) == 0:
         try:
             r["cpu"] = cpu_baseline(path, a.cpu_threads, a.cpu_reps, a.fa)
         except Exception as e:  # the baseline must never hide the GPU result
@@ -268,10 +322,10 @@ def run_worker(a, la, path, gpu, n_ctx, split, dist) -> dict:
     return r
 
 
-def emit(a, la, gguf_synth, cfg, suffix, ws, split, gpu, n_ctx, r):
+def emit(a, la, gguf_synth, cfg, suffix, ws, gpu, n_ctx, r):
     t = r["t"]
-    n_units = a.gpus if split else ws          # devices in the job
-    streams = 1 if split else ws               # independent decode streams
+    n_units = ws                               # GPUs in the job, one replica each
+    streams = ws                               # independent decode streams
     value = streams * a.steps / t
     wbytes = gguf_synth.weight_bytes_per_token(
         gguf_synth.ModelConfig(**{**cfg.__dict__, "n_layer": a.layers or cfg.n_layer}))
@@ -319,7 +373,7 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, split, gpu, n_ctx, r):
         "warmup": a.warmup,
         "ms_per_step": round(1e3 * t / a.steps, 4),
         "higher_is_better": True,
-        "scaling": "strong" if split else "weak",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "i8",
         "data": "synthetic",
@@ -330,8 +384,7 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, split, gpu, n_ctx, r):
             "model": a.config + suffix,
             "global_batch": streams,
             "seq_len": depth1,
-            "parallelism": (f"layer split over {a.gpus} GPUs in one process (libllama -sm layer, RCCL send/recv "
-                            f"stage hand-off)" if split else (f"replicas x{ws}" if ws > 1 else "single GPU")),
+            "parallelism": f"replicas x{ws} (one Llama-3-8B decode stream per GPU)" if ws > 1 else "single GPU",
         },
         "pp_tok_s": round(pp_tps, 2) if pp_tps else None,
         "pp_tokens": a.pp,
@@ -352,7 +405,8 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, split, gpu, n_ctx, r):
         "step_split_ms": r.get("split"),
         "cpu_baseline": r.get("cpu"),
         "hipgraph": dict(zip(("captures", "replays"), r["gstats"])) if r.get("gstats") else None,
-        "stage_handoffs": dict(zip(("rccl", "peer"), r["p2p"])) if r.get("p2p") else None,
+        # BASELINE.json configs[3] at this N: the 70B split by layers over the job's GPUs
+        "split_series": r.get("split_series"),
     }
     print(json.dumps(out))
 

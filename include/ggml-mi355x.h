@@ -43,6 +43,14 @@ int  ggml_backend_mi355x_get_timing(int kind, double * ms, double * bytes, long 
 // with hipGraph replay), kind 6 = host time spent inside graph_compute
 void ggml_backend_mi355x_set_graph_timing(int enable);
 
+// in-graph kernel timeline (profiling): each instrumented launch (the decode mat-vecs and the
+// exact flash attention) stamps the chip's realtime counter per workgroup at entry and per wave
+// at exit, also inside replayed hipGraphs; graph_compute then synchronises and decodes the
+// stamps.  ktrace_dump writes "graph,idx,kernel,nwg,start_ns,last_start_ns,end_ns" rows (times
+// from the graph's first stamp), clears them and returns the row count (-1: file error)
+void ggml_backend_mi355x_set_ktrace(int enable);
+int  ggml_backend_mi355x_ktrace_dump(const char * path);
+
 // run-time switches (default from GGML_MI355X_NO_FUSE / GGML_MI355X_NO_GRAPH): no_fuse = one
 // kernel per ggml node, no_graph = no hipGraph replay of repeated graphs
 void ggml_backend_mi355x_set_flags(int no_fuse, int no_graph);

@@ -122,6 +122,9 @@ void exec_ctx::free_scratch() {
     tail_cnt = nullptr;
     if (rsum_buf) (void) hipFree(rsum_buf);
     rsum_buf = nullptr;
+    if (kt_buf) (void) hipFree(kt_buf);
+    kt_buf = nullptr;
+    kt_cap = kt_off = 0;
 }
 
 hipEvent_t exec_ctx::get_event() {
@@ -389,6 +392,8 @@ struct graph_entry {
     hipGraphExec_t  exec = nullptr;
     uint64_t        last_use = 0;
     uint64_t        gen = 0;          // exec_ctx::scratch_gen the graph was captured under
+    std::vector<exec_ctx::kt_launch> kt_list;   // timeline regions baked into the capture
+    size_t          kt_off = 0;
 };
 
 struct mi_backend_ctx {
@@ -585,8 +590,27 @@ static std::atomic<int> g_no_fuse{env_flag("GGML_MI355X_NO_FUSE")};
 // kernels of a replayed hipGraph; under kernel tracing the same kernels are launched
 // eagerly instead (profiles/README.md)
 static std::atomic<int> g_no_graph{env_flag("GGML_MI355X_NO_GRAPH") | env_flag("ROCPROF_KERNEL_TRACE")};
+// in-graph kernel timeline (profiling; GGML_MI355X_KTRACE=1 or ggml_backend_mi355x_set_ktrace)
+static std::atomic<int> g_ktrace{env_flag("GGML_MI355X_KTRACE")};
+struct kt_sample { long graph; int idx; const char * name; unsigned nwg; double t0, t_last_start, t1; };
+static std::mutex g_kt_mtx;
+static std::vector<kt_sample> g_kt_samples;
+static long g_kt_graphs = 0;
 
 namespace mi355x {
+bool ktrace_enabled() { return g_ktrace.load(std::memory_order_relaxed) != 0; }
+
+unsigned long long * exec_ctx::kt_take(const char * name, unsigned nwg, unsigned threads) {
+    if (!kt_buf) return nullptr;
+    const unsigned stride = 1 + threads / 64;
+    const size_t n = (size_t) nwg * stride;
+    if (kt_off + n > kt_cap) return nullptr;
+    kt_list.push_back({name, kt_off, nwg, stride});
+    unsigned long long * p = kt_buf + kt_off;
+    kt_off += n;
+    return p;
+}
+
 bool fusion_enabled() { return g_no_fuse.load(std::memory_order_relaxed) == 0; }
 bool graphs_enabled() { return g_no_graph.load(std::memory_order_relaxed) == 0; }
 }
@@ -613,6 +637,7 @@ static void graph_signature(ggml_cgraph * cgraph, std::vector<int64_t> & sig) {
         for (int k = 0; k < 4; ++k) sig.push_back((int64_t) t->nb[k]);
     };
     sig.push_back(n);
+    sig.push_back(ktrace_enabled() ? 1 : 0);   // a traced capture bakes the timeline regions in
     for (int i = 0; i < n; ++i) {
         const ggml_tensor * t = ggml_graph_node(cgraph, i);
         sig.push_back((int64_t) (intptr_t) t);
@@ -705,6 +730,41 @@ static bool mi_backend_cpy_tensor_async(ggml_backend_t backend_src, ggml_backend
     return true;
 }
 
+// decodes the current graph's timeline regions (synchronous: profiling runs only)
+static void kt_collect(mi_backend_ctx * ctx) {
+    auto & ex = ctx->ex;
+    MI_CHECK(hipStreamSynchronize(ex.stream));
+    if (ex.kt_list.empty()) return;
+    std::vector<unsigned long long> h(ex.kt_off);
+    MI_CHECK(hipMemcpy(h.data(), ex.kt_buf, ex.kt_off * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    static double tick_ns = 0.0;
+    if (tick_ns == 0.0) {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device) != hipSuccess || khz <= 0) khz = 100000;
+        tick_ns = 1e6 / khz;
+    }
+    std::lock_guard<std::mutex> lk(g_kt_mtx);
+    const long gs = g_kt_graphs++;
+    unsigned long long base = ~0ull;
+    for (auto & l : ex.kt_list) {
+        for (unsigned w = 0; w < l.nwg; ++w) {
+            const unsigned long long v = h[l.off + (size_t) w * l.stride];
+            if (v && v < base) base = v;
+        }
+    }
+    for (size_t i = 0; i < ex.kt_list.size(); ++i) {
+        const auto & l = ex.kt_list[i];
+        unsigned long long s0 = ~0ull, sl = 0, e1 = 0;
+        for (unsigned w = 0; w < l.nwg; ++w) {
+            const unsigned long long * r = h.data() + l.off + (size_t) w * l.stride;
+            if (r[0]) { s0 = std::min(s0, r[0]); sl = std::max(sl, r[0]); }
+            for (unsigned k = 1; k < l.stride; ++k) e1 = std::max(e1, r[k]);
+        }
+        if (s0 == ~0ull) continue;
+        g_kt_samples.push_back({gs, (int) i, l.name, l.nwg, (s0 - base) * tick_ns, (sl - base) * tick_ns, (e1 - base) * tick_ns});
+    }
+}
+
 static void mi_backend_synchronize(ggml_backend_t backend) {
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
@@ -713,6 +773,8 @@ static void mi_backend_synchronize(ggml_backend_t backend) {
 }
 
 static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
+    ex.kt_off = 0;
+    ex.kt_list.clear();
     ex.qcache_clear();
     ex.rt_table = nullptr;
     ex.done.clear();
@@ -767,6 +829,8 @@ static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
     e->last_use = ++ctx->use_clock;
     if (e->exec) {
         MI_CHECK(hipGraphLaunch(e->exec, ctx->ex.stream));
+        ctx->ex.kt_list = e->kt_list;
+        ctx->ex.kt_off = e->kt_off;
         g_graph_replays.fetch_add(1);
         return true;
     }
@@ -791,6 +855,8 @@ static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
     }
     MI_CHECK(hipGraphDestroy(g));
     e->gen = ctx->ex.scratch_gen;
+    e->kt_list = ctx->ex.kt_list;
+    e->kt_off = ctx->ex.kt_off;
     MI_CHECK(hipGraphLaunch(e->exec, ctx->ex.stream));
     g_graph_captures.fetch_add(1);
     return true;
@@ -810,10 +876,19 @@ static enum ggml_status mi_backend_graph_compute(ggml_backend_t backend, ggml_cg
         MI_CHECK(hipEventRecord(gbeg, ctx->ex.stream));
     }
     const bool dyn_ok = ctx->ex.prepare_dyn(cgraph);
+    const bool ktrace = ktrace_enabled();
+    if (ktrace) {
+        if (!ctx->ex.kt_buf) {
+            ctx->ex.kt_cap = (size_t) 1 << 22;
+            MI_CHECK(hipMalloc(&ctx->ex.kt_buf, ctx->ex.kt_cap * sizeof(unsigned long long)));
+        }
+        MI_CHECK(hipMemsetAsync(ctx->ex.kt_buf, 0, ctx->ex.kt_cap * sizeof(unsigned long long), ctx->ex.stream));
+    }
     const bool use_graph = dyn_ok && graphs_enabled() && !ctx->graphs_broken && !ctx->ex.timing;
     if (!use_graph || !graph_compute_hipgraph(ctx, cgraph)) {
         run_nodes(ctx->ex, cgraph);
     }
+    if (ktrace) kt_collect(ctx);
     if (gtime) {
         hipEvent_t gend = ctx->ex.get_event();
         MI_CHECK(hipEventRecord(gend, ctx->ex.stream));
@@ -1126,6 +1201,23 @@ GGML_BACKEND_API void ggml_backend_mi355x_set_flags(int no_fuse, int no_graph) {
 }
 
 GGML_BACKEND_API void ggml_backend_mi355x_set_timing(int enable) { g_timing.store(enable ? 1 : 0); }
+
+GGML_BACKEND_API void ggml_backend_mi355x_set_ktrace(int enable) { g_ktrace.store(enable ? 1 : 0); }
+
+GGML_BACKEND_API int ggml_backend_mi355x_ktrace_dump(const char * path) {
+    std::lock_guard<std::mutex> lk(g_kt_mtx);
+    FILE * f = fopen(path, "w");
+    if (!f) return -1;
+    fprintf(f, "graph,idx,kernel,nwg,start_ns,last_start_ns,end_ns\n");
+    for (const auto & k : g_kt_samples) {
+        fprintf(f, "%ld,%d,%s,%u,%.0f,%.0f,%.0f\n", k.graph, k.idx, k.name, k.nwg, k.t0, k.t_last_start, k.t1);
+    }
+    fclose(f);
+    const int n = (int) g_kt_samples.size();
+    g_kt_samples.clear();
+    g_kt_graphs = 0;
+    return n;
+}
 
 GGML_BACKEND_API void ggml_backend_mi355x_reset_timing(void) {
     std::lock_guard<std::mutex> lk(g_timing_mtx);

@@ -68,6 +68,18 @@ __device__ __forceinline__ uint16_t ld2(const void * p) { uint16_t v; __builtin_
 
 __device__ __forceinline__ int dot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
 
+// In-graph kernel timeline (profiling only, exec_ctx::kt_take): per workgroup the chip-wide
+// 100 MHz realtime counter at entry (slot 0) and at each wave's exit (slots 1 .. waves), so the
+// host can rebuild every instrumented launch's start, dispatch ramp, end and the gaps between
+// launches inside a REPLAYED hipGraph (rocprofv3 cannot trace replayed graphs on ROCm 7.2).
+__device__ __forceinline__ unsigned kt_wg() { return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); }
+__device__ __forceinline__ void kt_enter(unsigned long long * kt) {
+    if (kt && threadIdx.x == 0) kt[(1 + blockDim.x / 64) * kt_wg()] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void kt_exit(unsigned long long * kt) {
+    if (kt && (threadIdx.x & 63) == 0) kt[(1 + blockDim.x / 64) * kt_wg() + 1 + threadIdx.x / 64] = __builtin_amdgcn_s_memrealtime();
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

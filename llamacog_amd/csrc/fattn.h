@@ -26,6 +26,8 @@ struct fa_args {
     int * cnt;
     // microbenchmark hook: per-phase s_memtime cycles of workgroup (0,0) (nullable)
     unsigned long long * prof;
+    // in-graph kernel timeline region (common.h kt_enter / kt_exit; nullable)
+    unsigned long long * kt;
 };
 
 // set by mi355x_bench_op (capi.cpp) only; copied into fa_args.prof

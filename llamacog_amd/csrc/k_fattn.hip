@@ -450,6 +450,7 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     a.part = nullptr;
     a.qmode = 0;
     a.prof = g_fa_prof;
+    a.kt = nullptr;
     a.qs = nullptr; a.qd = nullptr; a.qsum = nullptr;
     if (nchunks > 1) a.part = (float *) ctx.scratch(1, sizeof(float) * nchunks * rows * (a.D + 2));
 
@@ -488,6 +489,8 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
                 a.cnt = ctx.fa_cnt;
             }
         }
+        // decode (one query row): k_fattn_exact, one 256-thread workgroup per head
+        if (a.n_q == 1) a.kt = ctx.kt_take("fa_exact", (unsigned) (a.H * nq3), 256);
         launch_fattn_exact(ctx.stream, a, nq3);
         if (a.qmode) ctx.qcache_put(mm->src[1], a.qmode == 1, act);
         if (ctx.timing) ctx.time_end(TK_FATTN, bytes, ev);

@@ -133,6 +133,7 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
     constexpr int CH = C::CH, U = C::U, NM = D / 16, NB = D / 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int qd = tid & 3;                 // lane in the quad of a position (phase 1)
+    kt_enter(a.kt);
     const int64_t iq1 = blockIdx.x;
     const int64_t h = blockIdx.y % a.H;
     const int64_t iq3 = blockIdx.y / a.H;
@@ -532,6 +533,7 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
             q8K_wave(q, lane, a.qs + iq1 * K + c0, a.qsum + iq1 * (K / 16) + c0 / 16, a.qd + iq1 * (K / 256) + c0 / 256);
         }
     }
+    kt_exit(a.kt);
 }
 
 // ==== prefill: a block of query rows x the G query heads of one KV head per workgroup ========

@@ -67,6 +67,7 @@ struct gemv_args {
     struct pro_t {
         const float * x; const float * w; const double * sum; float eps; int64_t n; int qmode; uint32_t lds_off;
     } pro;
+    unsigned long long * kt;              // in-graph kernel timeline region (nullable)
 };
 
 // the producer's partial sums: no-return f64 atomics serialize per 128-B line at the memory
@@ -365,7 +366,9 @@ __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_
 template <class T, int R, int WPR, int MODE>
 __global__ __launch_bounds__(256) void k_gemv_pipe(const gemv_args p, const int64_t ngroups) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
+    kt_enter(p.kt);
     gemv_pipe_body<T, R, WPR, MODE>(p, ngroups, blockIdx.x, gridDim.x, xr);
+    kt_exit(p.kt);
 }
 
 // Q/K of one K-quant and V of another (Llama-3 Q4_K_M: Q4_K and Q6_K on 16 of 32 layers) in
@@ -375,8 +378,10 @@ template <class T1, class T2, int R2, int WPR>
 __global__ __launch_bounds__(256) void k_gemv_pipe2(const gemv_args p1, const int64_t ng1, const int64_t nwg1,
                                                     const gemv_args p2, const int64_t ng2) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
+    kt_enter(p1.kt);
     if ((int64_t) blockIdx.x < nwg1) gemv_pipe_body<T1, 2, WPR, 1>(p1, ng1, blockIdx.x, nwg1, xr);
     else gemv_pipe_body<T2, R2, WPR, 1>(p2, ng2, (int64_t) blockIdx.x - nwg1, (int64_t) gridDim.x - nwg1, xr);
+    kt_exit(p1.kt);
 }
 
 
@@ -385,6 +390,8 @@ __global__ __launch_bounds__(256) void k_gemv_pipe2(const gemv_args p1, const in
 // (hipExtLaunchKernel records them at the dispatch's start and completion, without extra
 // marker packets around it), so bench.py's per-launch time is the kernel's own duration
 static thread_local hipEvent_t t_ev_beg = nullptr, t_ev_end = nullptr;
+// the launching context while a gemv_group runs (kernel timeline regions come from it)
+static thread_local exec_ctx * g_kt_ctx = nullptr;
 
 static int g_gemv_wgs = -1;    // GGML_MI355X_GEMV_WGS: persistent grid size
 static int g_num_cu = 0;
@@ -437,6 +444,15 @@ static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
         lds = (lds + 15) / 16 * 16;
         a.pro.lds_off = (uint32_t) lds;
         lds += pro_lds_bytes(a.pro.n, a.pro.qmode);
+    }
+    if (g_kt_ctx) {
+        // timeline label: the fused pieces of this launch
+        static const char * names[16] = {"gemv", "gemv+pro", "gemv+epi", "gemv+pro+epi", "gemv+tail", "gemv+pro+tail",
+                                         "gemv+epi+tail", "gemv+pro+epi+tail", "gemv+resid", "gemv+pro+resid",
+                                         "gemv+epi+resid", "gemv+pro+epi+resid", "gemv+tail+resid", "gemv+pro+tail+resid",
+                                         "gemv+epi+tail+resid", "gemv+all"};
+        const int k = (a.pro.x ? 1 : 0) | (MODE ? 2 : 0) | (a.tl.kind ? 4 : 0) | (a.rres ? 8 : 0);
+        a.kt = g_kt_ctx->kt_take(names[k], (unsigned) grid, 256);
     }
     if (t_ev_beg) {
         hipExtLaunchKernelGGL((k_gemv_pipe<T, R, WPR, MODE>), dim3((unsigned) grid), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a, ng);
@@ -504,6 +520,7 @@ static void launch_pipe2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a
         a1.pro.lds_off = a2.pro.lds_off = (uint32_t) lds;
         lds += pro_lds_bytes(a1.pro.n, a1.pro.qmode);
     }
+    a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv_pipe2", (unsigned) (w1 + w2), 64 * NWV) : nullptr;
     if (t_ev_beg) {
         hipExtLaunchKernelGGL((k_gemv_pipe2<T1, T2, R2, WPR>), dim3((unsigned) (w1 + w2)), dim3(64 * NWV), lds, st, t_ev_beg, t_ev_end,
                               0, a1, ng1, w1, a2, ng2);
@@ -575,6 +592,7 @@ bool gemv_epilogue_ok(const ggml_tensor * mm) { return gemv_supported(mm); }
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi) {
     GGML_ASSERT(nmat >= 1 && nmat <= GEMV_MAXMAT);
     gemv_init();
+    g_kt_ctx = ctx.kt_buf ? &ctx : nullptr;
     const ggml_tensor * src1 = mms[0]->src[1];
     const ggml_type wt = mms[0]->src[0]->type;
     const bool kq = is_kq(wt);
@@ -703,6 +721,7 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         t_ev_beg = t_ev_end = nullptr;
     }
     if (a.tl.qmode) ctx.qcache_put(epi->tq_key, tkq, tact);
+    g_kt_ctx = nullptr;
 }
 
 // the SwiGLU tails' arrival counters exist (allocated outside any capture, zeroed once)

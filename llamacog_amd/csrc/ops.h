@@ -126,6 +126,17 @@ struct exec_ctx {
         qc_tensor = t; qc_data = t->data; qc_kquant = k_quant; qc_act = act;
     }
 
+    // in-graph kernel timeline (GGML_MI355X_KTRACE / ggml_backend_mi355x_set_ktrace): a device
+    // buffer of realtime stamps (common.h kt_enter / kt_exit), one region per instrumented launch
+    // of the current graph, in launch order; the list is kept with a captured graph so a replay
+    // is decoded against the launches it replays
+    struct kt_launch { const char * name; size_t off; unsigned nwg; unsigned stride; };
+    unsigned long long * kt_buf = nullptr;
+    size_t kt_cap = 0, kt_off = 0;
+    std::vector<kt_launch> kt_list;
+    // region for one launch of nwg workgroups of `threads` threads, or nullptr (tracing off / full)
+    unsigned long long * kt_take(const char * name, unsigned nwg, unsigned threads);
+
     // kernel timing (HIP events on `stream`) for the roofline figure in bench.py
     bool   timing = false;
     struct timed { hipEvent_t beg, end; double bytes; int kind; };
@@ -150,6 +161,7 @@ bool fusion_enabled();
 bool graphs_enabled();
 // blocks while any thread has a hipGraph capture open (backend.cpp)
 void wait_no_capture();
+bool ktrace_enabled();
 
 // supports / dispatch
 bool op_supported(const ggml_tensor * op);

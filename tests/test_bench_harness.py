@@ -1,10 +1,10 @@
 """bench.py's multi-process contract on CPU (gloo, world_size 2, 127.0.0.1), as the driver
 launches it: `torch.distributed.run --nproc-per-node N bench.py --gpus N`.  The harness runs
 with --cpu (libllama's CPU backend, a tiny synthetic model), so what is tested is the rank
-logic — barriers, the max over ranks, rank 0's single JSON line — for both modes:
-  * --gpus 2: one stream split over two devices in rank 0's process (strong scaling; the
-    other rank only joins the barriers and the max);
-  * --gpus 1 under two ranks: replicas (weak scaling, value = 2 x steps / max time)."""
+logic — barriers, the max over ranks, rank 0's single JSON line — and the split series:
+  * value: one replica per rank (weak scaling, value = N x steps / the slowest rank's time);
+  * split_series: rank 0's child process (no rank environment) runs the layer-split model and
+    its object rides on the same line, at N = 2 and at N = 1."""
 import json
 import os
 import socket
@@ -30,12 +30,15 @@ def tiny_dir(tmp_path_factory):
     return str(d)
 
 
-def _run(tiny_dir, gpus):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--cpu", "--config", "tiny-q4km",
-           "--steps", "4", "--warmup", "1", "--pp", "0", "--roofline-steps", "0", "--no-cpu-baseline",
-           "--model-dir", tiny_dir]
+def _run(tiny_dir, gpus, nproc=2):
+    bench = [os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--cpu", "--config", "tiny-q4km",
+             "--steps", "4", "--warmup", "1", "--pp", "0", "--roofline-steps", "0", "--no-cpu-baseline",
+             "--model-dir", tiny_dir, "--split-config", "tiny-q4km", "--split-steps", "3", "--split-warmup", "1"]
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + bench
+    else:
+        cmd = [sys.executable] + bench
     env = dict(os.environ, OMP_NUM_THREADS="2")
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -44,16 +47,20 @@ def _run(tiny_dir, gpus):
     return json.loads(lines[0])
 
 
-def test_split_mode_two_ranks(tiny_dir):
+def test_replicas_two_ranks_with_split_series(tiny_dir):
     d = _run(tiny_dir, 2)
-    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["global_batch"] == 1
-    assert d["steps"] == 4 and d["value"] > 0
-    assert abs(d["value"] - 4 / (d["ms_per_step"] * 4 / 1e3)) / d["value"] < 0.01
-    assert "layer split over 2 GPUs" in d["config"]["parallelism"]
-
-
-def test_replica_mode_two_ranks(tiny_dir):
-    d = _run(tiny_dir, 1)
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["config"]["global_batch"] == 2
+    assert d["steps"] == 4 and d["value"] > 0
     # value is the whole job: two streams over the slowest rank's time
     assert abs(d["value"] - 2 * 4 / (d["ms_per_step"] * 4 / 1e3)) / d["value"] < 0.01
+    assert "replicas x2" in d["config"]["parallelism"]
+    sp = d["split_series"]
+    assert sp and "error" not in sp, sp
+    assert sp["model"] == "tiny-q4km" and sp["steps"] == 3 and sp["tg_tok_s"] > 0
+
+
+def test_single_process_with_split_series(tiny_dir):
+    d = _run(tiny_dir, 1, nproc=1)
+    assert d["n_gpus"] == 1 and d["config"]["global_batch"] == 1 and d["value"] > 0
+    sp = d["split_series"]
+    assert sp and "error" not in sp and sp["tg_tok_s"] > 0, sp
