@@ -351,10 +351,20 @@ static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tenso
     // its own prologue), and the norm output itself may be read only by the MUL
     std::vector<const ggml_tensor *> readers;
     const int pl = node_index(g, last);
+    int64_t rows = 0;
     for (int k = pl + 1; k < n && k <= pl + 16; ++k) {
         const ggml_tensor * c = ggml_graph_node(g, k);
-        if (c->op == GGML_OP_MUL_MAT && c->src[1] == last && gemv_supported(c)) readers.push_back(c);
+        if (c->op == GGML_OP_MUL_MAT && c->src[1] == last && gemv_supported(c)) {
+            readers.push_back(c);
+            rows += c->ne[0];
+        }
     }
+    // the one-shot GEMV forms the prologue in every workgroup: for wide consumers (the FFN
+    // gate/up, 28672 rows; the output head) that is thousands of redundant norms, and the
+    // stand-alone norm kernel plus a prologue-free launch measured faster (round 3 kernel
+    // timeline: gate/up 27.0 us with the prologue vs 15 + 4 without); Q/K/V keep it
+    static const int64_t pro_max = getenv("GGML_MI355X_PRO_MAX_ROWS") ? atoll(getenv("GGML_MI355X_PRO_MAX_ROWS")) : 16384;
+    if (rows > pro_max) return;
     if (!dead_after(g, n, pl + 1, last, readers)) return;
     if (mul && !dead_after(g, n, pn + 1, nm, {mul})) return;
     double * site = gemv_rsum_site(ctx);
@@ -558,7 +568,9 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     // the next norm chain moves into this launch (residual producer) and its consumers
     // (prologue); silu(gate) * up into the gate/up launch (SwiGLU tail).  GGML_MI355X_TAILS=0 /
     // GGML_MI355X_RESID=0 run those chains as their own launches (k_fused.hip)
-    static const bool tails = !getenv("GGML_MI355X_TAILS") || atoi(getenv("GGML_MI355X_TAILS")) != 0;
+    // the SwiGLU tail measured slower than the stand-alone product kernel in the replayed graph
+    // (in-graph kernel timeline, round 3: 2725 vs 2673 us per Llama-3-8B token): opt-in
+    static const bool tails = getenv("GGML_MI355X_TAILS") && atoi(getenv("GGML_MI355X_TAILS")) != 0;
     static const bool resid = !getenv("GGML_MI355X_RESID") || atoi(getenv("GGML_MI355X_RESID")) != 0;
     bool plain = true;
     for (int m = 0; m < nm; ++m) {

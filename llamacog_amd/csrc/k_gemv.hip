@@ -68,6 +68,7 @@ struct gemv_args {
         const float * x; const float * w; const double * sum; float eps; int64_t n; int qmode; uint32_t lds_off;
     } pro;
     unsigned long long * kt;              // in-graph kernel timeline region (nullable)
+    uint32_t wl_off;                      // one-shot kernel: LDS byte offset of the weight slices
 };
 
 // the producer's partial sums: no-return f64 atomics serialize per 128-B line at the memory
@@ -191,6 +192,72 @@ __device__ __forceinline__ void gemv_prologue(const gemv_args & p, uint8_t * buf
     A = {qs, qd, qsum};
 }
 
+// The same prologue in two halves for the one-shot kernel: gemv_pro_load issues the partial-sum
+// load and the first 4096 elements' x / w loads into registers BEFORE the weight DMAs, so that
+// the wait for them (vmcnt counts the DMAs issued after) leaves the weight stream in flight;
+// gemv_pro_finish forms the activation (later passes of n > 4096 load inline).
+struct pro_regs { double s; float4 xv[4], wv[4]; };
+__device__ __forceinline__ void gemv_pro_load(const gemv_args & p, pro_regs & pr) {
+    const auto & r = p.pro;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    pr.s = r.sum[RSUM_STRIDE * lane];
+    const int b = 4 * wave + (lane >> 4);
+    const int64_t e0 = 256 * (int64_t) min(b, (int) (r.n / 256) - 1) + 16 * (lane & 15);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        pr.xv[k] = *(const float4 *) (r.x + e0 + 4 * k);
+        pr.wv[k] = r.w ? *(const float4 *) (r.w + e0 + 4 * k) : make_float4(1.f, 1.f, 1.f, 1.f);
+    }
+}
+__device__ __forceinline__ void gemv_pro_finish(const gemv_args & p, const pro_regs & pr, uint8_t * buf, gemv_act & A) {
+    const auto & r = p.pro;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int NB = (int) (r.n / 256);
+    const double s = wave_sum(pr.s);   // a fixed tree: the same s in every workgroup
+    float mean;
+    if (!rms_mean_decided(s, r.n, mean)) {   // uniform: every thread holds the same s
+        __shared__ float pmean;
+        if (tid == 0) pmean = rms_mean_sequential(r.x, nullptr, r.n);
+        __syncthreads();
+        mean = pmean;
+    }
+    const float scale = 1.0f / sqrtf(mean + r.eps);
+    int8_t * qs = (int8_t *) buf;
+    float * qd = (float *) (buf + r.n);
+    int16_t * qsum = (int16_t *) (buf + r.n + 4 * (r.qmode == 1 ? r.n / 256 : r.n / 32));
+    for (int b0 = 0; b0 < NB; b0 += 16) {
+        const int b = b0 + 4 * wave + (lane >> 4);
+        if (b >= NB) continue;   // whole rows of 16 lanes
+        const int64_t e0 = 256 * (int64_t) b + 16 * (lane & 15);
+        float4 xv[4], wv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (b0 == 0) {
+                xv[k] = pr.xv[k];
+                wv[k] = pr.wv[k];
+            } else {
+                xv[k] = *(const float4 *) (r.x + e0 + 4 * k);
+                wv[k] = r.w ? *(const float4 *) (r.w + e0 + 4 * k) : make_float4(1.f, 1.f, 1.f, 1.f);
+            }
+        }
+        float y[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float xx[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+            const float ww[4] = {wv[k].x, wv[k].y, wv[k].z, wv[k].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float yn = __fmul_rn(xx[c], scale);
+                y[4 * k + c] = r.w ? __fmul_rn(yn, ww[c]) : yn;
+            }
+        }
+        if (r.qmode == 1) q8K_row16(y, lane, qs + 256 * (int64_t) b, qsum + 16 * (int64_t) b, qd + b);
+        else q8_0_row16(y, lane, qs + 256 * (int64_t) b, qd + 8 * (int64_t) b, qsum + 8 * (int64_t) b);
+    }
+    __syncthreads();
+    A = {qs, qd, qsum};
+}
+
 // LDS bytes of the prologue's activation (gemv_act layout, 16-B aligned pieces)
 static inline uint32_t pro_lds_bytes(int64_t n, int qmode) {
     const int64_t nd = qmode == 1 ? n / 256 : n / 32, ns = qmode == 1 ? n / 16 : n / 32;
@@ -229,6 +296,17 @@ static constexpr size_t xrec_dwords(int rpg, int64_t nb) { return (size_t) 2 * r
 // The body runs as workgroup wg0 of nwg over the launch's ngroups row groups, so one launch can
 // hold two bodies of different weight types (k_gemv_pipe2).  MODE 0: plain stores; 1: row
 // values parked in LDS and the epilogues run after the loop on all threads.
+// the matrix of row group g as a wave-uniform (SGPR) index: kernel-argument arrays indexed by a
+// VGPR are read with vector loads from the kernarg segment, a memory round trip in front of the
+// first weight load of every workgroup (the one-shot gate/up launch ran 20.3 instead of 14.3 us)
+__device__ __forceinline__ int gemv_mat(const gemv_args & p, int64_t g) {
+    const int gi = __builtin_amdgcn_readfirstlane((int) g);
+    int mi = 0;
+#pragma unroll
+    for (int k = 1; k < GEMV_MAXMAT; ++k) mi += gi >= p.blk0[k] ? 1 : 0;
+    return __builtin_amdgcn_readfirstlane(mi);
+}
+
 template <class T, int R, int WPR, int MODE>
 __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_t ngroups, const int64_t wg0, const int64_t nwg,
                                                uint32_t * xr) {
@@ -243,9 +321,7 @@ __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_
     const int nb = p.ntasks / T::per_block;
     const int rowl0 = (wave / WPR) * R;    // this wave's first row within the group
     auto locate = [&](int64_t g, int & mi, int64_t & row0) {
-        mi = 0;
-#pragma unroll
-        for (int k = 1; k < GEMV_MAXMAT; ++k) mi += g >= p.blk0[k] ? 1 : 0;
+        mi = gemv_mat(p, g);
         row0 = (g - p.blk0[mi]) * RPG + rowl0;
     };
     auto fetch = [&](int64_t g, typename T::raw (&w)[R]) {
@@ -384,6 +460,156 @@ __global__ __launch_bounds__(256) void k_gemv_pipe2(const gemv_args p1, const in
     kt_exit(p1.kt);
 }
 
+// ---- one-shot body: one row group per workgroup, weights staged by LDS-DMA ----------------------
+// Each wave copies its R row slices (at most 64 tasks of a row: os_geo<T>::SEG bytes each) HBM ->
+// LDS with global_load_lds, 1 KiB of contiguous bytes per wave instruction, so every 128-B line
+// is requested once (the register fetch of a task's header + quants asks each line three
+// times), and no VGPR is held for bytes in flight; the dispatcher's workgroup turnover does the
+// pipelining.  The norm prologue's sources are loaded before the DMAs are issued, so waiting
+// for them leaves the weight stream in flight; a Q8 activation slice is loaded after them.
+// Records, walker and epilogues are the pipelined kernel's (the same bits).
+template <class T> struct os_geo {
+    static constexpr int SEG = (WAVE / T::per_block) * T::blk_bytes;   // a wave's row slice
+    static constexpr int NI = (SEG + 1023) / 1024;                        // DMA instructions per slice
+    static constexpr int SLICE = NI * 1024;                               // LDS bytes per slice
+};
+typedef __attribute__((address_space(3))) void * gemv_lds_t;
+
+template <class T, int R, int WPR, int MODE, bool PRO>
+__device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t g, uint8_t * wl, uint32_t * xr) {
+    constexpr int NWV = 4;
+    constexpr int NT = 64 * NWV;
+    constexpr int RPG = (NWV / WPR) * R;
+    using G = os_geo<T>;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wsub = wave % WPR;
+    const int t = wsub * WAVE + lane;
+    const bool active = t < p.ntasks;
+    const int tt = active ? t : 0;
+    const int nb = p.ntasks / T::per_block;
+    const int rowl0 = (wave / WPR) * R;
+    const int mi = gemv_mat(p, g);
+    const int64_t row0 = (g - p.blk0[mi]) * RPG + rowl0;
+    const int64_t M = p.M[mi];
+    // ---- activation sources first ----
+    pro_regs pr;
+    if constexpr (PRO) gemv_pro_load(p, pr);
+    const int wr = lane / T::LPR, ws = lane % T::LPR;
+    const int wrc = wr < R ? wr : 0;
+    float rc = 0.0f;
+    if (MODE == 0 && p.rres) rc = p.rres[min(row0 + wrc, p.M[0] - 1)];
+    // ---- weight DMA: this wave's R row slices -> its LDS region (nt: read once per token) ----
+    uint8_t * mine = wl + (size_t) wave * R * G::SLICE;
+    {
+        const int nt_w = min(WAVE, p.ntasks - WAVE * wsub);
+        const int seg = (nt_w / T::per_block) * T::blk_bytes;
+        const uint8_t * Wm = p.W[mi];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint8_t * src = Wm + min(row0 + r, M - 1) * p.nb01[mi] + (int64_t) wsub * G::SEG;
+#pragma unroll
+            for (int i = 0; i < G::NI; ++i) {
+                const int off = min(i * 1024 + 16 * lane, seg - 16);
+                __builtin_amdgcn_global_load_lds((const void *) (src + off), (gemv_lds_t) (mine + r * G::SLICE + i * 1024), 16, 0,
+                                                 MI_WNT ? 2 : 0);
+            }
+        }
+    }
+    // the activation slice after the DMAs: T::load computes on what it loads (bsum pairs, the
+    // Q6_K -32 sums), and a wait for a load issued BEFORE the DMAs would hold the DMA issue back
+    // by an L2 round trip (the one-shot kernel's rec stage took ~35 % longer that way)
+    typename T::act x;
+    if constexpr (PRO) {
+        gemv_act A = p.A;
+        gemv_pro_finish(p, pr, (uint8_t *) xr + p.pro.lds_off, A);
+        T::load(A, tt, x);
+    } else {
+        T::load(p.A, tt, x);
+    }
+    __shared__ float2 rtab[MODE ? GEMV_ROPE_MAXPAIRS : 1];
+    __shared__ uint16_t * f16p[2 * GEMV_MAXMAT];
+    if (MODE) {
+        if (threadIdx.x < 2 * GEMV_MAXMAT) {
+            const int m2 = threadIdx.x >> 1;
+            uint16_t * const * slot = (threadIdx.x & 1) ? p.rope_f16[m2] : p.f16out[m2];
+            f16p[threadIdx.x] = slot ? *slot : nullptr;
+        }
+        if (p.need_pairs) {
+            for (int ip = threadIdx.x; ip < p.rp.n_dims / 2; ip += NT) rtab[ip] = p.rtab_g[ip];
+        }
+    }
+    // ---- this wave's weights are in LDS (the issuing wave's vmcnt covers its own DMAs) ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t * xb = xr;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        typename T::raw w;
+        T::template fetch<typename lds_loader<T>::type>(mine + r * G::SLICE - (int64_t) wsub * G::SEG, tt, w);
+        T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * nb * T::RS);
+    }
+    if constexpr (WPR > 1 || MODE != 0) __syncthreads();
+    else wave_lds_sync();
+    __shared__ float res[MODE ? RPG : 1];
+    if (wsub == 0) {
+        const float v = T::walk(xb + (size_t) (rowl0 + wrc) * nb * T::RS, nb, ws);
+        if (wr < R && ws == 0) {
+            if constexpr (MODE == 0) {
+                if (row0 + wr < M) {
+                    if (p.rres) {   // ADD(v, res): the CPU's single f32 add
+                        const float xv = __fadd_rn(v, rc);
+                        p.rxsum[row0 + wr] = xv;
+                        rc = xv;
+                    } else {
+                        p.dst[mi][row0 + wr] = v;
+                    }
+                }
+            } else {
+                res[rowl0 + wr] = v;
+            }
+        }
+    }
+    if constexpr (MODE == 0) {
+        if (p.rres) {
+            // this workgroup's rows' sum of squares (walker lanes hold x) to its shard (no-return atomic)
+            __shared__ double rpart[RPG];
+            if (wsub == 0 && wr < R && ws == 0) rpart[rowl0 + wr] = row0 + wr < M ? (double) __fmul_rn(rc, rc) : 0.0;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                double tot = 0.0;
+#pragma unroll
+                for (int k = 0; k < RPG; ++k) tot = __dadd_rn(tot, rpart[k]);
+                __hip_atomic_fetch_add(p.rsum + RSUM_STRIDE * (g % RSUM_SHARDS), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if constexpr (MODE >= 1) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < RPG; i += NT) {
+            const int64_t row = (g - p.blk0[mi]) * RPG + i;
+            // rope partner row ^ 1 lies in the same group (RPG is even whenever rope is fused)
+            if (row < M) gemv_store(p, mi, M, row, res[i], res[RPG > 1 ? i ^ 1 : i], rtab, f16p);
+        }
+    }
+}
+
+template <class T, int R, int WPR, int MODE, bool PRO>
+__global__ __launch_bounds__(256) void k_gemv_os(const gemv_args p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
+    kt_enter(p.kt);
+    // dynamic LDS: [records RPG x nb x RS dwords | prologue activation | weight slices]
+    gemv_os_body<T, R, WPR, MODE, PRO>(p, blockIdx.x, (uint8_t *) xr + p.wl_off, xr);
+    kt_exit(p.kt);
+}
+
+template <class T1, class T2, int R2, int WPR, bool PRO>
+__global__ __launch_bounds__(256) void k_gemv_os2(const gemv_args p1, const int64_t ng1, const gemv_args p2) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
+    kt_enter(p1.kt);
+    if ((int64_t) blockIdx.x < ng1) gemv_os_body<T1, 2, WPR, 1, PRO>(p1, blockIdx.x, (uint8_t *) xr + p1.wl_off, xr);
+    else gemv_os_body<T2, R2, WPR, 1, PRO>(p2, (int64_t) blockIdx.x - ng1, (uint8_t *) xr + p2.wl_off, xr);
+    kt_exit(p1.kt);
+}
+
 
 // ---- host ----------------------------------------------------------------------------------------
 // kernel-timing mode: the GEMV kernel itself is launched with start/stop events
@@ -476,8 +702,117 @@ static void launch_pipe(hipStream_t st, gemv_args & a, int nmat) {
 
 static int wpr_of(int ntasks) { return ntasks <= WAVE ? 1 : (ntasks <= 2 * WAVE ? 2 : 4); }
 
+// ---- one-shot launches (k_gemv_os): one row group per workgroup ---------------------------------
+// GGML_MI355X_GEMV_OS=0 keeps the persistent pipelined kernel (A/B only)
+static bool os_enabled() {
+    static const bool on = !getenv("GGML_MI355X_GEMV_OS") || atoi(getenv("GGML_MI355X_GEMV_OS")) != 0;
+    return on;
+}
+
+static inline size_t r16(size_t x) { return (x + 15) / 16 * 16; }
+
+// LDS-DMA moves 16-B pieces: every row slice must start 16-B aligned and end on a 16-B boundary
+template <class T>
+static bool os_aligned(const gemv_args & a, int nmat) {
+    const int wpr = a.ntasks <= WAVE ? 1 : (a.ntasks <= 2 * WAVE ? 2 : 4);
+    const int nt_last = a.ntasks - WAVE * (wpr - 1);
+    if ((os_geo<T>::SEG % 16) != 0 || ((nt_last / T::per_block) * T::blk_bytes) % 16 != 0) return false;
+    for (int i = 0; i < nmat; ++i) {
+        if (((uintptr_t) a.W[i] % 16) != 0 || (a.nb01[i] % 16) != 0) return false;
+    }
+    return true;
+}
+
+template <class T, int R, int WPR>
+static size_t os_lds_layout(gemv_args & a) {
+    constexpr int RPG = (4 / WPR) * R;
+    size_t off = r16((size_t) RPG * (a.ntasks / T::per_block) * T::RS * 4);
+    if (a.pro.x) {
+        a.pro.lds_off = (uint32_t) off;
+        off = r16(off + pro_lds_bytes(a.pro.n, a.pro.qmode));
+    }
+    a.wl_off = (uint32_t) off;
+    return off + (size_t) 4 * R * os_geo<T>::SLICE;
+}
+
+static const char * gemv_kt_name(const gemv_args & a, int mode) {
+    static const char * names[16] = {"gemv", "gemv+pro", "gemv+epi", "gemv+pro+epi", "gemv+tail", "gemv+pro+tail",
+                                     "gemv+epi+tail", "gemv+pro+epi+tail", "gemv+resid", "gemv+pro+resid",
+                                     "gemv+epi+resid", "gemv+pro+epi+resid", "gemv+tail+resid", "gemv+pro+tail+resid",
+                                     "gemv+epi+tail+resid", "gemv+all"};
+    return names[(a.pro.x ? 1 : 0) | (mode ? 2 : 0) | (a.tl.kind ? 4 : 0) | (a.rres ? 8 : 0)];
+}
+
+template <class T, int R, int WPR, int MODE>
+static void launch_os_m(hipStream_t st, gemv_args & a, int nmat) {
+    constexpr int RPG = (4 / WPR) * R;
+    const int64_t ng = set_groups(a, nmat, RPG);
+    const size_t lds = os_lds_layout<T, R, WPR>(a);
+    a.kt = g_kt_ctx ? g_kt_ctx->kt_take(gemv_kt_name(a, MODE), (unsigned) ng, 256) : nullptr;
+#define OS_LAUNCH(P)                                                                                              \
+    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P>), dim3((unsigned) ng), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a); \
+    else hipLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P>), dim3((unsigned) ng), dim3(256), lds, st, a)
+    if (a.pro.x) { OS_LAUNCH(true); } else { OS_LAUNCH(false); }
+#undef OS_LAUNCH
+}
+
+template <class T, int R, int WPR>
+static void launch_os(hipStream_t st, gemv_args & a, int nmat) {
+    if (needs_epilogue(a, nmat)) launch_os_m<T, R, WPR, 1>(st, a, nmat);
+    else launch_os_m<T, R, WPR, 0>(st, a, nmat);
+}
+
+// rows per wave of the one-shot kernel (tools/gemv_lab.hip, round 3): one row, except two for
+// the 4-bit K-quants at K = 14336 and wherever a norm prologue is formed per workgroup (half
+// the workgroups form it)
+template <class T>
+static bool launch_os_t(hipStream_t st, gemv_args & a, int nmat) {
+    if (!os_enabled() || a.tl.kind || !os_aligned<T>(a, nmat)) return false;
+    const int wpr = wpr_of(a.ntasks);
+    int R = 1;
+    if (a.pro.x || (wpr == 4 && !std::is_same<T, g_q6_K>::value)) R = 2;
+    if (wpr == 4 && needs_epilogue(a, nmat)) return false;   // rope pairs need an even group
+    gemv_args b = a;
+    const size_t lds = R == 2 ? (wpr == 1 ? os_lds_layout<T, 2, 1>(b) : wpr == 2 ? os_lds_layout<T, 2, 2>(b) : os_lds_layout<T, 2, 4>(b))
+                              : (wpr == 1 ? os_lds_layout<T, 1, 1>(b) : wpr == 2 ? os_lds_layout<T, 1, 2>(b) : os_lds_layout<T, 1, 4>(b));
+    if (lds > 64 * 1024) return false;
+    switch (R * 8 + wpr) {
+        case 2 * 8 + 1: launch_os<T, 2, 1>(st, a, nmat); break;
+        case 2 * 8 + 2: launch_os<T, 2, 2>(st, a, nmat); break;
+        case 2 * 8 + 4: launch_os<T, 2, 4>(st, a, nmat); break;
+        case 1 * 8 + 1: launch_os<T, 1, 1>(st, a, nmat); break;
+        case 1 * 8 + 2: launch_os<T, 1, 2>(st, a, nmat); break;
+        default:        launch_os<T, 1, 4>(st, a, nmat); break;
+    }
+    return true;
+}
+
+// two weight types in one one-shot launch: p1's matrices at two rows per wave, p2's at R2
+template <class T1, class T2, int R2, int WPR>
+static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2, int n2) {
+    constexpr int NWV = 4;
+    const int64_t ng1 = set_groups(a1, n1, (NWV / WPR) * 2), ng2 = set_groups(a2, n2, (NWV / WPR) * R2);
+    size_t rec = r16(std::max((size_t) (NWV / WPR) * 2 * (a1.ntasks / T1::per_block) * T1::RS * 4,
+                              (size_t) (NWV / WPR) * R2 * (a2.ntasks / T2::per_block) * T2::RS * 4));
+    size_t off = rec;
+    if (a1.pro.x) {
+        a1.pro.lds_off = a2.pro.lds_off = (uint32_t) off;
+        off = r16(off + pro_lds_bytes(a1.pro.n, a1.pro.qmode));
+    }
+    a1.wl_off = a2.wl_off = (uint32_t) off;
+    const size_t lds = off + std::max((size_t) 4 * 2 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
+    a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv2+pro+epi", (unsigned) (ng1 + ng2), 64 * NWV) : nullptr;
+#define OS2_LAUNCH(P)                                                                                                 \
+    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P>), dim3((unsigned) (ng1 + ng2)), dim3(64 * NWV), lds, st, t_ev_beg, \
+                                        t_ev_end, 0, a1, ng1, a2);                                                        \
+    else hipLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P>), dim3((unsigned) (ng1 + ng2)), dim3(64 * NWV), lds, st, a1, ng1, a2)
+    if (a1.pro.x) { OS2_LAUNCH(true); } else { OS2_LAUNCH(false); }
+#undef OS2_LAUNCH
+}
+
 template <class T>
 static void launch_t(hipStream_t st, gemv_args & a, int nmat) {
+    if (launch_os_t<T>(st, a, nmat)) return;
     int64_t Mt = 0;
     for (int i = 0; i < nmat; ++i) Mt += a.M[i];
     GGML_ASSERT(a.ntasks <= 4 * WAVE);
@@ -536,6 +871,13 @@ static bool launch_pipe2_t(hipStream_t st, gemv_args & a1, int n1, gemv_args & a
     int64_t m1 = 0, m2 = 0;
     for (int i = 0; i < n1; ++i) m1 += a1.M[i];
     for (int i = 0; i < n2; ++i) m2 += a2.M[i];
+    if (os_enabled() && os_aligned<T1>(a1, n1) && os_aligned<T2>(a2, n2)) {
+        // one-shot: the second type at one row per wave (two rows for the prologue consumers)
+        if (wpr == 1 && a1.pro.x) launch_os2_v<T1, T2, 2, 1>(st, a1, n1, a2, n2);
+        else if (wpr == 1) launch_os2_v<T1, T2, 1, 1>(st, a1, n1, a2, n2);
+        else launch_os2_v<T1, T2, 1, 2>(st, a1, n1, a2, n2);
+        return true;
+    }
     // the single-type launch's rows-per-wave rule (launch_t), per part
     if (ceil_div(m1 * wpr, 8) < 256) return false;
     const int r2 = ceil_div(m2 * wpr, 8) < 256 ? 1 : 2;

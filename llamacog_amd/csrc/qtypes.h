@@ -32,6 +32,10 @@
 namespace mi355x {
 
 __device__ __forceinline__ float asf(uint32_t u) { return __uint_as_float(u); }
+// a * b for operands that fit 24 signed bits (6-bit / int8 scales times block dot products, at
+// most 16 * 63 * 127 in magnitude): v_mul_i32_i24 / v_mad_i32_i24 run at full rate where the
+// generic 32-bit v_mul_lo_u32 is quarter rate (15 of them per Q6_K task dominated its rec)
+__device__ __forceinline__ int m24(int a, int b) { return __mul24(a, b); }
 __device__ __forceinline__ uint32_t asu(float f) { return __float_as_uint(f); }
 
 // hsum_float_8 over the 8 lanes s = 0..7 of a class group (lane s holds acc[s]); every lane of
@@ -93,6 +97,41 @@ __device__ __forceinline__ uint2 wld8(const uint8_t * p) { return ld8(p); }
 __device__ __forceinline__ uint32_t wld2(const uint8_t * p) { return ld2(p); }
 #endif
 
+// where a task's weight bytes come from: HBM (non-temporal, streamed once) or the LDS copy the
+// one-shot GEMV's LDS-DMA staged (k_gemv.hip); the byte offsets are the same either way
+struct ld_glb {
+    __device__ static uint4 l16(const uint8_t * p) { return wld16(p); }
+    __device__ static uint2 l8(const uint8_t * p) { return wld8(p); }
+    __device__ static uint32_t l2(const uint8_t * p) { return wld2(p); }
+};
+struct ld_lds {
+    __device__ static uint4 l16(const uint8_t * p) { return ld16(p); }
+    __device__ static uint2 l8(const uint8_t * p) { return ld8(p); }
+    __device__ static uint32_t l2(const uint8_t * p) { return ld2(p); }
+};
+// the same from LDS when a block may start 2 bytes off a dword (Q6_K 210-B, Q8_0 34-B, Q4_0
+// 18-B blocks): dword-aligned reads re-aligned by v_alignbyte.  Misaligned ds_reads are split
+// by the LDS unit; on the 6-bit K-quant they made the one-shot GEMV's record stage cost as much
+// as its weight stream (output head 63 -> 105 us, tools/gemv_lab.hip LAB_EXACT)
+struct ld_lds_u {
+    __device__ static uint32_t al(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
+    __device__ static uint4 l16(const uint8_t * p) {
+        const uint32_t s = (uint32_t) (uintptr_t) p & 3;
+        const uint32_t * q = (const uint32_t *) (p - s);
+        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3], w4 = q[4];
+        return make_uint4(al(w1, w0, s), al(w2, w1, s), al(w3, w2, s), al(w4, w3, s));
+    }
+    __device__ static uint2 l8(const uint8_t * p) {
+        const uint32_t s = (uint32_t) (uintptr_t) p & 3;
+        const uint32_t * q = (const uint32_t *) (p - s);
+        const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+        return make_uint2(al(w1, w0, s), al(w2, w1, s));
+    }
+    __device__ static uint32_t l2(const uint8_t * p) { return ld2(p); }
+};
+// the LDS loader for a weight type: plain where every block starts 16-B aligned
+template <class T> struct lds_loader { using type = typename std::conditional<T::blk_bytes % 16 == 0, ld_lds, ld_lds_u>::type; };
+
 // the Q8_K / Q8_0 activation (quant_act.h layout): qs, d, and the 16-sums (Q8_K) / 32-sums (Q8_0)
 struct gemv_act { const int8_t * qs; const float * d; const int16_t * s; };
 
@@ -114,12 +153,13 @@ __device__ __forceinline__ void k4_load(const gemv_act & A, int t, k4_act & x) {
 }
 
 struct q4k_raw { uint4 hdr, qa, qb; };
+template <class L = ld_glb>
 __device__ __forceinline__ void q4k_fetch(const uint8_t * wrow, int t, q4k_raw & w) {
     const int b = t >> 2, j = t & 3;
     const uint8_t * blk = wrow + (int64_t) b * 144;
-    w.hdr = wld16(blk);
-    w.qa  = wld16(blk + 16 + 32 * j);
-    w.qb  = wld16(blk + 32 + 32 * j);
+    w.hdr = L::l16(blk);
+    w.qa  = L::l16(blk + 16 + 32 * j);
+    w.qb  = L::l16(blk + 32 + 32 * j);
 }
 // sumi = sc_lo·<q_lo, y> + sc_hi·<q_hi, y> and the pair's min integer
 __device__ __forceinline__ void q4k_ints(const q4k_raw & w, int t, const k4_act & x, int & sumi, int & summ) {
@@ -133,8 +173,8 @@ __device__ __forceinline__ void q4k_ints(const q4k_raw & w, int t, const k4_act 
         dl = dot4((int) (q[i] & 0x0f0f0f0f), x.a[i], dl);
         dh = dot4((int) ((q[i] >> 4) & 0x0f0f0f0f), x.a[8 + i], dh);
     }
-    sumi = sc_lo * dl + sc_hi * dh;
-    summ = m_lo * x.bs0 + m_hi * x.bs1;
+    sumi = m24(sc_lo, dl) + m24(sc_hi, dh);
+    summ = m24(m_lo, x.bs0) + m24(m_hi, x.bs1);
 }
 
 // Q4_K, repacked gemv order R1.  Record: I, Imin, d·dy, dmin·dy (the quad of a block reduced by
@@ -144,7 +184,7 @@ struct g_q4_K {
     using act = k4_act;
     using raw = q4k_raw;
     __device__ static void load(const gemv_act & A, int t, act & x) { k4_load(A, t, x); }
-    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) { q4k_fetch(wrow, t, w); }
+    template <class L = ld_glb> __device__ static void fetch(const uint8_t * wrow, int t, raw & w) { q4k_fetch<L>(wrow, t, w); }
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         int sumi, summ;
         q4k_ints(w, t, x, sumi, summ);
@@ -175,7 +215,7 @@ struct g_q4_K_p {
     using act = k4_act;
     using raw = q4k_raw;
     __device__ static void load(const gemv_act & A, int t, act & x) { k4_load(A, t, x); }
-    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) { q4k_fetch(wrow, t, w); }
+    template <class L = ld_glb> __device__ static void fetch(const uint8_t * wrow, int t, raw & w) { q4k_fetch<L>(wrow, t, w); }
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         int sumi, summ;
         q4k_ints(w, t, x, sumi, summ);
@@ -218,11 +258,11 @@ struct g_q4_K_p {
 // acc_m[k]) with P[k] the mins of pair k; hsum8(acc) + ((m0+m2)+(m1+m3)).
 // Record: cls[8], P[4], dy·d, -dy·dmin.
 struct g_q4_K_c {
-    static constexpr int per_block = 4, blk_bytes = 144, RS = 14, LPR = 8;
+    static constexpr int per_block = 4, blk_bytes = 144, RS = 16, LPR = 8;   // 16-B aligned records
     using act = k4_act;
     using raw = q4k_raw;
     __device__ static void load(const gemv_act & A, int t, act & x) { k4_load(A, t, x); }
-    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) { q4k_fetch(wrow, t, w); }
+    template <class L = ld_glb> __device__ static void fetch(const uint8_t * wrow, int t, raw & w) { q4k_fetch<L>(wrow, t, w); }
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         const int j = t & 3;
         int sc_lo, sc_hi, m_lo, m_hi;
@@ -231,18 +271,17 @@ struct g_q4_K_c {
         int c[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            c[i] = sc_lo * dot4((int) (q[i] & 0x0f0f0f0f), x.a[i], 0) + sc_hi * dot4((int) ((q[i] >> 4) & 0x0f0f0f0f), x.a[8 + i], 0);
+            c[i] = m24(sc_lo, dot4((int) (q[i] & 0x0f0f0f0f), x.a[i], 0)) + m24(sc_hi, dot4((int) ((q[i] >> 4) & 0x0f0f0f0f), x.a[8 + i], 0));
             if (!active) c[i] = 0;
             c[i] = quad_sum(c[i]);
         }
         if (!active) return;
         uint32_t * r = rr + (t >> 2) * RS;
-        r[8 + j] = (uint32_t) (m_lo * x.bs0 + m_hi * x.bs1);
+        r[8 + j] = (uint32_t) (m24(m_lo, x.bs0) + m24(m_hi, x.bs1));
         if (j == 0) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) r[i] = (uint32_t) c[i];
-            r[12] = asu(x.dy * h2f(w.hdr.x & 0xffff));
-            r[13] = asu(-x.dy * h2f(w.hdr.x >> 16));
+            *(uint4 *) r = make_uint4((uint32_t) c[0], (uint32_t) c[1], (uint32_t) c[2], (uint32_t) c[3]);
+            *(uint4 *) (r + 4) = make_uint4((uint32_t) c[4], (uint32_t) c[5], (uint32_t) c[6], (uint32_t) c[7]);
+            *(uint2 *) (r + 12) = make_uint2(asu(x.dy * h2f(w.hdr.x & 0xffff)), asu(-x.dy * h2f(w.hdr.x >> 16)));
         }
     }
     __device__ static float walk(const uint32_t * rr, int nb, int s) {
@@ -258,18 +297,18 @@ struct g_q4_K_c {
 // Q5_K, vec_dot order (arch/x86/quants.c:2062): acc[c] = fma(dy·d, cls[c], acc[c]);
 // summs = fma(Imin, -dy·dmin, summs); hsum8(acc) + summs.  Record: cls[8], Imin, dy·d, -dy·dmin.
 struct g_q5_K {
-    static constexpr int per_block = 4, blk_bytes = 176, RS = 11, LPR = 8;
+    static constexpr int per_block = 4, blk_bytes = 176, RS = 12, LPR = 8;   // 16-B aligned records
     using act = k4_act;
     struct raw { uint4 hdr, ha, hb, qa, qb; };
     __device__ static void load(const gemv_act & A, int t, act & x) { k4_load(A, t, x); }
-    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+    template <class L = ld_glb> __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const int b = t >> 2, j = t & 3;
         const uint8_t * blk = wrow + (int64_t) b * 176;
-        w.hdr = wld16(blk);
-        w.ha  = wld16(blk + 16);
-        w.hb  = wld16(blk + 32);
-        w.qa  = wld16(blk + 48 + 32 * j);
-        w.qb  = wld16(blk + 64 + 32 * j);
+        w.hdr = L::l16(blk);
+        w.ha  = L::l16(blk + 16);
+        w.hb  = L::l16(blk + 32);
+        w.qa  = L::l16(blk + 48 + 32 * j);
+        w.qb  = L::l16(blk + 64 + 32 * j);
     }
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         const int j = t & 3;
@@ -282,19 +321,17 @@ struct g_q5_K {
         for (int i = 0; i < 8; ++i) {
             const uint32_t lo = (q[i] & 0x0f0f0f0f) | (((qh[i] >> (2 * j)) & 0x01010101) << 4);
             const uint32_t hi = ((q[i] >> 4) & 0x0f0f0f0f) | (((qh[i] >> (2 * j + 1)) & 0x01010101) << 4);
-            c[i] = sc_lo * dot4((int) lo, x.a[i], 0) + sc_hi * dot4((int) hi, x.a[8 + i], 0);
+            c[i] = m24(sc_lo, dot4((int) lo, x.a[i], 0)) + m24(sc_hi, dot4((int) hi, x.a[8 + i], 0));
             if (!active) c[i] = 0;
             c[i] = quad_sum(c[i]);
         }
-        int mn = active ? m_lo * x.bs0 + m_hi * x.bs1 : 0;
+        int mn = active ? m24(m_lo, x.bs0) + m24(m_hi, x.bs1) : 0;
         mn = quad_sum(mn);
         if (active && j == 0) {
             uint32_t * r = rr + (t >> 2) * RS;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) r[i] = (uint32_t) c[i];
-            r[8] = (uint32_t) mn;
-            r[9] = asu(x.dy * h2f(w.hdr.x & 0xffff));
-            r[10] = asu(-x.dy * h2f(w.hdr.x >> 16));
+            *(uint4 *) r = make_uint4((uint32_t) c[0], (uint32_t) c[1], (uint32_t) c[2], (uint32_t) c[3]);
+            *(uint4 *) (r + 4) = make_uint4((uint32_t) c[4], (uint32_t) c[5], (uint32_t) c[6], (uint32_t) c[7]);
+            *(uint4 *) (r + 8) = make_uint4((uint32_t) mn, asu(x.dy * h2f(w.hdr.x & 0xffff)), asu(-x.dy * h2f(w.hdr.x >> 16)), 0u);
         }
     }
     __device__ static float walk(const uint32_t * rr, int nb, int s) {
@@ -309,7 +346,9 @@ struct g_q5_K {
 // 256b + 128h + 32g + 16lr; its dot4 pieces i = 0..3 are classes 4lr + i.  The activation carries
 // -32·(sum of each 4-byte piece), so dot4(q6, y, -32Σy) = <q6 - 32, y>.  Record: cls[8], dy·d.
 struct g_q6_K {
-    static constexpr int per_block = 4, blk_bytes = 210, RS = 9, LPR = 8;
+    // RS = 12 (not 9): a record starts 16-B aligned, so its uint4 stores are single aligned
+    // ds_write_b128s (a 36-B stride split them; the one-shot GEMV's rec stage ran 1.8x longer)
+    static constexpr int per_block = 4, blk_bytes = 210, RS = 12, LPR = 8;
     struct act { int4 a0, a1, a2, a3; int4 n0, n1, n2, n3; float dy; };
     __device__ static void load(const gemv_act & A, int t, act & x) {
         const int b = t >> 2, h = (t >> 1) & 1, lr = t & 1;
@@ -326,14 +365,14 @@ struct g_q6_K {
         x.dy = A.d[b];
     }
     struct raw { uint4 la, lb, hh; uint2 sc8; uint32_t d16; };
-    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+    template <class L = ld_glb> __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const int b = t >> 2, h = (t >> 1) & 1, lr = t & 1;
         const uint8_t * blk = wrow + (int64_t) b * 210;
-        w.la = wld16(blk + 64 * h + 16 * lr);
-        w.lb = wld16(blk + 64 * h + 32 + 16 * lr);
-        w.hh = wld16(blk + 128 + 32 * h + 16 * lr);
-        w.sc8 = wld8(blk + 192 + 8 * h);
-        w.d16 = wld2(blk + 208);
+        w.la = L::l16(blk + 64 * h + 16 * lr);
+        w.lb = L::l16(blk + 64 * h + 32 + 16 * lr);
+        w.hh = L::l16(blk + 128 + 32 * h + 16 * lr);
+        w.sc8 = L::l8(blk + 192 + 8 * h);
+        w.d16 = L::l2(blk + 208);
     }
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         const int lr = t & 1;
@@ -355,7 +394,7 @@ struct g_q6_K {
             const int s1 = dot4((int) ((M[i] & 0x0f0f0f0f)        | (((H[i] >> 2) & 0x03030303) << 4)), A1[i], N1[i]);
             const int s2 = dot4((int) (((L[i] >> 4) & 0x0f0f0f0f) | (((H[i] >> 4) & 0x03030303) << 4)), A2[i], N2[i]);
             const int s3 = dot4((int) (((M[i] >> 4) & 0x0f0f0f0f) | (((H[i] >> 6) & 0x03030303) << 4)), A3[i], N3[i]);
-            c[i] = active ? sc0 * s0 + sc1 * s1 + sc2 * s2 + sc3 * s3 : 0;
+            c[i] = active ? m24(sc0, s0) + m24(sc1, s1) + m24(sc2, s2) + m24(sc3, s3) : 0;
             c[i] += dpp<DPP_XOR2>(c[i]);   // the other half h of the block
         }
         if (active && (t & 2) == 0) {
@@ -371,7 +410,7 @@ struct g_q6_K {
 // the same for batches).  Task = one 32-block; its eight dot4 are the eight classes.
 // Record: cls[8], dx·dy.
 struct g_q8_0 {
-    static constexpr int per_block = 1, blk_bytes = 34, RS = 9, LPR = 8;
+    static constexpr int per_block = 1, blk_bytes = 34, RS = 12, LPR = 8;   // 16-B aligned records
     struct act { int4 a0, a1; float dy; };
     __device__ static void load(const gemv_act & A, int t, act & x) {
         const int4 * ap = (const int4 *) (A.qs + (int64_t) t * 32);
@@ -379,11 +418,11 @@ struct g_q8_0 {
         x.dy = A.d[t];
     }
     struct raw { uint4 qa, qb; uint32_t d16; };
-    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+    template <class L = ld_glb> __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const uint8_t * blk = wrow + (int64_t) t * 34;
-        w.d16 = wld2(blk);
-        w.qa = wld16(blk + 2);
-        w.qb = wld16(blk + 18);
+        w.d16 = L::l2(blk);
+        w.qa = L::l16(blk + 2);
+        w.qb = L::l16(blk + 18);
     }
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         if (!active) return;
@@ -392,7 +431,7 @@ struct g_q8_0 {
                                   (uint32_t) dot4(w.qa.z, x.a0.z, 0), (uint32_t) dot4(w.qa.w, x.a0.w, 0));
         *(uint4 *) (r + 4) = make_uint4((uint32_t) dot4(w.qb.x, x.a1.x, 0), (uint32_t) dot4(w.qb.y, x.a1.y, 0),
                                         (uint32_t) dot4(w.qb.z, x.a1.z, 0), (uint32_t) dot4(w.qb.w, x.a1.w, 0));
-        r[8] = asu(h2f((uint16_t) w.d16) * x.dy);
+        *(uint4 *) (r + 8) = make_uint4(asu(h2f((uint16_t) w.d16) * x.dy), 0u, 0u, 0u);
     }
     __device__ static float walk(const uint32_t * rr, int nb, int s) { return hsum8_lanes(class_chain(rr, nb, RS, 8, s)); }
 };
@@ -409,10 +448,10 @@ struct g_q4_0 {
         x.dy = A.d[t];
     }
     struct raw { uint4 q; uint32_t d16; };
-    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
+    template <class L = ld_glb> __device__ static void fetch(const uint8_t * wrow, int t, raw & w) {
         const uint8_t * blk = wrow + (int64_t) t * 18;
-        w.d16 = wld2(blk);
-        w.q = wld16(blk + 2);
+        w.d16 = L::l2(blk);
+        w.q = L::l16(blk + 2);
     }
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         if (!active) return;
@@ -440,11 +479,11 @@ struct g_q4_0 {
 // Q4_0 in the vec_dot order (M % 8 != 0, arch/x86/quants.c:531): classes j/4 (low nibbles,
 // elements j < 16) and 4 + j/4 (high nibbles).  Record: cls[8], dx·dy.
 struct g_q4_0_c {
-    static constexpr int per_block = 1, blk_bytes = 18, RS = 9, LPR = 8;
+    static constexpr int per_block = 1, blk_bytes = 18, RS = 12, LPR = 8;   // 16-B aligned records
     using act = g_q8_0::act;
     using raw = g_q4_0::raw;
     __device__ static void load(const gemv_act & A, int t, act & x) { g_q8_0::load(A, t, x); }
-    __device__ static void fetch(const uint8_t * wrow, int t, raw & w) { g_q4_0::fetch(wrow, t, w); }
+    template <class L = ld_glb> __device__ static void fetch(const uint8_t * wrow, int t, raw & w) { g_q4_0::template fetch<L>(wrow, t, w); }
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         if (!active) return;
         const uint32_t q[4] = {w.q.x, w.q.y, w.q.z, w.q.w};
@@ -452,13 +491,16 @@ struct g_q4_0_c {
         const int ah[4] = {x.a1.x, x.a1.y, x.a1.z, x.a1.w};
         const int m8 = 0x08080808;
         uint32_t * r = rr + t * RS;
+        uint32_t lo[4], hi[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             // <q - 8, y> = <q, y> - <8, y>
-            r[i] = (uint32_t) (dot4((int) (q[i] & 0x0f0f0f0f), al[i], 0) - dot4(m8, al[i], 0));
-            r[4 + i] = (uint32_t) (dot4((int) ((q[i] >> 4) & 0x0f0f0f0f), ah[i], 0) - dot4(m8, ah[i], 0));
+            lo[i] = (uint32_t) (dot4((int) (q[i] & 0x0f0f0f0f), al[i], 0) - dot4(m8, al[i], 0));
+            hi[i] = (uint32_t) (dot4((int) ((q[i] >> 4) & 0x0f0f0f0f), ah[i], 0) - dot4(m8, ah[i], 0));
         }
-        r[8] = asu(h2f((uint16_t) w.d16) * x.dy);
+        *(uint4 *) r = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+        *(uint4 *) (r + 4) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+        *(uint4 *) (r + 8) = make_uint4(asu(h2f((uint16_t) w.d16) * x.dy), 0u, 0u, 0u);
     }
     __device__ static float walk(const uint32_t * rr, int nb, int s) { return hsum8_lanes(class_chain(rr, nb, RS, 8, s)); }
 };

@@ -202,6 +202,28 @@ def test_mul_mat_prefill_bit_exact(K, name, Kd, M):
         assert_bits(K.mul_mat(t, wq, Kd, M, x), O.mul_mat_cpu(t, wq, Kd, M, x), f"{name} {Kd}x{M} T={T}")
 
 
+@pytest.mark.parametrize("name,Kd,M", [("q4_K", 4096, 14336), ("q6_K", 14336, 4096), ("q4_K", 14336, 4096),
+                                        ("q4_K", 8192, 28672), ("q6_K", 28672, 8192)])
+def test_mul_mat_prefill_full_llama_shapes_t512(K, name, Kd, M):
+    """pp512's own launches at full Llama-3-8B / 70B matrix sizes (FFN gate/up 4096 x 14336, down
+    14336 x 4096 in Q4_K and Q6_K, the 70B 8192 x 28672 and 28672 x 8192): the GPU computes every
+    row for T = 512; the oracle checks the first 64, the last 64 and 16 groups of 8 spread between
+    (rows are independent, so a row's bits do not depend on which others are computed)."""
+    from llamacog_amd import gguf_synth as gs
+    t = CPU_TYPES[name]
+    rng = np.random.default_rng(Kd + M)
+    blk, bs = gs.BLOCK[t]
+    wq = gs.make_blocks(t, M * Kd // blk, rng).reshape(M, -1)
+    T = 512
+    x = rng.standard_normal((T, Kd)).astype(np.float32)
+    y = K.mul_mat(t, wq, Kd, M, x)
+    rows = np.unique(np.concatenate([np.arange(64), np.arange(M - 64, M), rng.choice(M, 16, replace=False)]))
+    # the repacked-Q4_K order needs whole groups of 8 rows: check the 8-row groups holding them
+    rows = np.unique((rows[:, None] // 8 * 8 + np.arange(8)[None, :]).reshape(-1))
+    ref = O.mul_mat_cpu(t, np.ascontiguousarray(wq[rows]), Kd, len(rows), x)
+    assert_bits(np.ascontiguousarray(y[:, rows]), ref, f"{name} {Kd}x{M} T={T} (rows {len(rows)})")
+
+
 MOE_TYPES = {"q4_K": O.Q4_K, "q5_K": O.Q5_K, "q6_K": O.Q6_K, "q8_0": O.Q8_0, "q4_0": O.Q4_0}
 
 
