@@ -507,8 +507,8 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
     ggml_tensor Q, K, V, Mk, O, X, R, A, N, Wt, Mu;
     unsigned long long * prof = nullptr;
     if (which == 2) {
-        MI_CHECK(hipMalloc(&prof, 6 * sizeof(unsigned long long)));
-        MI_CHECK(hipMemset(prof, 0, 6 * sizeof(unsigned long long)));
+        MI_CHECK(hipMalloc(&prof, 8 * sizeof(unsigned long long)));
+        MI_CHECK(hipMemset(prof, 0, 8 * sizeof(unsigned long long)));
         g_fa_prof = prof;
         which = 0;
     }
@@ -584,8 +584,8 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
         memcpy(O.op_params + 1, &zero, 4);
         memcpy(O.op_params + 2, &zero, 4);
         if (b) {
-            MI_CHECK(hipMalloc(&prof, 6 * sizeof(unsigned long long)));
-            MI_CHECK(hipMemset(prof, 0, 6 * sizeof(unsigned long long)));
+            MI_CHECK(hipMalloc(&prof, 8 * sizeof(unsigned long long)));
+            MI_CHECK(hipMemset(prof, 0, 8 * sizeof(unsigned long long)));
             g_fa_prof = prof;
         }
         run = [&] { op_flash_attn(sc.ex, &O); };
@@ -666,13 +666,15 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
         if (err != hipSuccess) fprintf(stderr, "mi355x_bench_op %d: %s\n", which, hipGetErrorString(err));
     }
     if (prof) {
-        unsigned long long h[6];
+        unsigned long long h[8];
         MI_CHECK(hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost));
-        const char * nm[6] = {"A(mask)", "0(V issue)", "1(scores)", "2(softmax coef)", "3(wait V)", "3(recurrence)"};
-        const char * nmp[6] = {"barrier+wait", "1(scores)", "2(coef)", "3(recurrence)", "chunks", "-"};
-        if (which == 302) for (int i = 0; i < 6; ++i) nm[i] = nmp[i];
+        const char * nm[8] = {"A(mask)", "0(V issue)", "1(scores)", "2(softmax coef)", "3(wait V)", "3(recurrence)", "-", "-"};
+        const char * nmp[8] = {"barrier+wait", "1(scores)", "2(coef)", "3(recurrence)", "chunks", "-", "-", "-"};
+        const char * nmd[8] = {"p:mask", "p:V issue", "p:scores", "p:coef", "p:V wait", "p:barrier", "chain busy", "chain wait"};
+        if (which == 302) for (int i = 0; i < 8; ++i) nm[i] = nmp[i];
+        else if (getenv("GGML_MI355X_FA_DEC2") == nullptr || atoi(getenv("GGML_MI355X_FA_DEC2")) != 0) for (int i = 0; i < 8; ++i) nm[i] = nmd[i];
         fprintf(stderr, "FA phases (s_memtime ticks per launch, wg 0):");
-        for (int i = 0; i < 6; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double) h[i] / (iters + 3));
+        for (int i = 0; i < 8; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double) h[i] / (iters + 3));
         fprintf(stderr, "\n");
         g_fa_prof = nullptr;
         MI_CHECK(hipFree(prof));

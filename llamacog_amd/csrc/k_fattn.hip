@@ -489,9 +489,15 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
                 a.cnt = ctx.fa_cnt;
             }
         }
-        // decode (one query row): k_fattn_exact, one 256-thread workgroup per head
-        if (a.n_q == 1) a.kt = ctx.kt_take("fa_exact", (unsigned) (a.H * nq3), 256);
-        launch_fattn_exact(ctx.stream, a, nq3);
+        // decode (one query row): two heads per workgroup with the scores produced under the
+        // recurrence (k_fattn_dec2) where it applies, else k_fattn_exact, one workgroup per head
+        if (fattn_dec2_ok(a, nq3)) {
+            a.kt = ctx.kt_take("fa_dec2", (unsigned) (a.H / 2 * nq3), 512);
+            launch_fattn_dec2(ctx.stream, a, nq3);
+        } else {
+            if (a.n_q == 1) a.kt = ctx.kt_take("fa_exact", (unsigned) (a.H * nq3), 256);
+            launch_fattn_exact(ctx.stream, a, nq3);
+        }
         if (a.qmode) ctx.qcache_put(mm->src[1], a.qmode == 1, act);
         if (ctx.timing) ctx.time_end(TK_FATTN, bytes, ev);
         return;

@@ -35,6 +35,8 @@
 // by the last of its workgroups to finish (device-scope counter, self-resetting).
 #include "fattn.h"
 #include "quant_act.h"
+#include "qtypes.h"
+#include "fa_chain.h"
 
 #include <cmath>
 
@@ -855,6 +857,358 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
         const float rs = 1.0f / S[i];
         *(float2 *) (drow + 2 * lane) = make_float2(__fmul_rn(h2f((uint16_t) y[i][0]), rs), __fmul_rn(h2f((uint16_t) y[i][1]), rs));
     }
+}
+
+// ==== decode, D = 128, f16 cache: two heads per workgroup, scores produced under the recurrence ====
+// The same arithmetic as k_fattn_exact (scores in the AVX-512 ggml_vec_dot_f16 order, the
+// prefix-max (ms, vs) coefficients, the f16 VKQ recurrence with the CPU's two roundings), laid
+// out so the serial part never waits on the rest:
+//   * waves 0-3 are the chains: wave w runs the recurrence of head 2j + (w >> 1), dims
+//     64 (w & 1) .. + 63, one dim per lane (one chain per SIMD);
+//   * waves 4-5 are the producers, one per head: for chunk c + 1 they load the mask, stream V
+//     into LDS (LDS-DMA), score the K rows (every K load of the chunk in flight at once), and
+//     form the coefficients and the per-batch flags, while the chains run chunk c; one
+//     workgroup barrier per chunk hands a double-buffered stage over;
+//   * both heads of a Q8_K block (256 = 2 x 128 outputs) finish in this workgroup, so the
+//     output quantization for the following projection needs no cross-workgroup hand-off.
+// Chunks of DC_CH positions; the running max carries across chunks in the producer, the f16
+// state in the chains, both in cache order, so the chunking changes no result.
+constexpr int DC_CH = 128, DC_U = 8;
+
+// LDS written by lanes of this wave and read back by other lanes of it: LDS instructions of one
+// wave execute in order, so only the compiler must not reorder them (wave_lds_sync's release
+// fence would also wait for this wave's outstanding LDS-DMA and global loads)
+__device__ __forceinline__ void dc_wave_lds_order() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// LDS of k_fattn_dec2, laid out by hand: the small arrays the chains read every batch first,
+// the V stages last (reads at high LDS addresses measured ~5 ticks per position slower,
+// tools/ubench_dc.hip); with GQA sharing only head 0's stages [0, 64 KiB) above them are used
+struct dc_smem {
+    float sc[2][2][DC_CH + 2 * DC_U];   // [head][stage] vs (0 where dead); read ahead by one batch
+    float cm[2][2][DC_CH + 2 * DC_U];   // ms (1 where dead)
+    float mk[2][2][DC_CH + 2 * DC_U];   // mask value (-inf = dead)
+    uint32_t bfl[2][2][2];              // [head][stage][half]: batches taking the general step
+    int nrs[2];                         // positions to run, per stage
+    float mpub[2];                      // [head]: running max through the first half of the chunk
+    int mseq[2];                        // [head]: chunk number + 1 that mpub belongs to
+    float mcar[2];                      // [head]: running max through the whole chunk
+    uint64_t etab[32];                  // expf's table (lx_exp2f_tab)
+    float ol[2 * 128];
+    uint16_t vl[2][2][DC_CH * 128];     // [head][stage][position][dim]
+};
+
+__global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
+    constexpr int D = 128, NM = D / 16, CH = DC_CH, U = DC_U, NPH = CH / 32;   // NPH: score passes per half
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    kt_enter(a.kt);
+    const int64_t hp = blockIdx.x;          // head pair: heads 2 hp, 2 hp + 1
+    const int64_t iq3 = blockIdx.y;
+    const int64_t G = a.H / a.Hkv;
+    const bool vsh = (2 * hp) / G == (2 * hp + 1) / G;   // both heads read one KV head: one V stage
+    __shared__ __attribute__((aligned(16))) dc_smem sm;
+    const int64_t nchunk = (a.n_kv + CH - 1) / CH;
+    const char * mrow = a.mask ? a.mask + (0 % a.mask_ne1) * a.nbm1 : nullptr;
+    if (tid < 32) sm.etab[tid] = lx_exp2f_tab[tid];
+    if (tid < 2) { sm.mseq[tid] = 0; sm.mcar[tid] = -INFINITY; }
+    __syncthreads();
+
+    if (wave >= 4) {
+        // ===== producers: head ph, positions 64 hf .. 64 hf + 63 of each chunk =====
+        const int pw = wave - 4, ph = pw >> 1, hf = pw & 1;
+        const int64_t h = 2 * hp + ph, hk = h / G;
+        const int qd = lane & 3;
+        const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
+        const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
+        const bool dma = ph == 0 || !vsh;
+        auto mask_at = [&](int64_t j) -> uint16_t {   // f16 bits; 0xfc00 (-inf) past the cache
+            if (j >= a.n_kv) return 0xfc00;
+            return mrow ? *(const uint16_t *) (mrow + 2 * j) : (uint16_t) 0;
+        };
+        auto load_k = [&](int64_t c0, int jmax, uint2 (&kh)[NPH][NM]) {   // this half's K rows (<= jmax)
+#pragma unroll
+            for (int p = 0; p < NPH; ++p) {
+                const int j = min(64 * hf + 16 * p + (lane >> 2), jmax);
+                const char * krow = kbase + (c0 + j) * a.nbk1 + 8 * qd;
+#pragma unroll
+                for (int m = 0; m < NM; ++m) kh[p][m] = ld8(krow + 32 * m);
+            }
+        };
+        auto nrun_of = [](uint16_t m0b, uint16_t m1b) {   // positions up to the last live one
+            const unsigned long long b0 = __ballot(m0b != 0xfc00), b1 = __ballot(m1b != 0xfc00);
+            return b1 ? 128 - __clzll(b1) : (b0 ? 64 - __clzll(b0) : 0);
+        };
+        // chunk 0's K rows go out with q and the mask (bounded by the cache, not yet by the mask);
+        // later chunks' go out right after the previous chunk's scores
+        uint2 kh[NPH][NM];
+        if (nchunk > 0) load_k(0, (int) min<int64_t>(CH, a.n_kv) - 1, kh);
+        uint16_t mc0 = mask_at(lane), mc1 = mask_at(64 + lane);
+        float qf[NM][4];
+        {
+            const float * qrow = (const float *) (a.q + h * a.nbq2 + iq3 * a.nbq3);
+            float4 q4[NM];
+#pragma unroll
+            for (int m = 0; m < NM; ++m) q4[m] = *(const float4 *) (qrow + 16 * m + 4 * qd);
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                qf[m][0] = f16r(q4[m].x); qf[m][1] = f16r(q4[m].y); qf[m][2] = f16r(q4[m].z); qf[m][3] = f16r(q4[m].w);
+            }
+        }
+        float nz = -0.0f;
+        asm volatile("" : "+v"(nz));
+        const float slope = a.max_bias > 0.0f
+            ? (float) ((uint32_t) h < a.n_head_log2 ? pow((double) a.m0, (double) (h + 1))
+                                                   : pow((double) a.m1, (double) (2 * ((uint32_t) h - a.n_head_log2) + 1)))
+            : 1.0f;
+        const bool prof = a.prof && blockIdx.x == 0 && blockIdx.y == 0 && pw == 0 && lane == 0;
+        unsigned long long tp = prof ? __builtin_amdgcn_s_memtime() : 0, pc[6] = {0, 0, 0, 0, 0, 0};
+        auto mark = [&](int i) {
+            if (prof) { const unsigned long long t = __builtin_amdgcn_s_memtime(); pc[i] += t - tp; tp = t; }
+        };
+        for (int64_t c = 0; c <= nchunk; ++c) {
+            if (c < nchunk) {
+                const int st = (int) (c & 1);
+                const int64_t c0 = c * CH;
+                const uint16_t m0b = mc0, m1b = mc1;
+                const int nrun = nrun_of(m0b, m1b);
+                // the next chunk's mask, in flight under this one
+                mc0 = mask_at(c0 + CH + lane);
+                mc1 = mask_at(c0 + CH + 64 + lane);
+                const float mv = h2f(hf ? m1b : m0b);   // this half's positions: jl = 64 hf + lane
+                const int jl = 64 * hf + lane;
+                float * mkp = sm.mk[ph][st];
+                float * scp = sm.sc[ph][st];
+                float * cmp = sm.cm[ph][st];
+                mkp[jl] = mv;
+                if (hf && lane < 2 * U) { mkp[CH + lane] = -INFINITY; cmp[CH + lane] = 1.0f; scp[CH + lane] = 0.0f; }
+                const float mcarry = sm.mcar[ph];   // through the previous chunk (published before the last barrier)
+                float tot = mcarry;
+                if (nrun > 0) {
+                    const int lo = 64 * hf, hi = min(nrun, lo + 64);   // this half's rows to run: [lo, hi)
+                    mark(0);
+                    // V rows this wave stages: its half of the chunk, or with one KV head for both
+                    // heads a quarter (LDS-DMA issue runs at ~25 GB/s per wave)
+                    const int vlo = vsh ? 32 * pw : lo, vhi = min(nrun, vsh ? vlo + 32 : lo + 64);
+                    if ((vsh || dma) && vhi > vlo) {
+                        // 4 rows per instruction; the row address advances by addition (a 64-bit
+                        // multiply per instruction made the issue loop ~100 cycles per KiB)
+                        const int r_in = lane >> 4, col = lane & 15;
+                        const int64_t step = 4 * a.nbv1;
+                        const char * vp = vbase + (c0 + vlo + r_in) * a.nbv1 + 16 * col;
+                        const char * vlast = vbase + (c0 + vhi - 1) * a.nbv1 + 16 * col;
+                        uint16_t * dst = sm.vl[vsh ? 0 : ph][st] + 512 * (vlo / 4);
+                        const int np = (vhi - vlo + 3) / 4;
+                        for (int p = 0; p < np; ++p) {
+                            const char * src = (4 * p + r_in < vhi - vlo) ? vp : vlast;
+                            __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) dst, 16, 0, 0);
+                            vp += step;
+                            dst += 512;
+                        }
+                    }
+                    dc_wave_lds_order();                        // mask values, read back by other lanes
+                    mark(1);
+                    // the mask values of this lane's positions in one LDS round trip, then the
+                    // passes up to nrun (computing all four at small depth cost more than it hid)
+                    float mj[NPH];
+#pragma unroll
+                    for (int p = 0; p < NPH; ++p) mj[p] = mkp[lo + 16 * p + (lane >> 2)];
+#pragma unroll
+                    for (int p = 0; p < NPH; ++p) {
+                        if (lo + 16 * p >= nrun) break;
+                        const int j = lo + 16 * p + (lane >> 2);
+                        const float w = dot_f16_mix_d128(kh[p], qf, nz);
+                        if (qd == 0 && j < nrun) {
+                            float sv = __fmul_rn(w, a.scale);
+                            if (a.softcap != 0.0f) sv = __fmul_rn(a.softcap, tanhf(sv));
+                            scp[j] = __fadd_rn(sv, __fmul_rn(slope, mj[p]));
+                        }
+                    }
+                    // the next chunk's K rows, in flight under this chunk's coefficients and the
+                    // chains' recurrence
+                    if (c + 1 < nchunk) {
+                        const int nn = nrun_of(mc0, mc1);
+                        if (nn > 0) load_k(c0 + CH, nn - 1, kh);
+                    }
+                    dc_wave_lds_order();
+                    mark(2);
+                    // prefix max over the chunk: this half's scan, the first half's total from LDS
+                    const bool live = mv != -INFINITY && jl < nrun;
+                    const float sj = live ? scp[jl] : -INFINITY;
+                    const float smx = wave_scan_max(sj);
+                    const float th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(smx), 63));
+                    float base = mcarry;   // running max before this half
+                    if (hf == 0) {
+                        if (lane == 0) {
+                            // LDS only, in order: the value, its write done, then the sequence word
+                            // (a workgroup-scope fence would also wait for this wave's V DMA and K loads)
+                            *(volatile float *) &sm.mpub[ph] = fmaxf(mcarry, th);
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            *(volatile int *) &sm.mseq[ph] = (int) c + 1;
+                        }
+                    } else {
+                        // the first half of the same head publishes its max within its own chunk work
+                        int guard = 0;
+                        while (*(volatile int *) &sm.mseq[ph] != (int) c + 1 && ++guard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
+                        base = *(volatile float *) &sm.mpub[ph];
+                    }
+                    const float M = fmaxf(base, dpp_ninf<0x138>(smx));   // max over every position before jl
+                    float msv, vsv;
+                    if (!live) { msv = 1.0f; vsv = 0.0f; }
+                    else if (sj > M) { msv = M == -INFINITY ? 0.0f : lx_expf_t(M - sj, (const uint64_t *) sm.etab); vsv = 1.0f; }
+                    else { msv = 1.0f; vsv = lx_expf_t(sj - M, (const uint64_t *) sm.etab); }
+                    cmp[jl] = msv;
+                    scp[jl] = vsv;
+                    // batch flags: a dead position, a max update or padding past nrun
+                    const bool gen = jl < nrun ? (!live || sj > M) : (jl < nrun + U);
+                    const unsigned long long wb = __ballot(gen);
+                    uint32_t f = 0;
+#pragma unroll
+                    for (int bb = 0; bb < 64 / U; ++bb) f |= ((wb >> (U * bb)) & ((1ull << U) - 1)) ? 1u << bb : 0u;
+                    if (lane == 0) sm.bfl[ph][st][hf] = f;
+                    tot = fmaxf(base, th);
+                    mark(3);
+                } else {
+                    if (hf == 0 && lane == 0) *(volatile int *) &sm.mseq[ph] = (int) c + 1;
+                    if (c + 1 < nchunk) {
+                        const int nn = nrun_of(mc0, mc1);
+                        if (nn > 0) load_k(c0 + CH, nn - 1, kh);
+                    }
+                }
+                if (hf == 1 && lane == 0) sm.mcar[ph] = nrun > 0 ? tot : mcarry;   // read after the barrier
+                if (pw == 0 && lane == 0) sm.nrs[st] = nrun;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's V rows are in LDS
+                mark(4);
+            }
+            __syncthreads();
+            mark(5);
+        }
+        if (prof) for (int i = 0; i < 6; ++i) a.prof[i] += pc[i];
+    } else {
+        // ===== chains: head 2 hp + (wave >> 1), dim d =====
+        const int ch = wave >> 1;
+        const int d = (wave & 1) * 64 + lane;
+        uint32_t yb = 0;
+        float S = 0.0f;
+        const bool prof = a.prof && blockIdx.x == 0 && blockIdx.y == 0 && wave == 0 && lane == 0;
+        unsigned long long tp = prof ? __builtin_amdgcn_s_memtime() : 0, cbusy = 0, cwait = 0;
+        for (int64_t c = 0; c <= nchunk; ++c) {
+            if (c >= 1) {
+                const int st = (int) ((c - 1) & 1);
+                const int nrun = __builtin_amdgcn_readfirstlane(sm.nrs[st]);
+                const uint32_t flags = __builtin_amdgcn_readfirstlane(sm.bfl[ch][st][0] | (sm.bfl[ch][st][1] << 8));
+                const uint16_t * vrow = sm.vl[vsh ? 0 : ch][st] + d;
+                const float * scp = sm.sc[ch][st];
+                const float * cmp = sm.cm[ch][st];
+                const float * mkp = sm.mk[ch][st];
+                auto ld4 = [&](const float * p, float (&o)[U]) {
+#pragma unroll
+                    for (int u = 0; u < U; u += 4) {
+                        const float4 t = *(const float4 *) (p + u);
+                        o[u] = t.x; o[u + 1] = t.y; o[u + 2] = t.z; o[u + 3] = t.w;
+                    }
+                };
+                auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) vv[u] = vrow[(j + u) * D];
+                    ld4(scp + j, vs);
+                };
+                auto run = [&](const uint32_t (&vv)[U], const float (&vs)[U]) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        yb = f16_mad(vv[u], vs[u], yb);
+                        S = __fadd_rn(S, vs[u]);   // not contracted on the CPU
+                    }
+                };
+                // nf consecutive batches without a dead position or a max update, from position
+                // j0: a loop with nothing else in it (a flag test and the general step inside the
+                // loop cost ~15 ticks per position, tools/ubench_dc.hip)
+                auto fast_run = [&](int j0, int nf) {
+                    uint32_t va[U], vb[U];
+                    float sa[U], sb[U];
+                    ldb(j0, va, sa);
+                    for (int k = 0; k < nf; k += 2) {
+                        ldb(j0 + (k + 1) * U, vb, sb);
+                        run(va, sa);
+                        if (k + 1 >= nf) break;
+                        ldb(j0 + (k + 2) * U, va, sa);
+                        run(vb, sb);
+                    }
+                };
+                // a batch with a dead position or a running-max update: a dead position keeps the
+                // state (-0 must survive); an update (ms != 1) first rescales, y = f16(y*ms),
+                // S = S*ms (ops.cpp:7171-7190)
+                auto general = [&](int j) {
+                    uint32_t vv[U];
+                    float vs[U], ms[U], mv[U];
+                    ldb(j, vv, vs);
+                    ld4(cmp + j, ms);
+                    ld4(mkp + j, mv);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const bool live = __float_as_uint(mv[u]) != 0xff800000u;
+                        const bool upd = __float_as_uint(ms[u]) != 0x3f800000u;
+                        float t = __fmul_rn(h2f((uint16_t) yb), ms[u]);
+                        asm("" : "+v"(t));   // two roundings, as f16r
+                        const uint32_t ys = upd ? (uint32_t) f2h(t) : yb;
+                        const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
+                        const uint32_t yn = f16_mad(vv[u], vs[u], ys);
+                        const float Sn = __fadd_rn(Ss, vs[u]);
+                        yb = live ? yn : yb;
+                        S = live ? Sn : S;
+                    }
+                };
+                const int nb = (nrun + U - 1) / U;
+                int b = 0;
+                while (b < nb) {
+                    const uint32_t rest = flags >> b;
+                    const int nf = min(rest ? __builtin_ctz(rest) : 32, nb - b);   // fast batches before the next general one
+                    if (nf > 0) {
+                        fast_run(b * U, nf);
+                        b += nf;
+                    }
+                    if (b < nb) {
+                        general(b * U);
+                        ++b;
+                    }
+                }
+            }
+            if (prof) { const unsigned long long t = __builtin_amdgcn_s_memtime(); cbusy += t - tp; tp = t; }
+            __syncthreads();
+            if (prof) { const unsigned long long t = __builtin_amdgcn_s_memtime(); cwait += t - tp; tp = t; }
+        }
+        if (prof) { a.prof[6] += cbusy; a.prof[7] += cwait; }
+        const int64_t h = 2 * hp + ch;
+        const float o = __fmul_rn(h2f((uint16_t) yb), 1.0f / S);
+        float * drow = (float *) ((char *) a.dst + h * a.nb1_dst + iq3 * a.nb2_dst);
+        drow[d] = o;
+        sm.ol[ch * D + d] = o;
+    }
+    // ---- the two heads' 256 outputs: quantized here for the following projection ----
+    if (a.qmode) {
+        __syncthreads();
+        if (wave == 0) {
+            float q[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = sm.ol[4 * lane + k];
+            const int64_t c0 = 256 * hp;
+            if (a.qmode == 1) q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
+            else q8_0_wave(q, lane, true, a.qs + c0, a.qd + c0 / 32, a.qsum + c0 / 32);
+        }
+    }
+    kt_exit(a.kt);
+}
+
+bool fattn_dec2_ok(const fa_args & a, int64_t nq3) {
+    static const bool on = !getenv("GGML_MI355X_FA_DEC2") || atoi(getenv("GGML_MI355X_FA_DEC2")) != 0;
+    return on && a.n_q == 1 && a.D == 128 && a.k_type == GGML_TYPE_F16 && a.v_type == GGML_TYPE_F16 && a.H % 2 == 0 &&
+           (a.qmode == 0 || nq3 == 1);
+}
+
+void launch_fattn_dec2(hipStream_t st, const fa_args & a, int64_t nq3) {
+    hipLaunchKernelGGL(k_fattn_dec2, dim3((unsigned) (a.H / 2), (unsigned) nq3), dim3(512), 0, st, a);
 }
 
 void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {

@@ -55,9 +55,9 @@ LX_FN double lx_asdouble(uint64_t u) { double f; memcpy(&f, &u, 8); return f; }
 
 LX_TABLE uint64_t lx_exp2f_tab[32] = LX_EXP2F_TAB;
 
-LX_FN float lx_expf(float x) {
+// T: the 32-entry table (lx_exp2f_tab, or a copy of it in LDS)
+LX_FN float lx_expf_t(float x, const uint64_t * T) {
     LX_NOCONTRACT
-    const uint64_t * T = lx_exp2f_tab;
     const double invln2N = 0x1.71547652b82fep+0 * 32;
     const double SHIFT = 0x1.8p+52;
     const double C0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32;
@@ -90,6 +90,7 @@ LX_FN float lx_expf(float x) {
     y = y * s;
     return (float) y;
 }
+LX_FN float lx_expf(float x) { return lx_expf_t(x, lx_exp2f_tab); }
 
 // ---- sinf / cosf (s_sinf.c, s_cosf.c, sincosf.h; TOINT_INTRINSICS = 0) ----------------------
 struct lx_sincos_t { double sign[4], hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3; };

@@ -185,6 +185,34 @@ def test_flash_attn_f16_llama_shapes_vs_oracle(K, n_kv, n_q, Hkv, G):
     assert_bits(out, ref, f"flash_attn f16 n_kv={n_kv} n_q={n_q}")
 
 
+@pytest.mark.parametrize("n_kv,Hkv,G,pattern", [(300, 4, 1, "holes"), (1000, 8, 2, "first_chunk_dead"),
+                                                  (256, 8, 4, "single"), (129, 2, 4, "holes"), (4352, 8, 4, "sparse")])
+def test_flash_attn_f16_decode_masks_vs_oracle(K, n_kv, Hkv, G, pattern):
+    """Decode (one query row) over masks the causal tail does not exercise: dead positions inside
+    a batch, a whole dead chunk, a single live position, one position past a chunk boundary, and
+    a sparse mask at depth; heads without GQA sharing (G = 1: two KV heads per head pair)."""
+    rng = np.random.default_rng(n_kv * 7 + G)
+    D, H = 128, Hkv * G
+    q = (rng.standard_normal((1, H, D)) * 2).astype(np.float32)
+    k = rng.standard_normal((n_kv, Hkv, D)).astype(np.float16)
+    v = rng.standard_normal((n_kv, Hkv, D)).astype(np.float16)
+    m = np.zeros((1, n_kv), dtype=np.float16)
+    if pattern == "holes":
+        m[0, rng.random(n_kv) < 0.3] = -np.inf
+    elif pattern == "first_chunk_dead":
+        m[0, :128] = -np.inf
+        m[0, 500:517] = -np.inf
+    elif pattern == "single":
+        m[0, :] = -np.inf
+        m[0, 77] = 0
+    else:
+        m[0, rng.random(n_kv) < 0.9] = -np.inf
+        m[0, -1] = 0
+    out = K.flash_attn(q, k.view(np.uint8), v.view(np.uint8), m.view(np.uint16), O.F16, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    ref = O.flash_attn(q, k.view(np.uint8), v.view(np.uint8), m.view(np.uint16), O.F16, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    assert_bits(out, ref, f"flash_attn f16 decode {pattern} n_kv={n_kv} G={G}")
+
+
 @pytest.mark.parametrize("name,Kd,M", [("q4_K", 4096, 256), ("q5_K", 4096, 200), ("q6_K", 4096, 136),
                                         ("q4_K", 14336, 128), ("q6_K", 14336, 64), ("q4_K", 4096, 100)])
 def test_mul_mat_prefill_bit_exact(K, name, Kd, M):
