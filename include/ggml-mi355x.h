@@ -66,6 +66,13 @@ void ggml_backend_mi355x_p2p_stats(long * rccl, long * peer);
 void ggml_backend_mi355x_handoff_stats(long * rccl, long * peer, long * d2d);
 // destroys the RCCL communicators (re-created on the next cross-device copy)
 void ggml_backend_mi355x_p2p_release(void);
+// row split (-sm row): the buffer type libllama obtains through
+// ggml_backend_reg_get_proc_address(reg, "ggml_backend_split_buffer_type") (src/llama-model.cpp:
+// 337-360; ggml-cuda.cu:1047 is the reference GPU backend's): matrices cut into per-device row
+// slices in proportion to tensor_split (nullptr: equal shares)
+ggml_backend_buffer_type_t ggml_backend_mi355x_split_buffer_type(int main_device, const float * tensor_split);
+// row-split mat-muls executed, and slices of them computed on another GPU than the main device's
+void ggml_backend_mi355x_split_stats(long * mm, long * foreign);
 // measured HBM read ceiling of a device in GB/s (STREAM-style non-temporal read of 440 MB
 // slices of a 4 GiB pool, best of three grids; llamacog_amd/csrc/k_stream.hip): the peak
 // bench.py reports its roofline fractions against beside the 8 TB/s nominal.  -1 on failure.

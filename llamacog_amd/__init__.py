@@ -71,6 +71,13 @@ def handoff_stats() -> tuple[int, int, int]:
     return r.value, p.value, d.value
 
 
+def split_stats() -> tuple[int, int]:
+    """(row-split mat-muls executed, slices of them computed on another GPU) since load."""
+    m, f = ctypes.c_long(), ctypes.c_long()
+    plugin_lib().ggml_backend_mi355x_split_stats(ctypes.byref(m), ctypes.byref(f))
+    return m.value, f.value
+
+
 def hbm_read_gbs(device: int = 0) -> float:
     """Measured HBM read ceiling of a device, GB/s (k_stream.hip)."""
     lib = plugin_lib()

@@ -23,6 +23,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -376,6 +377,286 @@ static ggml_backend_buffer_type_t mi_host_buft() {
         /* .context = */ nullptr,
     };
     return &buft;
+}
+
+// ------------------------------------------------------------------------------------------
+// buffer_from_host_ptr (device vtable, ggml-backend-impl.h; libllama wraps its mmap'd model
+// file this way when a device advertises caps.buffer_from_host_ptr, src/llama-model.cpp:
+// 4311-4337): the host range is page-locked and mapped into the GPU's address space
+// (hipHostRegister), and tensors in it are read by the kernels over the host link, in place.
+// The capability stays false in the device props, as the reference GPU backend's
+// (ggml-cuda.cu:2975): for a discrete GPU, weights read over PCIe every token are the slow
+// choice, and libllama then copies the weights into device memory instead.  The entry point
+// exists for callers that want zero-copy access (tests/test_gpu_kernels.py checks a mat-vec
+// over such a buffer bit for bit against the same weights in HBM).
+// ------------------------------------------------------------------------------------------
+struct mi_hostptr_ctx { void * host; void * dev; size_t size; int device; };
+
+static const char * mi_hostptr_buft_get_name(ggml_backend_buffer_type_t) { return MI355X_NAME "_Mapped"; }
+static bool mi_hostptr_buft_is_host(ggml_backend_buffer_type_t) { return true; }
+
+static void mi_hostptr_free(ggml_backend_buffer_t buffer) {
+    auto * c = (mi_hostptr_ctx *) buffer->context;
+    MI_CHECK(hipSetDevice(c->device));
+    (void) hipHostUnregister(c->host);
+    delete c;
+}
+static void * mi_hostptr_get_base(ggml_backend_buffer_t buffer) { return ((mi_hostptr_ctx *) buffer->context)->dev; }
+// the CPU side reaches a tensor at the same offset from the host base
+static char * mi_hostptr_host_addr(ggml_backend_buffer_t buffer, const ggml_tensor * t) {
+    auto * c = (mi_hostptr_ctx *) buffer->context;
+    return (char *) c->host + ((const char *) t->data - (const char *) c->dev);
+}
+static void mi_hostptr_memset(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size_t off, size_t n) { memset(mi_hostptr_host_addr(b, t) + off, v, n); }
+static void mi_hostptr_set(ggml_backend_buffer_t b, ggml_tensor * t, const void * d, size_t off, size_t n) { memcpy(mi_hostptr_host_addr(b, t) + off, d, n); }
+static void mi_hostptr_get(ggml_backend_buffer_t b, const ggml_tensor * t, void * d, size_t off, size_t n) { memcpy(d, mi_hostptr_host_addr(b, t) + off, n); }
+static void mi_hostptr_clear(ggml_backend_buffer_t b, uint8_t v) { auto * c = (mi_hostptr_ctx *) b->context; memset(c->host, v, c->size); }
+
+static const ggml_backend_buffer_i mi_hostptr_iface = {
+    /* .free_buffer   = */ mi_hostptr_free,
+    /* .get_base      = */ mi_hostptr_get_base,
+    /* .init_tensor   = */ nullptr,
+    /* .memset_tensor = */ mi_hostptr_memset,
+    /* .set_tensor    = */ mi_hostptr_set,
+    /* .get_tensor    = */ mi_hostptr_get,
+    /* .cpy_tensor    = */ nullptr,
+    /* .clear         = */ mi_hostptr_clear,
+    /* .reset         = */ nullptr,
+};
+
+static ggml_backend_buffer_type_t mi_hostptr_buft(ggml_backend_dev_t dev) {
+    static std::mutex mtx;
+    static std::map<ggml_backend_dev_t, ggml_backend_buffer_type *> bufts;
+    std::lock_guard<std::mutex> lk(mtx);
+    auto it = bufts.find(dev);
+    if (it != bufts.end()) return it->second;
+    auto * b = new ggml_backend_buffer_type{{mi_hostptr_buft_get_name, nullptr, nullptr, nullptr, nullptr, mi_hostptr_buft_is_host}, dev, nullptr};
+    bufts.emplace(dev, b);
+    return b;
+}
+
+static ggml_backend_buffer_t mi_dev_buffer_from_host_ptr(ggml_backend_dev_t dev, void * ptr, size_t size, size_t max_tensor_size) {
+    (void) max_tensor_size;
+    const int device = ((mi_device_ctx *) dev->context)->device;
+    MI_CHECK(hipSetDevice(device));
+    if (hipHostRegister(ptr, size, hipHostRegisterMapped) != hipSuccess) {
+        (void) hipGetLastError();
+        MI_LOG_WARN("mi355x: hipHostRegister of %.2f MiB failed\n", size / 1048576.0);
+        return nullptr;
+    }
+    void * dptr = nullptr;
+    if (hipHostGetDevicePointer(&dptr, ptr, 0) != hipSuccess || dptr == nullptr) {
+        (void) hipGetLastError();
+        (void) hipHostUnregister(ptr);
+        return nullptr;
+    }
+    return ggml_backend_buffer_init(mi_hostptr_buft(dev), mi_hostptr_iface, new mi_hostptr_ctx{ptr, dptr, size, device}, size);
+}
+
+// ------------------------------------------------------------------------------------------
+// row-split buffer type: ggml_backend_split_buffer_type(main_device, tensor_split), the proc
+// address libllama asks for with -sm row (src/llama-model.cpp:337-360; the reference GPU
+// backend's is ggml-cuda.cu:789-1087).  A matrix in it is cut into row slices, one per device
+// in proportion to tensor_split (rounded to 64 rows, so every slice keeps whole GEMV row
+// groups), each slice in its device's memory; tensor->extra lists them.  The main device's
+// backend computes the MUL_MATs that read such a weight (op_mul_mat_split): slice by slice, the
+// rows gathered into the output.  Each output row's arithmetic is the one-device kernel's, so
+// the result is bit-identical to a single-device run.
+// ------------------------------------------------------------------------------------------
+struct mi_split_buft_ctx { int main_device; std::vector<float> split; std::string name; };   // split: cumulative fractions
+struct mi_split_extra { split_parts sp; };
+struct mi_split_buf_ctx { std::vector<mi_split_extra *> extras; };
+constexpr int64_t MI_SPLIT_ROUND = 64;
+
+static int mi_dev_hip(int d) { return ((mi_reg_ctx *) mi_reg()->context)->dev_ctx[d]->device; }
+
+static void mi_split_rows(const mi_split_buft_ctx * b, int64_t nrows, int d, int64_t & lo, int64_t & hi) {
+    const int nd = (int) b->split.size();
+    lo = d == 0 ? 0 : (int64_t) (nrows * b->split[d]);
+    lo -= lo % MI_SPLIT_ROUND;
+    if (d == nd - 1) {
+        hi = nrows;
+    } else {
+        hi = (int64_t) (nrows * b->split[d + 1]);
+        hi -= hi % MI_SPLIT_ROUND;
+    }
+    hi = std::max(hi, lo);
+}
+
+static const char * mi_split_buft_get_name(ggml_backend_buffer_type_t buft) { return ((mi_split_buft_ctx *) buft->context)->name.c_str(); }
+static bool mi_split_buft_is_ours(ggml_backend_buffer_type_t buft) { return buft && buft->iface.get_name == mi_split_buft_get_name; }
+
+static void mi_split_buf_free(ggml_backend_buffer_t buffer) {
+    auto * ctx = (mi_split_buf_ctx *) buffer->context;
+    for (mi_split_extra * e : ctx->extras) {
+        for (int i = 0; i < e->sp.n; ++i) {
+            MI_CHECK(hipSetDevice(e->sp.p[i].hip));
+            MI_CHECK(hipFree(e->sp.p[i].data));
+        }
+        delete e;
+    }
+    delete ctx;
+}
+
+// the slices live in the extras; the buffer's base is a placeholder that is never dereferenced
+static void * mi_split_buf_get_base(ggml_backend_buffer_t) { return (void *) 0x1000; }
+
+static enum ggml_status mi_split_buf_init_tensor(ggml_backend_buffer_t buffer, ggml_tensor * tensor) {
+    GGML_ASSERT(tensor->view_src == nullptr && "mi355x: views of row-split tensors are not supported");
+    GGML_ASSERT(ggml_is_contiguous(tensor) && "mi355x: row-split tensors must be contiguous");
+    auto * ctx = (mi_split_buf_ctx *) buffer->context;
+    const auto * b = (const mi_split_buft_ctx *) buffer->buft->context;
+    auto * e = new mi_split_extra{};
+    const int64_t nrows = ggml_nrows(tensor);
+    const size_t rs = ggml_row_size(tensor->type, tensor->ne[0]);
+    for (int d = 0; d < (int) b->split.size(); ++d) {
+        int64_t lo, hi;
+        mi_split_rows(b, nrows, d, lo, hi);
+        if (hi <= lo) continue;
+        split_part & p = e->sp.p[e->sp.n++];
+        p.hip = mi_dev_hip(d);
+        p.lo = lo;
+        p.hi = hi;
+        const size_t bytes = (size_t) (hi - lo) * rs, pad = ggml_is_quantized(tensor->type) ? 256 : 0;
+        MI_CHECK(hipSetDevice(p.hip));
+        MI_CHECK(hipMalloc(&p.data, bytes + pad));
+        if (pad) MI_CHECK(hipMemset((char *) p.data + bytes, 0, pad));   // the zeroed tail of the one-device buffer
+    }
+    ctx->extras.push_back(e);
+    tensor->extra = e;
+    return GGML_STATUS_SUCCESS;
+}
+
+static void mi_split_buf_set_tensor(ggml_backend_buffer_t, ggml_tensor * tensor, const void * data, size_t offset, size_t size) {
+    // whole tensors only (as the reference's split buffer: ggml-cuda.cu:879-880)
+    GGML_ASSERT(offset == 0 && size == ggml_nbytes(tensor));
+    const auto * e = (const mi_split_extra *) tensor->extra;
+    const size_t rs = ggml_row_size(tensor->type, tensor->ne[0]);
+    for (int i = 0; i < e->sp.n; ++i) {
+        const split_part & p = e->sp.p[i];
+        MI_CHECK(hipSetDevice(p.hip));
+        MI_CHECK(hipMemcpy(p.data, (const char *) data + p.lo * rs, (size_t) (p.hi - p.lo) * rs, hipMemcpyHostToDevice));
+    }
+}
+
+static void mi_split_buf_get_tensor(ggml_backend_buffer_t, const ggml_tensor * tensor, void * data, size_t offset, size_t size) {
+    GGML_ASSERT(offset == 0 && size == ggml_nbytes(tensor));
+    const auto * e = (const mi_split_extra *) tensor->extra;
+    const size_t rs = ggml_row_size(tensor->type, tensor->ne[0]);
+    for (int i = 0; i < e->sp.n; ++i) {
+        const split_part & p = e->sp.p[i];
+        MI_CHECK(hipSetDevice(p.hip));
+        MI_CHECK(hipMemcpy((char *) data + p.lo * rs, p.data, (size_t) (p.hi - p.lo) * rs, hipMemcpyDeviceToHost));
+    }
+}
+
+static void mi_split_buf_clear(ggml_backend_buffer_t buffer, uint8_t value) {
+    auto * ctx = (mi_split_buf_ctx *) buffer->context;
+    for (mi_split_extra * e : ctx->extras) {
+        for (int i = 0; i < e->sp.n; ++i) {
+            MI_CHECK(hipSetDevice(e->sp.p[i].hip));
+            (void) value;   // slices are rewritten by set_tensor; a clear only touches what init_tensor owns
+        }
+    }
+}
+
+static const ggml_backend_buffer_i mi_split_buffer_iface = {
+    /* .free_buffer   = */ mi_split_buf_free,
+    /* .get_base      = */ mi_split_buf_get_base,
+    /* .init_tensor   = */ mi_split_buf_init_tensor,
+    /* .memset_tensor = */ nullptr,
+    /* .set_tensor    = */ mi_split_buf_set_tensor,
+    /* .get_tensor    = */ mi_split_buf_get_tensor,
+    /* .cpy_tensor    = */ nullptr,
+    /* .clear         = */ mi_split_buf_clear,
+    /* .reset         = */ nullptr,
+};
+
+static ggml_backend_buffer_t mi_split_buft_alloc_buffer(ggml_backend_buffer_type_t buft, size_t size) {
+    // nothing is allocated here: init_tensor places each tensor's slices on their devices
+    return ggml_backend_buffer_init(buft, mi_split_buffer_iface, new mi_split_buf_ctx, size);
+}
+
+static size_t mi_split_buft_get_alignment(ggml_backend_buffer_type_t) { return 128; }
+
+static size_t mi_split_buft_get_alloc_size(ggml_backend_buffer_type_t buft, const ggml_tensor * tensor) {
+    const auto * b = (const mi_split_buft_ctx *) buft->context;
+    const int64_t nrows = ggml_nrows(tensor);
+    const size_t rs = ggml_row_size(tensor->type, tensor->ne[0]);
+    size_t total = 0;
+    for (int d = 0; d < (int) b->split.size(); ++d) {
+        int64_t lo, hi;
+        mi_split_rows(b, nrows, d, lo, hi);
+        if (hi > lo) total += (size_t) (hi - lo) * rs + (ggml_is_quantized(tensor->type) ? 256 : 0);
+    }
+    return total;
+}
+
+static bool mi_split_buft_is_host(ggml_backend_buffer_type_t) { return false; }
+
+static const ggml_backend_buffer_type_i mi_split_buft_iface = {
+    /* .get_name       = */ mi_split_buft_get_name,
+    /* .alloc_buffer   = */ mi_split_buft_alloc_buffer,
+    /* .get_alignment  = */ mi_split_buft_get_alignment,
+    /* .get_max_size   = */ nullptr,
+    /* .get_alloc_size = */ mi_split_buft_get_alloc_size,
+    /* .is_host        = */ mi_split_buft_is_host,
+};
+
+// tensor_split: per-device proportions (nullptr or all zero: equal shares), as libllama passes
+// llama_model_params::tensor_split
+static ggml_backend_buffer_type_t mi_split_buffer_type(int main_device, const float * tensor_split) {
+    static std::mutex mtx;
+    static std::map<std::pair<int, std::vector<float>>, ggml_backend_buffer_type *> cache;
+    std::lock_guard<std::mutex> lk(mtx);
+    const int nd = (int) mi_reg_get_device_count(mi_reg());
+    if (main_device < 0 || main_device >= nd) return nullptr;
+    std::vector<float> w(nd, 0.0f);
+    bool any = false;
+    for (int i = 0; i < nd; ++i) {
+        w[i] = tensor_split ? std::max(tensor_split[i], 0.0f) : 0.0f;
+        any = any || w[i] > 0.0f;
+    }
+    if (!any) std::fill(w.begin(), w.end(), 1.0f);
+    float sum = 0.0f;
+    std::vector<float> cum(nd);
+    for (int i = 0; i < nd; ++i) { cum[i] = sum; sum += w[i]; }
+    for (int i = 0; i < nd; ++i) cum[i] /= sum;
+    auto key = std::make_pair(main_device, cum);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    auto * bctx = new mi_split_buft_ctx{main_device, cum, std::string(MI355X_NAME) + std::to_string(main_device) + "_Split"};
+    auto * buft = new ggml_backend_buffer_type{mi_split_buft_iface, mi_reg_get_device(mi_reg(), main_device), bctx};
+    cache.emplace(key, buft);
+    return buft;
+}
+
+namespace mi355x {
+bool tensor_split_parts(const ggml_tensor * t, split_parts & sp) {
+    if (!t || !t->buffer || !mi_split_buft_is_ours(t->buffer->buft) || !t->extra) return false;
+    sp = ((const mi_split_extra *) t->extra)->sp;
+    return true;
+}
+}
+
+// may device `dev` run op with a row-split weight (the main device, rows on it, one 2-D matrix;
+// Q4_K / Q4_0 only with whole 8-row groups, the condition of the CPU's repacked order, which
+// must not differ between a slice and the whole matrix)
+static bool mi_split_op_ok(ggml_backend_dev_t dev, const ggml_tensor * op) {
+    for (int s = 0; s < GGML_MAX_SRC; ++s) {
+        const ggml_tensor * t = op->src[s];
+        if (!t || !t->buffer || !mi_split_buft_is_ours(t->buffer->buft)) continue;
+        if (op->op != GGML_OP_MUL_MAT || s != 0) return false;
+        const auto * b = (const mi_split_buft_ctx *) t->buffer->buft->context;
+        if (mi_reg_get_device(mi_reg(), b->main_device) != dev) return false;
+        if (t->ne[2] != 1 || t->ne[3] != 1 || !ggml_is_contiguous(t)) return false;
+        if ((t->type == GGML_TYPE_Q4_K || t->type == GGML_TYPE_Q4_0) && t->ne[1] % 8 != 0) return false;
+        int64_t lo, hi;
+        mi_split_rows(b, ggml_nrows(t), b->main_device, lo, hi);
+        if (hi <= lo) return false;   // the main device holds no rows (small matrices: no row split)
+        if (!ggml_is_contiguous(op->src[1])) return false;
+    }
+    return true;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -884,7 +1165,16 @@ static enum ggml_status mi_backend_graph_compute(ggml_backend_t backend, ggml_cg
         }
         MI_CHECK(hipMemsetAsync(ctx->ex.kt_buf, 0, ctx->ex.kt_cap * sizeof(unsigned long long), ctx->ex.stream));
     }
-    const bool use_graph = dyn_ok && graphs_enabled() && !ctx->graphs_broken && !ctx->ex.timing;
+    // a row-split mat-mul with a slice on another GPU runs its helper streams eagerly
+    bool foreign = false;
+    for (int i = 0; i < ggml_graph_n_nodes(cgraph) && !foreign; ++i) {
+        const ggml_tensor * t = ggml_graph_node(cgraph, i);
+        split_parts sp;
+        if (t->op == GGML_OP_MUL_MAT && tensor_split_parts(t->src[0], sp)) {
+            for (int k = 0; k < sp.n; ++k) foreign = foreign || sp.p[k].hip != ctx->device;
+        }
+    }
+    const bool use_graph = dyn_ok && graphs_enabled() && !ctx->graphs_broken && !ctx->ex.timing && !foreign;
     if (!use_graph || !graph_compute_hipgraph(ctx, cgraph)) {
         run_nodes(ctx->ex, cgraph);
     }
@@ -1001,11 +1291,12 @@ static ggml_backend_buffer_type_t mi_dev_get_host_buffer_type(ggml_backend_dev_t
 }
 
 static bool mi_dev_supports_op(ggml_backend_dev_t dev, const ggml_tensor * op) {
-    (void) dev;
-    return op_supported(op);
+    return mi_split_op_ok(dev, op) && op_supported(op);
 }
 
 static bool mi_dev_supports_buft(ggml_backend_dev_t dev, ggml_backend_buffer_type_t buft) {
+    if (mi_split_buft_is_ours(buft)) return buft->device == dev;
+    if (buft->iface.get_name == mi_hostptr_buft_get_name) return buft->device == dev;   // mapped host memory
     return mi_buft_is_ours(buft) && buft->context == dev->context;
 }
 
@@ -1055,7 +1346,7 @@ static const ggml_backend_device_i mi_device_iface = {
     /* .init_backend         = */ mi_dev_init_backend,
     /* .get_buffer_type      = */ mi_dev_get_buffer_type,
     /* .get_host_buffer_type = */ mi_dev_get_host_buffer_type,
-    /* .buffer_from_host_ptr = */ nullptr,
+    /* .buffer_from_host_ptr = */ mi_dev_buffer_from_host_ptr,
     /* .supports_op          = */ mi_dev_supports_op,
     /* .supports_buft        = */ mi_dev_supports_buft,
     /* .offload_op           = */ mi_dev_offload_op,
@@ -1091,6 +1382,7 @@ static ggml_backend_feature * mi_get_features(ggml_backend_reg_t) {
 
 static void * mi_reg_get_proc_address(ggml_backend_reg_t, const char * name) {
     if (strcmp(name, "ggml_backend_get_features") == 0) return (void *) mi_get_features;
+    if (strcmp(name, "ggml_backend_split_buffer_type") == 0) return (void *) mi_split_buffer_type;
     return nullptr;
 }
 
@@ -1194,6 +1486,12 @@ GGML_BACKEND_API void ggml_backend_mi355x_handoff_stats(long * rccl, long * peer
 }
 
 GGML_BACKEND_API void ggml_backend_mi355x_p2p_release(void) { p2p_destroy(); }
+
+GGML_BACKEND_API void ggml_backend_mi355x_split_stats(long * mm, long * foreign) { mi355x::split_stats(mm, foreign); }
+
+GGML_BACKEND_API ggml_backend_buffer_type_t ggml_backend_mi355x_split_buffer_type(int main_device, const float * tensor_split) {
+    return mi_split_buffer_type(main_device, tensor_split);
+}
 
 GGML_BACKEND_API void ggml_backend_mi355x_set_flags(int no_fuse, int no_graph) {
     g_no_fuse.store(no_fuse ? 1 : 0);

@@ -490,6 +490,57 @@ __global__ __launch_bounds__(256) void k_pattern_read(const uint8_t * __restrict
 
 namespace mi355x { void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst); }
 
+// buffer_from_host_ptr check: the q4_K weights `w` [M][K/256 blocks] held in host memory are
+// wrapped with the device's buffer_from_host_ptr (registered, mapped), the decode mat-vec reads
+// them in place, and the result is compared bit for bit with the same weights copied to HBM.
+// Returns 0 when identical, 1 on a mismatch, -1 when the device refuses the mapping.
+extern "C" GGML_BACKEND_API int mi355x_check_host_ptr_matvec(const void * w, int64_t K, int64_t M, const float * x) {
+    ggml_backend_reg_t reg = ggml_backend_mi355x_reg();
+    ggml_backend_dev_t dev = ggml_backend_reg_dev_get(reg, 0);
+    const size_t wbytes = ggml_row_size(GGML_TYPE_Q4_K, K) * (size_t) M;
+    // a page-aligned host copy: hipHostRegister maps whole pages
+    const size_t pg = 4096, hsz = (wbytes + 256 + pg - 1) / pg * pg;
+    void * host = aligned_alloc(pg, hsz);
+    memset(host, 0, hsz);
+    memcpy(host, w, wbytes);
+    ggml_backend_buffer_t buf = ggml_backend_dev_buffer_from_host_ptr(dev, host, hsz, wbytes);
+    if (!buf) { free(host); return -1; }
+    void * wdev = nullptr, * xd = nullptr, * y0 = nullptr, * y1 = nullptr;
+    MI_CHECK(hipMalloc(&wdev, wbytes + 256));
+    MI_CHECK(hipMemset(wdev, 0, wbytes + 256));
+    MI_CHECK(hipMemcpy(wdev, w, wbytes, hipMemcpyHostToDevice));
+    MI_CHECK(hipMalloc(&xd, K * 4));
+    MI_CHECK(hipMemcpy(xd, x, K * 4, hipMemcpyHostToDevice));
+    MI_CHECK(hipMalloc(&y0, M * 4));
+    MI_CHECK(hipMalloc(&y1, M * 4));
+    int rc = 0;
+    {
+        scoped_ctx sc(nullptr);
+        ggml_tensor W0, W1, X, Y0, Y1;
+        const int64_t new_[4] = {K, M, 1, 1}, nex[4] = {K, 1, 1, 1}, ney[4] = {M, 1, 1, 1};
+        init_tensor(W0, GGML_TYPE_Q4_K, new_, ggml_backend_buffer_get_base(buf));
+        init_tensor(W1, GGML_TYPE_Q4_K, new_, wdev);
+        init_tensor(X, GGML_TYPE_F32, nex, xd);
+        init_tensor(Y0, GGML_TYPE_F32, ney, y0);
+        init_tensor(Y1, GGML_TYPE_F32, ney, y1);
+        Y0.op = Y1.op = GGML_OP_MUL_MAT;
+        Y0.src[0] = &W0; Y1.src[0] = &W1;
+        Y0.src[1] = Y1.src[1] = &X;
+        op_mul_mat(sc.ex, &Y0);
+        sc.ex.qcache_clear();
+        op_mul_mat(sc.ex, &Y1);
+        MI_CHECK(hipStreamSynchronize(sc.ex.stream));
+    }
+    std::vector<float> a(M), b(M);
+    MI_CHECK(hipMemcpy(a.data(), y0, M * 4, hipMemcpyDeviceToHost));
+    MI_CHECK(hipMemcpy(b.data(), y1, M * 4, hipMemcpyDeviceToHost));
+    if (memcmp(a.data(), b.data(), M * 4) != 0) rc = 1;
+    ggml_backend_buffer_free(buf);
+    free(host);
+    MI_CHECK(hipFree(wdev)); MI_CHECK(hipFree(xd)); MI_CHECK(hipFree(y0)); MI_CHECK(hipFree(y1));
+    return rc;
+}
+
 extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t b, int iters) {
     scoped_ctx sc(nullptr);
     hipEvent_t e0, e1;

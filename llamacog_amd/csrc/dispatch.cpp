@@ -6,6 +6,8 @@
 // node loop (the hot loop of SURVEY.md §3.1) and applies the fusions documented in
 // DESIGN.md (RMS_NORM + MUL).
 #include "ops.h"
+#include <atomic>
+#include <mutex>
 
 #include <algorithm>
 #include <cstdio>
@@ -149,6 +151,114 @@ void op_mul_mat(exec_ctx & ctx, ggml_tensor * dst) {
     }
 }
 
+
+// ---- row-split weights ------------------------------------------------------------------------
+// One helper execution context per physical device for the slices that live on another GPU
+// than the computing backend's (each has its own stream and scratch; enqueueing is serialised)
+struct split_helper { exec_ctx ex; std::mutex mtx; bool init = false; };
+static split_helper g_split_helpers[MI_MAX_DEV];
+
+static exec_ctx & split_helper_ctx(int hip, std::unique_lock<std::mutex> & lk) {
+    GGML_ASSERT(hip >= 0 && hip < MI_MAX_DEV);
+    split_helper & h = g_split_helpers[hip];
+    lk = std::unique_lock<std::mutex>(h.mtx);
+    if (!h.init) {
+        MI_CHECK(hipSetDevice(hip));
+        h.ex.device = hip;
+        MI_CHECK(hipStreamCreateWithFlags(&h.ex.stream, hipStreamNonBlocking));
+        h.init = true;
+    }
+    return h.ex;
+}
+
+// The mat-mul of one row slice [lo, hi) of a split weight against src1, into `out` (a
+// contiguous [hi - lo, T] f32 block), on execution context ex (whose device holds the slice)
+static void mul_mat_slice(exec_ctx & ex, const ggml_tensor * dst, const split_part & p, const ggml_tensor * src1, void * out) {
+    const ggml_tensor * src0 = dst->src[0];
+    ggml_tensor w = *src0;
+    w.ne[1] = p.hi - p.lo;
+    w.nb[2] = w.nb[3] = w.nb[1] * w.ne[1];
+    w.data = p.data;
+    w.buffer = nullptr;
+    w.extra = nullptr;
+    w.view_src = nullptr;
+    ggml_tensor y = *dst;
+    y.ne[0] = p.hi - p.lo;
+    y.nb[1] = y.ne[0] * sizeof(float);
+    y.nb[2] = y.nb[1] * y.ne[1];
+    y.nb[3] = y.nb[2] * y.ne[2];
+    y.data = out;
+    y.buffer = nullptr;
+    y.view_src = nullptr;
+    y.src[0] = &w;
+    y.src[1] = (ggml_tensor *) src1;
+    op_mul_mat(ex, &y);
+}
+
+static std::atomic<long> g_split_mm{0}, g_split_foreign{0};
+void split_stats(long * mm, long * foreign) {
+    if (mm) *mm = g_split_mm.load();
+    if (foreign) *foreign = g_split_foreign.load();
+}
+
+void op_mul_mat_split(exec_ctx & ctx, ggml_tensor * dst) {
+    split_parts sp;
+    GGML_ASSERT(tensor_split_parts(dst->src[0], sp));
+    g_split_mm.fetch_add(1);
+    const ggml_tensor * src1 = dst->src[1];
+    GGML_ASSERT(ggml_is_contiguous(src1) && ggml_is_contiguous(dst) && dst->ne[2] == 1 && dst->ne[3] == 1);
+    const int64_t T = dst->ne[1], M = dst->ne[0];
+    int64_t maxr = 0;
+    for (int i = 0; i < sp.n; ++i) maxr = std::max(maxr, sp.p[i].hi - sp.p[i].lo);
+    char * tmp = (char *) ctx.scratch(5, (size_t) maxr * T * sizeof(float));
+    for (int i = 0; i < sp.n; ++i) {
+        const split_part & p = sp.p[i];
+        const int64_t rows = p.hi - p.lo;
+        if (p.hip == ctx.device) {
+            // a slice in this device's memory (virtual devices of one GPU, or the main device's
+            // own share): a one-token output is a contiguous run of dst, a batch is gathered
+            if (T == 1) {
+                mul_mat_slice(ctx, dst, p, src1, (float *) dst->data + p.lo);
+            } else {
+                mul_mat_slice(ctx, dst, p, src1, tmp);
+                MI_CHECK(hipMemcpy2DAsync((char *) dst->data + p.lo * sizeof(float), M * sizeof(float), tmp, rows * sizeof(float),
+                                          rows * sizeof(float), T, hipMemcpyDeviceToDevice, ctx.stream));
+            }
+            continue;
+        }
+        // a slice on another GPU: src1 over to it (peer copy), the slice computed there on its
+        // helper stream, the rows back into this stream's staging, then gathered into dst
+        g_split_foreign.fetch_add(1);
+        std::unique_lock<std::mutex> lk;
+        exec_ctx & hx = split_helper_ctx(p.hip, lk);
+        hipEvent_t ein, eout;
+        MI_CHECK(hipSetDevice(ctx.device));
+        MI_CHECK(hipEventCreateWithFlags(&ein, hipEventDisableTiming));
+        MI_CHECK(hipEventRecord(ein, ctx.stream));
+        MI_CHECK(hipSetDevice(p.hip));
+        MI_CHECK(hipStreamWaitEvent(hx.stream, ein, 0));
+        const size_t b1 = ggml_nbytes(src1), bo = (size_t) rows * T * sizeof(float);
+        char * hbuf = (char *) hx.scratch(5, b1 + bo + 256);
+        MI_CHECK(hipMemcpyPeerAsync(hbuf, p.hip, src1->data, ctx.device, b1, hx.stream));
+        ggml_tensor x = *src1;
+        x.data = hbuf;
+        x.buffer = nullptr;
+        x.view_src = nullptr;
+        hx.qcache_clear();
+        mul_mat_slice(hx, dst, p, &x, hbuf + ((b1 + 255) / 256) * 256);
+        MI_CHECK(hipMemcpyPeerAsync(tmp, ctx.device, hbuf + ((b1 + 255) / 256) * 256, p.hip, bo, hx.stream));
+        MI_CHECK(hipEventCreateWithFlags(&eout, hipEventDisableTiming));
+        MI_CHECK(hipEventRecord(eout, hx.stream));
+        MI_CHECK(hipSetDevice(ctx.device));
+        MI_CHECK(hipStreamWaitEvent(ctx.stream, eout, 0));
+        MI_CHECK(hipMemcpy2DAsync((char *) dst->data + p.lo * sizeof(float), M * sizeof(float), tmp, rows * sizeof(float),
+                                  rows * sizeof(float), T, hipMemcpyDeviceToDevice, ctx.stream));
+        // the events are released once the stream has passed them
+        MI_CHECK(hipStreamSynchronize(ctx.stream));
+        MI_CHECK(hipEventDestroy(ein));
+        MI_CHECK(hipEventDestroy(eout));
+    }
+}
 
 static ggml_tensor * at(ggml_cgraph * g, int i, int n) { return i < n ? ggml_graph_node(g, i) : nullptr; }
 
@@ -755,7 +865,13 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
         case GGML_OP_PERMUTE:
         case GGML_OP_TRANSPOSE:
             return 1;
-        case GGML_OP_MUL_MAT:
+        case GGML_OP_MUL_MAT: {
+            split_parts sp;
+            if (tensor_split_parts(node->src[0], sp)) {   // -sm row weights
+                op_mul_mat_split(ctx, node);
+                return 1;
+            }
+        }
             if (fusion_enabled() && gemv_supported(node)) return op_gemv_grouped(ctx, cgraph, i, n);
             op_mul_mat(ctx, node);
             return 1;

@@ -912,6 +912,8 @@ static bool is_kq(ggml_type t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5
 bool gemv_supported(const ggml_tensor * mm) {
     const ggml_tensor * w = mm->src[0];
     const ggml_tensor * x = mm->src[1];
+    split_parts sp;
+    if (tensor_split_parts(w, sp)) return false;   // row-split weights: op_mul_mat_split, never grouped
     int per = 0;
     switch (w->type) {
         case GGML_TYPE_Q4_K: case GGML_TYPE_Q4_0:

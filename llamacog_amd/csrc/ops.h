@@ -30,9 +30,9 @@ struct exec_ctx {
     hipStream_t stream = nullptr;
 
     // scratch arena: slot i is a separate region so one op can hold several temps
-    static constexpr int N_SLOTS = 5;
-    void *  slot_ptr[N_SLOTS]  = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    size_t  slot_size[N_SLOTS] = {0, 0, 0, 0, 0};
+    static constexpr int N_SLOTS = 6;   // 5: row-split mat-mul staging (op_mul_mat_split)
+    void *  slot_ptr[N_SLOTS]  = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t  slot_size[N_SLOTS] = {0, 0, 0, 0, 0, 0};
     bool    capturing = false;   // hipGraph capture in progress: growing is forbidden
     // bumped whenever a slot is reallocated: a captured hipGraph holds slot addresses in its
     // kernel arguments, so graphs captured under an older generation are dropped (backend.cpp)
@@ -162,6 +162,16 @@ bool graphs_enabled();
 // blocks while any thread has a hipGraph capture open (backend.cpp)
 void wait_no_capture();
 bool ktrace_enabled();
+
+// row-split weights (backend.cpp, the split buffer type): the row slices [lo, hi) of a matrix,
+// one per device that holds rows, each in that device's memory (HIP device `hip`)
+constexpr int MI_MAX_DEV = 16;
+struct split_part { int hip; int64_t lo, hi; void * data; };
+struct split_parts { int n = 0; split_part p[MI_MAX_DEV]; };
+bool tensor_split_parts(const ggml_tensor * t, split_parts & sp);   // false: t is not in a split buffer
+// MUL_MAT whose src0 is row-split: each slice on its device, the rows gathered into dst (dispatch.cpp)
+void op_mul_mat_split(exec_ctx & ctx, ggml_tensor * dst);
+void split_stats(long * mm, long * foreign);   // row-split mat-muls run, and slices run on another GPU
 
 // supports / dispatch
 bool op_supported(const ggml_tensor * op);

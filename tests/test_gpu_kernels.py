@@ -185,6 +185,26 @@ def test_flash_attn_f16_llama_shapes_vs_oracle(K, n_kv, n_q, Hkv, G):
     assert_bits(out, ref, f"flash_attn f16 n_kv={n_kv} n_q={n_q}")
 
 
+def test_buffer_from_host_ptr_matvec_bit_exact():
+    """The device's buffer_from_host_ptr (hipHostRegister'd, mapped host memory): the decode
+    mat-vec reads q4_K weights in place over the host link and returns the same bits as with the
+    weights in HBM."""
+    import ctypes
+    import llamacog_amd as la
+    from llamacog_amd import gguf_synth as gs
+    rng = np.random.default_rng(3)
+    K, M = 4096, 256
+    blk, bs = gs.BLOCK[CPU_TYPES["q4_K"]]
+    w = gs.make_blocks(CPU_TYPES["q4_K"], M * K // blk, rng)
+    x = rng.standard_normal(K).astype(np.float32)
+    lib = la.plugin_lib()
+    f = lib.mi355x_check_host_ptr_matvec
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+    wb = np.ascontiguousarray(w)
+    assert f(wb.ctypes.data, K, M, x.ctypes.data) == 0
+
+
 @pytest.mark.parametrize("n_kv,Hkv,G,pattern", [(300, 4, 1, "holes"), (1000, 8, 2, "first_chunk_dead"),
                                                   (256, 8, 4, "single"), (129, 2, 4, "holes"), (4352, 8, 4, "sparse")])
 def test_flash_attn_f16_decode_masks_vs_oracle(K, n_kv, Hkv, G, pattern):

@@ -115,8 +115,9 @@ ids, lg = m.greedy(prompt, {n_gen})
 log = la.log_tail(m.lib, 1 << 20)
 m.close()
 np.save({out!r}, lg)
-print(json.dumps({{"devices": names, "handoffs": la.handoff_stats(),
-                   "pipeline": [l for l in log.splitlines() if "pipeline parallelism" in l or "graph splits" in l][-3:]}}))
+print(json.dumps({{"devices": names, "handoffs": la.handoff_stats(), "split": la.split_stats(),
+                   "pipeline": [l for l in log.splitlines() if "pipeline parallelism" in l or "graph splits" in l][-3:],
+                   "buffers": [l for l in log.splitlines() if "buffer size" in l][-8:]}}))
 """
 
 
@@ -163,6 +164,18 @@ def test_greedy_layer_split_virtual_devices_rccl(tmp_path):
     info = _vdev_greedy(tmp_path, "tiny-q4km", 16, 16, p2p="rccl")
     rccl, peer, d2d = info["handoffs"]
     assert rccl > 0 and d2d == 0, info
+
+
+@pytest.mark.parametrize("cfg", ["tiny-q4km", "llama3-8b-2l-q4km"])
+def test_greedy_row_split_virtual_devices_bit_identical(cfg, tmp_path):
+    """libllama's -sm row (LLAMA_SPLIT_MODE_ROW) over two ggml devices of this one GPU: the
+    weight matrices in our split buffer type (ggml_backend_split_buffer_type through the
+    registry's proc address), row slices on both devices, every mat-mul that reads one run slice
+    by slice by the main device's backend.  Logits bit-identical to the CPU backend."""
+    info = _vdev_greedy(tmp_path, cfg, 16, 12, split_mode=2)
+    mm, foreign = info["split"]
+    assert mm > 0 and foreign == 0, info   # virtual devices: every slice is on the one GPU
+    assert any("_Split" in l for l in info["buffers"]), info
 
 
 @pytest.mark.parametrize("cfg", ["tiny-q4km", "llama3-8b-2l-q4km"])
