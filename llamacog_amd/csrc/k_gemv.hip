@@ -601,11 +601,11 @@ __global__ __launch_bounds__(256) void k_gemv_os(const gemv_args p) {
     kt_exit(p.kt);
 }
 
-template <class T1, class T2, int R2, int WPR, bool PRO>
+template <class T1, class T2, int R2, int WPR, bool PRO, int R1 = 2>
 __global__ __launch_bounds__(256) void k_gemv_os2(const gemv_args p1, const int64_t ng1, const gemv_args p2) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
     kt_enter(p1.kt);
-    if ((int64_t) blockIdx.x < ng1) gemv_os_body<T1, 2, WPR, 1, PRO>(p1, blockIdx.x, (uint8_t *) xr + p1.wl_off, xr);
+    if ((int64_t) blockIdx.x < ng1) gemv_os_body<T1, R1, WPR, 1, PRO>(p1, blockIdx.x, (uint8_t *) xr + p1.wl_off, xr);
     else gemv_os_body<T2, R2, WPR, 1, PRO>(p2, (int64_t) blockIdx.x - ng1, (uint8_t *) xr + p2.wl_off, xr);
     kt_exit(p1.kt);
 }
@@ -763,20 +763,23 @@ static void launch_os(hipStream_t st, gemv_args & a, int nmat) {
 }
 
 // rows per wave of the one-shot kernel (tools/gemv_lab.hip, round 3): one row, except two for
-// the 4-bit K-quants at K = 14336 and wherever a norm prologue is formed per workgroup (half
-// the workgroups form it)
+// the 4-bit K-quants at K = 14336, and two (four at K <= 4096) wherever a norm prologue is formed
+// per workgroup (fewer workgroups form it)
 template <class T>
 static bool launch_os_t(hipStream_t st, gemv_args & a, int nmat) {
     if (!os_enabled() || a.tl.kind || !os_aligned<T>(a, nmat)) return false;
     const int wpr = wpr_of(a.ntasks);
     int R = 1;
     if (a.pro.x || (wpr == 4 && !std::is_same<T, g_q6_K>::value)) R = 2;
+    if (a.pro.x && wpr == 1) R = 4;   // a norm prologue per workgroup: half as many of them (9.9 -> 9.3 us)
     if (wpr == 4 && needs_epilogue(a, nmat)) return false;   // rope pairs need an even group
     gemv_args b = a;
-    const size_t lds = R == 2 ? (wpr == 1 ? os_lds_layout<T, 2, 1>(b) : wpr == 2 ? os_lds_layout<T, 2, 2>(b) : os_lds_layout<T, 2, 4>(b))
+    const size_t lds = R == 4 ? os_lds_layout<T, 4, 1>(b)
+                     : R == 2 ? (wpr == 1 ? os_lds_layout<T, 2, 1>(b) : wpr == 2 ? os_lds_layout<T, 2, 2>(b) : os_lds_layout<T, 2, 4>(b))
                               : (wpr == 1 ? os_lds_layout<T, 1, 1>(b) : wpr == 2 ? os_lds_layout<T, 1, 2>(b) : os_lds_layout<T, 1, 4>(b));
     if (lds > 64 * 1024) return false;
     switch (R * 8 + wpr) {
+        case 4 * 8 + 1: launch_os<T, 4, 1>(st, a, nmat); break;
         case 2 * 8 + 1: launch_os<T, 2, 1>(st, a, nmat); break;
         case 2 * 8 + 2: launch_os<T, 2, 2>(st, a, nmat); break;
         case 2 * 8 + 4: launch_os<T, 2, 4>(st, a, nmat); break;
@@ -788,11 +791,11 @@ static bool launch_os_t(hipStream_t st, gemv_args & a, int nmat) {
 }
 
 // two weight types in one one-shot launch: p1's matrices at two rows per wave, p2's at R2
-template <class T1, class T2, int R2, int WPR>
+template <class T1, class T2, int R2, int WPR, int R1 = 2>
 static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2, int n2) {
     constexpr int NWV = 4;
-    const int64_t ng1 = set_groups(a1, n1, (NWV / WPR) * 2), ng2 = set_groups(a2, n2, (NWV / WPR) * R2);
-    size_t rec = r16(std::max((size_t) (NWV / WPR) * 2 * (a1.ntasks / T1::per_block) * T1::RS * 4,
+    const int64_t ng1 = set_groups(a1, n1, (NWV / WPR) * R1), ng2 = set_groups(a2, n2, (NWV / WPR) * R2);
+    size_t rec = r16(std::max((size_t) (NWV / WPR) * R1 * (a1.ntasks / T1::per_block) * T1::RS * 4,
                               (size_t) (NWV / WPR) * R2 * (a2.ntasks / T2::per_block) * T2::RS * 4));
     size_t off = rec;
     if (a1.pro.x) {
@@ -800,12 +803,12 @@ static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2,
         off = r16(off + pro_lds_bytes(a1.pro.n, a1.pro.qmode));
     }
     a1.wl_off = a2.wl_off = (uint32_t) off;
-    const size_t lds = off + std::max((size_t) 4 * 2 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
+    const size_t lds = off + std::max((size_t) 4 * R1 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
     a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv2+pro+epi", (unsigned) (ng1 + ng2), 64 * NWV) : nullptr;
 #define OS2_LAUNCH(P)                                                                                                 \
-    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P>), dim3((unsigned) (ng1 + ng2)), dim3(64 * NWV), lds, st, t_ev_beg, \
+    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P, R1>), dim3((unsigned) (ng1 + ng2)), dim3(64 * NWV), lds, st, t_ev_beg, \
                                         t_ev_end, 0, a1, ng1, a2);                                                        \
-    else hipLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P>), dim3((unsigned) (ng1 + ng2)), dim3(64 * NWV), lds, st, a1, ng1, a2)
+    else hipLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P, R1>), dim3((unsigned) (ng1 + ng2)), dim3(64 * NWV), lds, st, a1, ng1, a2)
     if (a1.pro.x) { OS2_LAUNCH(true); } else { OS2_LAUNCH(false); }
 #undef OS2_LAUNCH
 }
@@ -873,7 +876,9 @@ static bool launch_pipe2_t(hipStream_t st, gemv_args & a1, int n1, gemv_args & a
     for (int i = 0; i < n2; ++i) m2 += a2.M[i];
     if (os_enabled() && os_aligned<T1>(a1, n1) && os_aligned<T2>(a2, n2)) {
         // one-shot: the second type at one row per wave (two rows for the prologue consumers)
-        if (wpr == 1 && a1.pro.x) launch_os2_v<T1, T2, 2, 1>(st, a1, n1, a2, n2);
+        // with the norm prologue formed per workgroup: four rows per wave for the first type (half
+        // the prologues; Q/K/V 10.1 -> 9.1 us, in-graph timeline round 3), two for the second
+        if (wpr == 1 && a1.pro.x) launch_os2_v<T1, T2, 2, 1, 4>(st, a1, n1, a2, n2);
         else if (wpr == 1) launch_os2_v<T1, T2, 1, 1>(st, a1, n1, a2, n2);
         else launch_os2_v<T1, T2, 1, 2>(st, a1, n1, a2, n2);
         return true;
