@@ -302,17 +302,6 @@ static bool can_hoist(ggml_cgraph * g, int i, int j, const ggml_tensor * const *
     return true;
 }
 
-// SiLU node that directly follows MUL_MAT node i and reads exactly its output, or nullptr
-static ggml_tensor * silu_after(ggml_cgraph * g, int i, int n) {
-    ggml_tensor * mm = ggml_graph_node(g, i);
-    ggml_tensor * nx = at(g, i + 1, n);
-    if (nx && nx->op == GGML_OP_UNARY && ggml_get_unary_op(nx) == GGML_UNARY_OP_SILU && nx->src[0] == mm &&
-        nx->type == GGML_TYPE_F32 && ggml_is_contiguous(nx) && ggml_are_same_shape(nx, mm)) {
-        return nx;
-    }
-    return nullptr;
-}
-
 // base node of a (chain of) view/reshape nodes
 static const ggml_tensor * base_of(const ggml_tensor * t) {
     while (t && t->view_src) t = t->view_src;
@@ -473,8 +462,7 @@ static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tenso
     // gate/up, 28672 rows; the output head) that is thousands of redundant norms, and the
     // stand-alone norm kernel plus a prologue-free launch measured faster (round 3 kernel
     // timeline: gate/up 27.0 us with the prologue vs 15 + 4 without); Q/K/V keep it
-    static const int64_t pro_max = getenv("GGML_MI355X_PRO_MAX_ROWS") ? atoll(getenv("GGML_MI355X_PRO_MAX_ROWS")) : 16384;
-    if (rows > pro_max) return;
+    if (rows > 16384) return;
     if (!dead_after(g, n, pl + 1, last, readers)) return;
     if (mul && !dead_after(g, n, pn + 1, nm, {mul})) return;
     double * site = gemv_rsum_site(ctx);
@@ -564,23 +552,12 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     std::vector<const ggml_tensor *> absorbed;   // nodes this launch computes (besides node i)
     std::vector<const ggml_tensor *> outs = {mm0};
 
-    // epilogues of matrix m (node position pm): silu, or rope (+ its cache store), or a cache store
+    // epilogues of matrix m (node position pm): rope (+ its cache store), or a cache store.  (The
+    // SiLU of a gate projection is left to the FFN-product kernel, op_compute GGML_OP_UNARY, which
+    // forms silu(gate)*up in one pass: as an epilogue it parked the row sums and cost the 66 MB
+    // gate/up launch ~2 us, round 2)
     auto add_epilogues = [&](int m, int pm) {
         ggml_tensor * mm = mms[m];
-        // SiLU of the gate projection: by default left to the FFN-product kernel (op_compute,
-        // GGML_OP_UNARY), which forms silu(gate)*up in one pass — the epilogue parks the row
-        // sums and costs the 66 MB gate/up launch ~2 us (scripts/probe_mall.py);
-        // GGML_MI355X_SILU_EPI=1 keeps it in the GEMV
-        static const bool silu_epi = getenv("GGML_MI355X_SILU_EPI") && atoi(getenv("GGML_MI355X_SILU_EPI")) != 0;
-        if (ggml_tensor * sl = silu_epi ? silu_after(g, pm, n) : nullptr) {
-            const ggml_tensor * o[1] = {sl};
-            if (!overlaps_any(sl, outs, mm) && (pm == i || can_hoist(g, i, pm + 1, o, 1, absorbed))) {
-                epi.silu[m] = sl;
-                absorbed.push_back(sl);
-                outs.push_back(sl);
-            }
-            return;
-        }
         if (ggml_tensor * r = rope_of(g, mm, pm, n)) {
             const ggml_tensor * o[1] = {r};
             const int pr = node_index(g, r);

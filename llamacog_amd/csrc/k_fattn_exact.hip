@@ -1,5 +1,5 @@
-// k_fattn_exact.hip — CPU-exact flash attention over an f16 or q8_0 KV cache (the default; the
-// split-K f32 kernel in k_fattn.hip is selected with GGML_MI355X_FA_FAST=1).
+// k_fattn_exact.hip — CPU-exact flash attention over an f16, q8_0 or q4_0 KV cache (every
+// FLASH_ATTN_EXT the backend takes runs here).
 //
 // Reproduces ggml_compute_forward_flash_attn_ext_f16 (ggml-cpu/ops.cpp:7015-7232) as the
 // x86-64-v4 (AVX-512) CPU backend computes it — the variant the reference selects on the
@@ -1215,12 +1215,11 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     GGML_ASSERT(a0.H % a0.Hkv == 0);
     fa_args a = a0;
     const dim3 grid((unsigned) a.n_q, (unsigned) (a.H * nq3));
-    static const int pocc = getenv("GGML_MI355X_FA_PREFILL_OCC") ? atoi(getenv("GGML_MI355X_FA_PREFILL_OCC")) : 2;
-    // prefill chunk: GGML_MI355X_FA_PREFILL_CH = 128 (default: 32 KiB of V in LDS; half the
-    // phase-1 K registers, so OCC 2 fits 256 VGPRs without the 40 spills of CH 256 — pp512
-    // 9.6k -> 10.6k tok/s; OCC 3/4 spill and run slower, 8.5k / 8.2k) or 256 (64 KiB)
-    static const int pch = getenv("GGML_MI355X_FA_PREFILL_CH") ? atoi(getenv("GGML_MI355X_FA_PREFILL_CH")) : 128;
-    const bool wide = a.n_q * a.H * nq3 > 256 && pocc >= 2;   // prefill: more workgroups than CUs
+    // prefill (more workgroups than CUs): two workgroups per CU and a 128-position chunk (32 KiB
+    // of V in LDS; half the phase-1 K registers of a 256 chunk, so occupancy 2 fits 256 VGPRs
+    // without its 40 spills — pp512 9.6k -> 10.6k tok/s, round 2; occupancy 3 / 4 spilled and ran
+    // slower, 8.5k / 8.2k)
+    const bool wide = a.n_q * a.H * nq3 > 256;
     if (a.k_type == GGML_TYPE_Q4_0) {
         switch (a.D) {
             case 64:  hipLaunchKernelGGL((k_fattn_exact<64, 1, 0, true, true>), grid, dim3(256), 0, st, a); break;
@@ -1245,11 +1244,9 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
         }
         return;
     }
-    // prefill, f16 cache, D = 128: query blocks x the GQA group (GGML_MI355X_FA_PF=0: one
-    // workgroup per query row and head)
-    static const bool pf_on = !getenv("GGML_MI355X_FA_PF") || atoi(getenv("GGML_MI355X_FA_PF")) != 0;
+    // prefill, f16 cache, D = 128: query blocks x the GQA group
     const int64_t G = a.H / a.Hkv;
-    if (pf_on && a.D == 128 && a.n_q >= 16 && a.qmode == 0 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) {
+    if (a.D == 128 && a.n_q >= 16 && a.qmode == 0 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) {
         const dim3 g((unsigned) ceil_div(a.n_q, (int64_t) PF_P / G), (unsigned) (a.Hkv * nq3));
         switch (G) {
             case 1:  hipLaunchKernelGGL(k_fattn_pf<1>, g, dim3(256), 0, st, a); break;
@@ -1264,10 +1261,7 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
         case 64:  hipLaunchKernelGGL(k_fattn_exact<64>, grid, dim3(256), 0, st, a); break;
         case 128:
             if (!wide) hipLaunchKernelGGL(k_fattn_exact<128>, grid, dim3(256), 0, st, a);
-            else if (pch == 128 && pocc == 4) hipLaunchKernelGGL((k_fattn_exact<128, 4, 128>), grid, dim3(256), 0, st, a);
-            else if (pch == 128 && pocc == 3) hipLaunchKernelGGL((k_fattn_exact<128, 3, 128>), grid, dim3(256), 0, st, a);
-            else if (pch == 128) hipLaunchKernelGGL((k_fattn_exact<128, 2, 128>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((k_fattn_exact<128, 2>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((k_fattn_exact<128, 2, 128>), grid, dim3(256), 0, st, a);
             break;
         case 256: hipLaunchKernelGGL(k_fattn_exact<256>, grid, dim3(256), 0, st, a); break;
         default: GGML_ABORT("mi355x: FA head size %d", (int) a.D);

@@ -198,13 +198,10 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     } else {
         p.qs = nullptr; p.qd = nullptr; p.qsum = nullptr;
     }
-    // GGML_MI355X_NORM_BT: threads per row (default 1024; 512 / 256 measured no faster on
-    // Llama-3-8B decode, 371-374 / 352 tok/s vs 347-382, scripts/gpu_norm_bt.sh); fewer threads take several float4
-    // per thread.  The canonical slice order j = w + NW k is the same for every split, so the
-    // bits do not change
-    static const int nbt = getenv("GGML_MI355X_NORM_BT") ? atoi(getenv("GGML_MI355X_NORM_BT")) : 1024;
-    int nv = ne0 <= 4096 ? 1 : (int) (ne0 / 4096);
-    if ((nbt == 256 || nbt == 512) && ne0 % (4 * nbt) == 0 && ne0 / (4 * nbt) <= 4) nv = (int) (ne0 / (4 * nbt));
+    // up to 1024 threads per row, one float4 each (512 / 256 threads with several float4 each
+    // measured no faster on Llama-3-8B decode, round 2); the canonical slice order j = w + NW k
+    // is the same for every split, so the bits would not change
+    const int nv = ne0 <= 4096 ? 1 : (int) (ne0 / 4096);
     const dim3 block((unsigned) (ne0 / (4 * nv)));
     p.nrows = nrows;
     const dim3 grid((unsigned) nrows);

@@ -619,13 +619,13 @@ static thread_local hipEvent_t t_ev_beg = nullptr, t_ev_end = nullptr;
 // the launching context while a gemv_group runs (kernel timeline regions come from it)
 static thread_local exec_ctx * g_kt_ctx = nullptr;
 
-static int g_gemv_wgs = -1;    // GGML_MI355X_GEMV_WGS: persistent grid size
+static int g_gemv_wgs = -1;    // the pipelined kernel's persistent grid (2048: 8 per CU)
 static int g_num_cu = 0;
 static std::once_flag g_gemv_once;   // several contexts may launch from several threads
 
 static void gemv_init() {
     std::call_once(g_gemv_once, [] {
-        g_gemv_wgs = getenv("GGML_MI355X_GEMV_WGS") ? atoi(getenv("GGML_MI355X_GEMV_WGS")) : 2048;
+        g_gemv_wgs = 2048;
         int dev = 0;
         hipDeviceProp_t prop;
         MI_CHECK(hipGetDevice(&dev));
@@ -651,18 +651,12 @@ static void launch_pipe_m(hipStream_t st, gemv_args & a, int nmat) {
         // workgroups beats 2048 single-group workgroups in two rounds (Q4_K 4096 x 14336: 12.0 ->
         // 11.2 us at 5 per CU, scripts/probe_geom.py); with the residual producer's epilogue 3 per
         // CU (768) is faster again, 12.5 -> 11.2 us (scripts/gpu_trace_var.sh, round 2)
-        static const int wgs4 = getenv("GGML_MI355X_GEMV_WGS4") ? atoi(getenv("GGML_MI355X_GEMV_WGS4")) : 3 * g_num_cu;
-        if (wgs4 > 0) grid = std::min<int64_t>(ng, wgs4);
-    }
-    if constexpr (WPR == 4 && std::is_same<T, g_q6_K>::value) {
-        static const int wgs6 = getenv("GGML_MI355X_GEMV_WGS4Q6") ? atoi(getenv("GGML_MI355X_GEMV_WGS4Q6")) : 0;
-        if (wgs6 > 0) grid = std::min<int64_t>(ng, wgs6);
+        grid = std::min<int64_t>(ng, 3 * g_num_cu);
     }
     if (a.pro.x) {
-        // every workgroup forms the activation: one resident round (GGML_MI355X_PRO_WGS), so no
+        // every workgroup forms the activation: one resident round (1024), so no
         // workgroup pays the prologue after the weight stream is under way
-        static const int pro_wgs = getenv("GGML_MI355X_PRO_WGS") ? atoi(getenv("GGML_MI355X_PRO_WGS")) : 1024;
-        if (pro_wgs > 0) grid = std::min<int64_t>(grid, pro_wgs);
+        grid = std::min<int64_t>(grid, 1024);
     }
     if (MODE >= 1 || a.tl.kind) grid = std::max<int64_t>(grid, ceil_div(ng, GEMV_MAXG));   // LDS-parked row sums / tail lists
     size_t lds = 4 * xrec_dwords<T>(RPG, a.ntasks / T::per_block);
@@ -904,9 +898,8 @@ static bool launch_mixed(hipStream_t st, ggml_type t1, gemv_args & a1, int n1, g
 }
 
 bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c) {
-    static const int on = getenv("GGML_MI355X_GEMV_MIXED") ? atoi(getenv("GGML_MI355X_GEMV_MIXED")) : 1;
     const ggml_type t1 = mm0->src[0]->type, t2 = c->src[0]->type;
-    return on && ((t1 == GGML_TYPE_Q4_K && (t2 == GGML_TYPE_Q6_K || t2 == GGML_TYPE_Q5_K)) ||
+    return ((t1 == GGML_TYPE_Q4_K && (t2 == GGML_TYPE_Q6_K || t2 == GGML_TYPE_Q5_K)) ||
                   (t1 == GGML_TYPE_Q5_K && t2 == GGML_TYPE_Q6_K));
 }
 

@@ -11,7 +11,7 @@
 // which flips qs, d and bsums together and leaves every product unchanged; qtypes.h).
 //
 // Tiles: Q4_K MUL_MAT runs the f16-operand tile (k_mmq_f16.hip); Q4_K MUL_MAT_ID (expert-sorted
-// pairs, all gemv order) and GGML_MI355X_MMQ_F16=0 run the int8 scale-folded tile below
+// pairs, all gemv order) runs the int8 scale-folded tile below
 // (v_mfma_i32_16x16x64_i8); Q6_K / Q5_K run the class-exact tile (the vec_dot order).
 // MFMA layouts (tools/mfma_layout.hip, tools/mfma_probe.hip): 16x16x32 i8 / f16 lane l holds
 // A[row l&15][k 8(l>>4)+j], B[k 8(l>>4)+j][col l&15]; 16x16x64 i8 k 16(l>>4)+j;
@@ -626,12 +626,9 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
     p.gemm_cols = p.T - p.T % 4;   // repack.cpp:1261-1274
     p.dst = (float *) dst->data; p.nb1 = dst->nb[1];
     p.cnt = p.off = p.list = nullptr; p.n_used = 1; p.nb02 = 0; p.nb2 = 0;
-    // Q4_K: the f16-operand tile (GGML_MI355X_MMQ_F16=0: the int8 one)
-    static const bool f16_on = !getenv("GGML_MI355X_MMQ_F16") || atoi(getenv("GGML_MI355X_MMQ_F16")) != 0;
-    if (w->type == GGML_TYPE_Q4_K && f16_on) {
-        // GGML_MI355X_MMQ_NW=8: 128-token workgroups of 8 waves (the fold is shared by twice the tokens)
-        static const int nw = getenv("GGML_MI355X_MMQ_NW") ? atoi(getenv("GGML_MI355X_MMQ_NW")) : 4;
-        launch_mmq_q4Kh(ctx.stream, p, nw);
+    // Q4_K: the f16-operand tile, 64-token workgroups of four waves
+    if (w->type == GGML_TYPE_Q4_K) {
+        launch_mmq_q4Kh(ctx.stream, p, 4);
     } else {
         const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(p.T, MQ_BN));
         launch_mmq(ctx.stream, w->type, grid, p);

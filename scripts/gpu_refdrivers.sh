@@ -2,7 +2,7 @@
 #   * tests/test_refhost_drivers.py (llama-bench / llama-cli with the plugin via GGML_BACKEND_PATH);
 #   * refhost llama-bench -p 512 -n 128 -ngl 99 -fa 1 on the Llama-3-8B Q4_K_M synthetic GGUF;
 #   * config 1: stories15M Q8_0 on ggml-cpu through llama-bench (no plugin);
-#   * tg at KV depth 4096 (bench.py --depth 4096), exact FA and the split-K FA.
+#   * tg at KV depth 4096 (bench.py --depth 4096).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd $R
@@ -18,5 +18,3 @@ timeout -k 10 300 refhost/build/llama-bench -m $M/stories15m-q8_0-s0.gguf -p 512
 cat $OUT/llama_bench_stories15m_cpu.md
 timeout -k 10 600 python bench.py --depth 4096 --steps 32 --warmup 4 --pp 0 --no-cpu-baseline --roofline-steps 8 > $OUT/bench_depth4096.json 2> $OUT/bench_depth4096.err || { tail -20 $OUT/bench_depth4096.err; exit 1; }
 python3 -c "import json; d=json.load(open('$OUT/bench_depth4096.json')); print('depth4096 exact FA', d['value'], d['roofline']['fattn_avg_us'], d['step_split_ms'])"
-GGML_MI355X_FA_FAST=1 timeout -k 10 600 python bench.py --depth 4096 --steps 32 --warmup 4 --pp 0 --no-cpu-baseline --roofline-steps 8 > $OUT/bench_depth4096_fafast.json 2> $OUT/bench_depth4096_fafast.err || { tail -20 $OUT/bench_depth4096_fafast.err; exit 1; }
-python3 -c "import json; d=json.load(open('$OUT/bench_depth4096_fafast.json')); print('depth4096 split-K FA', d['value'], d['roofline']['fattn_avg_us'])"

@@ -1,5 +1,6 @@
 """Decode GEMV geometry on the Llama-3-8B FFN shapes (cold weights, mi355x_bench_gemv2 kind 0):
-run once per GEMV knob setting (GGML_MI355X_GEMV_WGS / _BAL / _R4W in the environment)."""
+one launch per shape, timed with HIP events; under `rocprofv3 --pmc FETCH_SIZE` it is the
+traffic calibration run (scripts/pmc_calib.py)."""
 import ctypes
 import os
 import sys
