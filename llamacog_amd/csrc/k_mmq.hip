@@ -628,7 +628,7 @@ void mul_mat_q(exec_ctx & ctx, ggml_tensor * dst) {
     p.cnt = p.off = p.list = nullptr; p.n_used = 1; p.nb02 = 0; p.nb2 = 0;
     // Q4_K: the f16-operand tile, 64-token workgroups of four waves
     if (w->type == GGML_TYPE_Q4_K) {
-        launch_mmq_q4Kh(ctx.stream, p, 4);
+        launch_mmq_q4Kh(ctx.stream, p);
     } else {
         const dim3 grid((unsigned) ceil_div(p.M, MQ_BM), (unsigned) ceil_div(p.T, MQ_BN));
         launch_mmq(ctx.stream, w->type, grid, p);

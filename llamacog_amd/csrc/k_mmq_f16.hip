@@ -16,8 +16,8 @@ namespace mi355x {
 // sums of 16 Q8_K values (|sum| <= 2048: exact f16) with the sums outside the pair zeroed.
 // 64 rows x 64 tokens per workgroup of 4 waves (two workgroups per CU); wave w multiplies the 64
 // rows with tokens 16w .. +15.  The folded weight planes are the only LDS data (double-buffered: the fold of
-// block b+1 overlaps block b, one barrier per block; 16-byte chunk c of row r in slot c ^ (r & 15)
-// so every ds_read_b128 lane group hits distinct banks); each wave streams its 16 tokens' Q8_K
+// block b+1 overlaps block b, one barrier per block; 16-byte chunks swizzled by mh_slot so the
+// reads and the fold's stores are conflict-free); each wave streams its 16 tokens' Q8_K
 // bytes straight into registers one block ahead and widens them to f16 there
 // ((0x6400 | (y ^ 0x80)) - 1152 = y, exact).
 constexpr int MH_BM = 64;
@@ -31,6 +31,12 @@ struct mh_tok {   // one K block of a lane's token: bytes 64pp + 16h .. +15 per 
     uint2 s;
     float d;
 };
+
+// LDS slot of 16-byte chunk ch (0..31) of plane row `row`: ch ^ (row & 15) makes the 16 lanes of an
+// MFMA A-fragment read (rows c16 = 0..15) hit distinct bank groups; the extra 2·(ch >> 3) makes the
+// fold's ds_write_b128 (8-lane groups = two rows x four pairs, chunks 8fq + k) distinct too (without
+// it four lanes of a group shared a bank group: 4-way conflicts on every fold store)
+__device__ __forceinline__ int mh_slot(int row, int ch) { return ch ^ (row & 15) ^ (2 * (ch >> 3)); }
 
 // 8 int8 (two words) -> 8 f16, exact
 __device__ __forceinline__ mh8 i8x8_f16(uint32_t w0, uint32_t w1) {
@@ -46,27 +52,30 @@ __device__ __forceinline__ mh8 i8x8_f16(uint32_t w0, uint32_t w1) {
     return __builtin_bit_cast(mh8, r);
 }
 
-template <int NW>   // waves: 4 (64 tokens, two workgroups per CU) or 8 (128 tokens, one)
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmq_q4Kh(const mmq_args p) {
-    constexpr int BN = 16 * NW;
+// ALLG: every token of the grid takes the gemm order.  (Loading the tokens two or three blocks
+// ahead instead of one measured 4-7 % slower: 52.9 / 54.4 vs 50.8 us at M = 4096, T = 512.)
+template <bool ALLG>
+__global__ __launch_bounds__(256, 2) void k_mmq_q4Kh(const mmq_args p) {
+    constexpr int NW = 4, BN = 16 * NW;
     __shared__ __attribute__((aligned(16))) uint8_t wpl[2][MH_BM * 512];
     __shared__ __attribute__((aligned(16))) uint32_t wmn[2][MH_BM][4];   // f16 (m_2p, m_2p+1) per pair
     __shared__ __attribute__((aligned(16))) float wd[2][MH_BM], wdm[2][MH_BM];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int64_t bx = blockIdx.x, by = blockIdx.y;
-    if ((gridDim.x & 7) == 0) {   // XCD-major: one row tile's token tiles on one XCD
+    if (ALLG && (gridDim.x & 7) == 0) {   // XCD-major: one row tile's token tiles on one XCD
         const int64_t id = bx + (int64_t) gridDim.x * by, j = id >> 3;
         by = j % gridDim.y;
         bx = (j / gridDim.y) * 8 + (id & 7);
     }
-    const int64_t row0 = bx * MH_BM, tok0 = by * BN, T = p.T;
+    // ALLG: every token of the grid takes the gemm order (the tiles below gemm_cols); otherwise
+    // the grid is the ragged tail from token tile p.ty0 on, the order chosen per token
+    const int64_t row0 = bx * MH_BM, tok0 = (ALLG ? by : by + p.ty0) * BN, T = p.T;
     const int h = lane >> 4, c16 = lane & 15;
-    const int tg = wave, rg = 0;   // wave w: the 64 rows x tokens 16w .. +15
+    const int tg = wave;   // wave w: the 64 rows x tokens 16w .. +15
     const int64_t KB = p.K / 256;
     const int64_t tok = tok0 + 16 * tg + c16;                // this lane's token
     const bool gemm = tok < p.gemm_cols;
-    const bool allg = tok0 + 16 * tg + 15 < p.gemm_cols;     // uniform: the wave's 16 tokens all gemm-order
 
     // token side: straight to registers
     const int64_t tl = min(tok, T - 1);
@@ -79,16 +88,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmq_q4Kh(const mmq
         o.s = *(const uint2 *) (srow + b * 16);
         o.d = drow_[b];
     };
-    // weight side: thread (row fr, pair fq[, byte half fh]) folds 64 (NW = 8: 32) weights into f16
-    constexpr int FT = NW == 4 ? 4 : 8;   // fold threads per row
-    const int fr = tid / FT, fq = (tid % FT) / (FT / 4), fh = NW == 4 ? 0 : tid & 1;
+    // weight side: thread (row fr, pair fq) folds 64 weights into f16
+    const int fr = tid / 4, fq = tid % 4;
     const uint8_t * wrow = p.W + min(row0 + fr, p.M - 1) * p.nb01;
     uint4 whdr, wqa, wqb;
     auto load_w = [&](int64_t b) __attribute__((always_inline)) {
         const uint8_t * blk = wrow + b * 144;
         whdr = ld16(blk);
-        wqa = ld16(blk + 16 + 32 * fq + 16 * fh);
-        if constexpr (NW == 4) wqb = ld16(blk + 32 + 32 * fq);
+        wqa = ld16(blk + 16 + 32 * fq);
+        wqb = ld16(blk + 32 + 32 * fq);
     };
     auto fold_w = [&](int buf) __attribute__((always_inline)) {
         int sc_lo, sc_hi, m_lo, m_hi;
@@ -96,32 +104,27 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmq_q4Kh(const mmq
         uint8_t * dp = wpl[buf] + fr * 512;
         // (1024 + q)·sc - 1024·sc = q·sc, one rounding of an exact f16 value.  Chunk 8fq + k of the
         // row: k < 4 low nibbles of qs bytes 8k .. 8k+7 of the pair (sub-block 2fq), k >= 4 high
-        constexpr int NK = NW == 4 ? 8 : 4;
 #pragma unroll
-        for (int kk = 0; kk < NK; ++kk) {
-            const int half = NW == 4 ? kk >> 2 : kk >> 1;
-            const int kq = NW == 4 ? kk & 3 : (kk & 1);            // 8-byte group within this thread's bytes
-            const int k = NW == 4 ? kk : 4 * half + 2 * fh + kq;   // chunk within the pair
+        for (int k = 0; k < 8; ++k) {
+            const int half = k >> 2, kq = k & 3;
             const _Float16 sc = (_Float16) (half ? sc_hi : sc_lo);
             const mh2 s2 = {sc, sc}, n2 = {(_Float16) -1024.0f * sc, (_Float16) -1024.0f * sc};
             uint32_t o[4];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int wi = 2 * kq + u;
-                const uint32_t w = NW == 4 ? (wi < 4 ? (&wqa.x)[wi] : (&wqb.x)[wi - 4]) : (&wqa.x)[wi];
+                const uint32_t w = wi < 4 ? (&wqa.x)[wi] : (&wqb.x)[wi - 4];
                 const uint32_t nb = half ? (w >> 4) & 0x0f0f0f0fu : w & 0x0f0f0f0fu;
                 const mh2 lo = __builtin_bit_cast(mh2, __builtin_amdgcn_perm(0x64646464u, nb, 0x04010400u));
                 const mh2 hi = __builtin_bit_cast(mh2, __builtin_amdgcn_perm(0x64646464u, nb, 0x04030402u));
                 o[2 * u] = __builtin_bit_cast(uint32_t, __builtin_elementwise_fma(lo, s2, n2));
                 o[2 * u + 1] = __builtin_bit_cast(uint32_t, __builtin_elementwise_fma(hi, s2, n2));
             }
-            *(uint4 *) (dp + 16 * ((8 * fq + k) ^ (fr & 15))) = make_uint4(o[0], o[1], o[2], o[3]);
+            *(uint4 *) (dp + 16 * mh_slot(fr, 8 * fq + k)) = make_uint4(o[0], o[1], o[2], o[3]);
         }
-        if (fh == 0) {
-            const mh2 mm = {(_Float16) m_lo, (_Float16) m_hi};
-            wmn[buf][fr][fq] = __builtin_bit_cast(uint32_t, mm);
-            if (fq == 0) { wd[buf][fr] = h2f(whdr.x & 0xffff); wdm[buf][fr] = h2f(whdr.x >> 16); }
-        }
+        const mh2 mm = {(_Float16) m_lo, (_Float16) m_hi};
+        wmn[buf][fr][fq] = __builtin_bit_cast(uint32_t, mm);
+        if (fq == 0) { wd[buf][fr] = h2f(whdr.x & 0xffff); wdm[buf][fr] = h2f(whdr.x >> 16); }
     };
 
     float A[4][4], B[4][4];   // [row tile][row 4h + i]
@@ -130,122 +133,113 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmq_q4Kh(const mmq
 #pragma unroll
         for (int i = 0; i < 4; ++i) A[r][i] = B[r][i] = 0.0f;
 
-    auto compute = [&](int buf, const mh_tok & x, auto allg_c) __attribute__((always_inline)) {
-        constexpr bool ALLG = decltype(allg_c)::value;
+    // pair-outer order: for each pair pp, the token's pair bytes become two f16 B fragments and
+    // the four row tiles multiply them; every chain A[r][i] / B[r][i] still takes the pairs in
+    // order 0..3, so the bits are those of the row-tile-outer order
+    auto compute = [&](int buf, const mh_tok & x) __attribute__((always_inline)) {
         const uint8_t * pl = wpl[buf];
-        // the token's block as f16 fragments, and its 16-sums (|sum| <= 2048: exact f16) — per
-        // pair pp only slots 4pp .. 4pp+3, held by lanes h == pp
-        mh8 bf[4][2];
-        mh4 bz[4];
-        {
-            const mh4 sf = {(_Float16) (int16_t) (x.s.x & 0xffff), (_Float16) (int16_t) (x.s.x >> 16),
-                            (_Float16) (int16_t) (x.s.y & 0xffff), (_Float16) (int16_t) (x.s.y >> 16)};
-#pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-                bf[pp][0] = i8x8_f16(x.x[pp].x, x.x[pp].y);
-                bf[pp][1] = i8x8_f16(x.x[pp].z, x.x[pp].w);
-                bz[pp] = h == pp ? sf : (mh4){0, 0, 0, 0};
-            }
-        }
-        // row tile r's LDS operands (A fragments, d / dmin, mins) are read while tile r-1 computes
-        mh8 af[2][4][2];
-        float4 dwv[2], dmv[2];
-        uint32_t wmv[2];
-        auto lda = [&](int r, int sl) __attribute__((always_inline)) {
-            const int rb = 64 * rg + 16 * r;
-            const uint8_t * ar = pl + (rb + c16) * 512;
-#pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-                af[sl][pp][0] = *(const mh8 *) (ar + 16 * ((8 * pp + 2 * h) ^ c16));
-                af[sl][pp][1] = *(const mh8 *) (ar + 16 * ((8 * pp + 2 * h + 1) ^ c16));
-            }
-            dwv[sl] = *(const float4 *) &wd[buf][rb + 4 * h];
-            dmv[sl] = *(const float4 *) &wdm[buf][rb + 4 * h];
-            wmv[sl] = wmn[buf][rb + c16][h];
-        };
-        lda(0, 0);
+        // the CPU's scale products d·dy, dmin·dy of rows 16r + 4h + i, and the mins operand of row
+        // 16r + c16 (slots 4h .. 4h+3 are sub-blocks 2h, 2h, 2h+1, 2h+1)
+        float sA[4][4], sB[4][4];
+        mh4 mA[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int sl = r & 1;
-            if (r < 3) lda(r + 1, sl ^ 1);
-            __builtin_amdgcn_sched_barrier(0);   // the next tile's reads are in flight; bounded live ranges
-            // the CPU's scale products d·dy, dmin·dy of rows rb + 4h + i
-            const float sA[4] = {dwv[sl].x * x.d, dwv[sl].y * x.d, dwv[sl].z * x.d, dwv[sl].w * x.d};
-            const float sB[4] = {dmv[sl].x * x.d, dmv[sl].y * x.d, dmv[sl].z * x.d, dmv[sl].w * x.d};
-            // mins operand of row rb + c16: slots 4h .. 4h+3 are sub-blocks 2h, 2h, 2h+1, 2h+1
-            const uint32_t w = wmv[sl];
-            const mh4 mA = __builtin_bit_cast(mh4, make_uint2(__builtin_amdgcn_perm(w, w, 0x01000100u), __builtin_amdgcn_perm(w, w, 0x03020302u)));
-            int ib[4], mb[4];   // gemv-order sums (exact ints: a block's I can pass 2^24)
-            if constexpr (!ALLG) {
+            const float4 dw = *(const float4 *) &wd[buf][16 * r + 4 * h];
+            const float4 dm = *(const float4 *) &wdm[buf][16 * r + 4 * h];
+            sA[r][0] = dw.x * x.d; sA[r][1] = dw.y * x.d; sA[r][2] = dw.z * x.d; sA[r][3] = dw.w * x.d;
+            sB[r][0] = dm.x * x.d; sB[r][1] = dm.y * x.d; sB[r][2] = dm.z * x.d; sB[r][3] = dm.w * x.d;
+            const uint32_t w = wmn[buf][16 * r + c16][h];
+            mA[r] = __builtin_bit_cast(mh4, make_uint2(__builtin_amdgcn_perm(w, w, 0x01000100u), __builtin_amdgcn_perm(w, w, 0x03020302u)));
+        }
+        const mh4 sf = {(_Float16) (int16_t) (x.s.x & 0xffff), (_Float16) (int16_t) (x.s.x >> 16),
+                        (_Float16) (int16_t) (x.s.y & 0xffff), (_Float16) (int16_t) (x.s.y >> 16)};
+        int ib[ALLG ? 1 : 4][4], mb[ALLG ? 1 : 4][4];   // gemv-order sums (exact ints: a block's I can pass 2^24)
+        if constexpr (!ALLG) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ib[i] = mb[i] = 0;
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) ib[r][i] = mb[r][i] = 0;
+        }
+        // A fragments of (pair pp, row tile r): read one step ahead of their MFMAs
+        mh8 af[2][2];
+        auto lda = [&](int j, int sl) __attribute__((always_inline)) {
+            const int pp = j >> 2, r = j & 3;
+            const uint8_t * ar = pl + (16 * r + c16) * 512;
+            af[sl][0] = *(const mh8 *) (ar + 16 * mh_slot(c16, 8 * pp + 2 * h));
+            af[sl][1] = *(const mh8 *) (ar + 16 * mh_slot(c16, 8 * pp + 2 * h + 1));
+        };
+        lda(0, 0);
+        mh8 bf0, bf1;
+        mh4 bz;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int pp = j >> 2, r = j & 3, sl = j & 1;
+            if (r == 0) {
+                bf0 = i8x8_f16(x.x[pp].x, x.x[pp].y);
+                bf1 = i8x8_f16(x.x[pp].z, x.x[pp].w);
+                bz = h == pp ? sf : (mh4){0, 0, 0, 0};
             }
+            if (j < 15) lda(j + 1, sl ^ 1);
+            const v4f z = {0.f, 0.f, 0.f, 0.f};
+            v4f I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][0], bf0, z, 0, 0, 0);
+            I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][1], bf1, I, 0, 0, 0);
+            const v4f Im = __builtin_amdgcn_mfma_f32_16x16x16f16(mA[r], bz, z, 0, 0, 0);
+            if constexpr (ALLG) {
 #pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-                const v4f z = {0.f, 0.f, 0.f, 0.f};
-                v4f I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][pp][0], bf[pp][0], z, 0, 0, 0);
-                I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][pp][1], bf[pp][1], I, 0, 0, 0);
-                const v4f Im = __builtin_amdgcn_mfma_f32_16x16x16f16(mA, bz[pp], z, 0, 0, 0);
-                if constexpr (ALLG) {
+                for (int i = 0; i < 4; ++i) {
+                    A[r][i] = fmaf(I[i], sA[r][i], A[r][i]);
+                    B[r][i] = fmaf(Im[i], sB[r][i], B[r][i]);
+                }
+            } else {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        A[r][i] = fmaf(I[i], sA[i], A[r][i]);
-                        B[r][i] = fmaf(Im[i], sB[i], B[r][i]);
-                    }
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        if (gemm) {
-                            A[r][i] = fmaf(I[i], sA[i], A[r][i]);
-                            B[r][i] = fmaf(Im[i], sB[i], B[r][i]);
-                        } else {
-                            ib[i] += (int) I[i];
-                            mb[i] += (int) Im[i];
-                        }
+                for (int i = 0; i < 4; ++i) {
+                    if (gemm) {
+                        A[r][i] = fmaf(I[i], sA[r][i], A[r][i]);
+                        B[r][i] = fmaf(Im[i], sB[r][i], B[r][i]);
+                    } else {
+                        ib[r][i] += (int) I[i];
+                        mb[r][i] += (int) Im[i];
                     }
                 }
             }
-            if constexpr (!ALLG) {
-                if (!gemm) {
+            __builtin_amdgcn_sched_barrier(0);   // bounded live ranges
+        }
+        if constexpr (!ALLG) {
+            if (!gemm) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        A[r][i] = fmaf((float) ib[i], sA[i], A[r][i]);
-                        B[r][i] = fmaf((float) mb[i], sB[i], B[r][i]);
+                        A[r][i] = fmaf((float) ib[r][i], sA[r][i], A[r][i]);
+                        B[r][i] = fmaf((float) mb[r][i], sB[r][i], B[r][i]);
                     }
-                }
             }
         }
     };
 
-    mh_tok xa, xb;
+    const int64_t last = p.nblk - 1;
     load_w(0);
+    mh_tok xa, xb;
     load_x(0, xa);
     fold_w(0);
-    load_w(min((int64_t) 1, p.nblk - 1));
+    load_w(min((int64_t) 1, last));
     // block b: planes[b & 1] were folded during block b-1; the fold of b+1 (planes[(b+1) & 1],
     // last read in block b-1) and the token loads of b+1 overlap block b's MFMAs
     // (no branches around the loads: the last blocks re-load the final block, so the memory
     // counter waits stay exact instead of draining every load at each block)
-    auto step = [&](int64_t b, mh_tok & cur, mh_tok & nxt, auto allg_c) __attribute__((always_inline)) {
+    for (int64_t b = 0; b < p.nblk; ++b) {
         __syncthreads();
-        load_x(min(b + 1, p.nblk - 1), nxt);
+        load_x(min(b + 1, last), xb);
         fold_w((int) ((b + 1) & 1));
-        load_w(min(b + 2, p.nblk - 1));
-        compute((int) (b & 1), cur, allg_c);
-    };
-    auto run = [&](auto allg_c) __attribute__((always_inline)) {
-        for (int64_t b = 0; b < p.nblk; ++b) {
-            step(b, xa, xb, allg_c);
-            xa = xb;
-        }
-    };
-    if (allg) run(std::integral_constant<bool, true>());
-    else run(std::integral_constant<bool, false>());
+        load_w(min(b + 2, last));
+        compute((int) (b & 1), xa);
+        xa = xb;
+    }
     if (tok < T) {
         char * drow = (char *) p.dst + tok * p.nb1;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int64_t m0 = row0 + 64 * rg + 16 * r + 4 * h;
+            const int64_t m0 = row0 + 16 * r + 4 * h;
             if (m0 + 3 < p.M) {
                 *(float4 *) (drow + m0 * 4) = make_float4(__fsub_rn(A[r][0], B[r][0]), __fsub_rn(A[r][1], B[r][1]),
                                                           __fsub_rn(A[r][2], B[r][2]), __fsub_rn(A[r][3], B[r][3]));
@@ -259,13 +253,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_mmq_q4Kh(const mmq
 }
 
 
-void launch_mmq_q4Kh(hipStream_t st, const mmq_args & p, int nw) {
-    if (nw == 8) {
-        const dim3 grid((unsigned) ceil_div(p.M, (int64_t) MH_BM), (unsigned) ceil_div(p.T, (int64_t) 128));
-        hipLaunchKernelGGL(k_mmq_q4Kh<8>, grid, dim3(512), 0, st, p);
-    } else {
-        const dim3 grid((unsigned) ceil_div(p.M, (int64_t) MH_BM), (unsigned) ceil_div(p.T, (int64_t) 64));
-        hipLaunchKernelGGL(k_mmq_q4Kh<4>, grid, dim3(256), 0, st, p);
+void launch_mmq_q4Kh(hipStream_t st, const mmq_args & p0) {
+    mmq_args p = p0;
+    const int64_t gx = ceil_div(p.M, (int64_t) MH_BM);
+    const int64_t full = p.gemm_cols / 64, tiles = ceil_div(p.T, (int64_t) 64);   // token tiles all in gemm order
+    if (full > 0) {
+        p.ty0 = 0;
+        hipLaunchKernelGGL((k_mmq_q4Kh<true>), dim3((unsigned) gx, (unsigned) full), dim3(256), 0, st, p);
+    }
+    if (tiles > full) {
+        p.ty0 = full;
+        hipLaunchKernelGGL((k_mmq_q4Kh<false>), dim3((unsigned) gx, (unsigned) (tiles - full)), dim3(256), 0, st, p);
     }
 }
 

@@ -22,9 +22,10 @@ struct mmq_args {
     // activation columns off[z] .. off[z] + cnt[z] - 1, column j is pair list[j] = e + n_used * t and
     // lands at dst + e * nb1 + t * nb2; nullptr cnt = a plain MUL_MAT
     const int32_t * cnt; const int32_t * off; const int32_t * list; int64_t n_used; int64_t nb02; int64_t nb2;
+    int64_t ty0 = 0;            // k_mmq_q4Kh: first token tile of the grid
 };
 
-// the f16-operand Q4_K tile (k_mmq_f16.hip); nw = 4 (64-token workgroups) or 8 (128)
-void launch_mmq_q4Kh(hipStream_t st, const mmq_args & p, int nw);
+// the f16-operand Q4_K tile (k_mmq_f16.hip), 64-token workgroups of four waves
+void launch_mmq_q4Kh(hipStream_t st, const mmq_args & p);
 
 }  // namespace mi355x

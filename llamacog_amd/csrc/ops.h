@@ -232,6 +232,7 @@ struct gemv_epi {
 bool gemv_supported(const ggml_tensor * mm);
 bool gemv_tail_ready(exec_ctx & ctx);
 double * gemv_rsum_site(exec_ctx & ctx);   // a zeroed site of rsum_buf, or nullptr
+bool gemv_ring_wide(int64_t rows);          // a launch of this many rows takes the persistent ring kernel
 bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi);
 bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c);   // c may join mm0's launch as a second weight type

@@ -18,8 +18,8 @@ cd /tmp
 # decode-only traced run: W + K timed + (4 + K) split + (4 + R) roofline single-token decodes
 W=4; K=32; RF=8
 NTOK=$((W + K + 4 + K + 4 + RF))
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace -o run -- python3 $R/bench.py --steps $K --warmup $W --roofline-steps $RF --pp 0 --no-cpu-baseline > $R/$OUT/trace_bench.json 2> $R/$OUT/trace_bench.err || { echo "trace rc=$?"; tail -20 $R/$OUT/trace_bench.err; exit 1; }
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/$OUT/pmc -o run -- python3 $R/bench.py --steps 16 --warmup 2 --pp 0 --no-cpu-baseline --roofline-steps 0 > $R/$OUT/pmc_bench.json 2> $R/$OUT/pmc_bench.err || { echo "pmc rc=$?"; tail -20 $R/$OUT/pmc_bench.err; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/trace -o run -- python3 $R/bench.py --steps $K --warmup $W --roofline-steps $RF --pp 0 --no-cpu-baseline --no-split-series > $R/$OUT/trace_bench.json 2> $R/$OUT/trace_bench.err || { echo "trace rc=$?"; tail -20 $R/$OUT/trace_bench.err; exit 1; }
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/$OUT/pmc -o run -- python3 $R/bench.py --steps 16 --warmup 2 --pp 0 --no-cpu-baseline --roofline-steps 0 --no-split-series > $R/$OUT/pmc_bench.json 2> $R/$OUT/pmc_bench.err || { echo "pmc rc=$?"; tail -20 $R/$OUT/pmc_bench.err; exit 1; }
 cd $R
 python3 scripts/kstats.py $(find $OUT/trace -name '*kernel_stats.csv' | head -1) $NTOK > $OUT/kernel_stats_summary.txt
 cp $(find $OUT/trace -name '*kernel_stats.csv' | head -1) $OUT/kernel_stats.csv

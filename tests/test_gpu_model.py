@@ -117,7 +117,7 @@ m.close()
 np.save({out!r}, lg)
 print(json.dumps({{"devices": names, "handoffs": la.handoff_stats(), "split": la.split_stats(),
                    "pipeline": [l for l in log.splitlines() if "pipeline parallelism" in l or "graph splits" in l][-3:],
-                   "buffers": [l for l in log.splitlines() if "buffer size" in l][-8:]}}))
+                   "buffers": [l for l in log.splitlines() if "buffer size" in l]}}))
 """
 
 
