@@ -461,9 +461,10 @@ static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tenso
     // the one-shot GEMV forms the prologue in every workgroup: for wide consumers (the FFN
     // gate/up, 28672 rows; the output head) that is thousands of redundant norms, and the
     // stand-alone norm kernel plus a prologue-free launch measured faster (round 3 kernel
-    // timeline: gate/up 27.0 us with the prologue vs 15 + 4 without); Q/K/V keep it, and the
-    // persistent ring kernel (k_gemv_ring) forms it once per resident workgroup
-    if (rows > 16384 && !gemv_ring_wide(rows)) return;
+    // timeline: gate/up 27.0 us with the prologue vs 15 + 4 without); Q/K/V keep it.  A persistent
+    // LDS-ring kernel that forms it once per resident workgroup measured slower still (round 3:
+    // gate/up + prologue 22.0 us, tg 393-415 vs 420-430 tok/s over five ring geometries)
+    if (rows > 16384) return;
     if (!dead_after(g, n, pl + 1, last, readers)) return;
     if (mul && !dead_after(g, n, pn + 1, nm, {mul})) return;
     double * site = gemv_rsum_site(ctx);

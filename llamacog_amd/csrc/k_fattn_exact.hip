@@ -66,6 +66,15 @@ __device__ __forceinline__ float quad_from_plus1(float v) {
 
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
+// LDS-DMA of 16 B per lane issued as inline asm: the compiler then sees no LDS write in flight
+// and does not drain vmcnt before the issuing wave's next LDS read (with the builtin it waited
+// for the V stage — and for the next chunk's K loads issued after it — before every score
+// write / coefficient read of k_fattn_dec2's producers).  The caller waits for the data itself.
+__device__ __forceinline__ void lds_dma16(const void * src, const void * lds) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (lds_ptr_t) lds);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+}
+
 // one step of the f16 accumulation, y = f16(fma(v, vs, y)) with v and y as f16 bits in the low
 // halves: v_fma_mix_f32 converts both exactly and rounds the fma once to f32, v_cvt_f16_f32
 // rounds that to f16 — the CPU's cvtph_ps / fmadd_ps / cvtps_ph sequence, two dependent
@@ -884,6 +893,12 @@ __device__ __forceinline__ void dc_wave_lds_order() {
     asm volatile("" ::: "memory");
 }
 
+// the producers' LDS hand-off words as relaxed workgroup-scope atomics: they compile to ds_read /
+// ds_write (a volatile access through a generic pointer became a flat access, which counts in
+// vmcnt — the compiler then drained the next chunk's K loads right after issuing them)
+template <class V> __device__ __forceinline__ V lds_ld(V * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+template <class V> __device__ __forceinline__ void lds_st(V * p, V v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
 // LDS of k_fattn_dec2, laid out by hand: the small arrays the chains read every batch first,
 // the V stages last (reads at high LDS addresses measured ~5 ticks per position slower,
 // tools/ubench_dc.hip); with GQA sharing only head 0's stages [0, 64 KiB) above them are used
@@ -973,6 +988,7 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
                 const int st = (int) (c & 1);
                 const int64_t c0 = c * CH;
                 const uint16_t m0b = mc0, m1b = mc1;
+                bool kout = false;   // the next chunk's K loads were issued
                 const int nrun = nrun_of(m0b, m1b);
                 // the next chunk's mask, in flight under this one
                 mc0 = mask_at(c0 + CH + lane);
@@ -1003,7 +1019,7 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
                         const int np = (vhi - vlo + 3) / 4;
                         for (int p = 0; p < np; ++p) {
                             const char * src = (4 * p + r_in < vhi - vlo) ? vp : vlast;
-                            __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) dst, 16, 0, 0);
+                            lds_dma16(src, dst);
                             vp += step;
                             dst += 512;
                         }
@@ -1028,9 +1044,11 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
                     }
                     // the next chunk's K rows, in flight under this chunk's coefficients and the
                     // chains' recurrence
+                    // (bounded by the cache only: waiting for the next chunk's mask here would also
+                    // wait for this chunk's V DMA, issued after it)
                     if (c + 1 < nchunk) {
-                        const int nn = nrun_of(mc0, mc1);
-                        if (nn > 0) load_k(c0 + CH, nn - 1, kh);
+                        load_k(c0 + CH, (int) min<int64_t>(CH, a.n_kv - c0 - CH) - 1, kh);
+                        kout = true;
                     }
                     dc_wave_lds_order();
                     mark(2);
@@ -1044,15 +1062,15 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
                         if (lane == 0) {
                             // LDS only, in order: the value, its write done, then the sequence word
                             // (a workgroup-scope fence would also wait for this wave's V DMA and K loads)
-                            *(volatile float *) &sm.mpub[ph] = fmaxf(mcarry, th);
+                            lds_st(&sm.mpub[ph], fmaxf(mcarry, th));
                             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                            *(volatile int *) &sm.mseq[ph] = (int) c + 1;
+                            lds_st(&sm.mseq[ph], (int) c + 1);
                         }
                     } else {
                         // the first half of the same head publishes its max within its own chunk work
                         int guard = 0;
-                        while (*(volatile int *) &sm.mseq[ph] != (int) c + 1 && ++guard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
-                        base = *(volatile float *) &sm.mpub[ph];
+                        while (lds_ld(&sm.mseq[ph]) != (int) c + 1 && ++guard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
+                        base = lds_ld(&sm.mpub[ph]);
                     }
                     const float M = fmaxf(base, dpp_ninf<0x138>(smx));   // max over every position before jl
                     float msv, vsv;
@@ -1071,15 +1089,18 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
                     tot = fmaxf(base, th);
                     mark(3);
                 } else {
-                    if (hf == 0 && lane == 0) *(volatile int *) &sm.mseq[ph] = (int) c + 1;
+                    if (hf == 0 && lane == 0) lds_st(&sm.mseq[ph], (int) c + 1);
                     if (c + 1 < nchunk) {
-                        const int nn = nrun_of(mc0, mc1);
-                        if (nn > 0) load_k(c0 + CH, nn - 1, kh);
+                        load_k(c0 + CH, (int) min<int64_t>(CH, a.n_kv - c0 - CH) - 1, kh);
+                        kout = true;
                     }
                 }
                 if (hf == 1 && lane == 0) sm.mcar[ph] = nrun > 0 ? tot : mcarry;   // read after the barrier
                 if (pw == 0 && lane == 0) sm.nrs[st] = nrun;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's V rows are in LDS
+                // this wave's V rows are in LDS: everything but the next chunk's K loads (the
+                // NPH x NM loads of load_k, the only vector-memory instructions after the V DMA)
+                if (kout) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPH * NM) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 mark(4);
             }
             __syncthreads();

@@ -611,182 +611,6 @@ __global__ __launch_bounds__(256) void k_gemv_os2(const gemv_args p1, const int6
 }
 
 
-// ---- persistent LDS-ring body: wide matrices (FFN gate/up, down) -----------------------------------
-// A resident grid (two workgroups per CU) walks the row groups wg0, wg0 + nwg, ...; each wave keeps
-// NS of its row-slice DMAs in flight in its own LDS ring (global_load_lds, as the one-shot body),
-// so the bytes in flight do not cost VGPRs and the norm prologue is formed once per workgroup
-// instead of once per row group.  Row values are parked in LDS; the stores, the residual
-// producer's x = v + res and sums of squares, the epilogues and the SwiGLU tail run after the
-// loop, so the loop issues no vector-memory instruction besides the DMAs and each group's wait is
-// an exact vmcnt.  Records, walker and epilogues are the one-shot body's (the same bits).
-// The ring's DMAs are issued as inline asm: the compiler then sees no LDS write in flight, so it
-// does not drain vmcnt before every LDS read of the loop (it cannot tell the ring's stages apart
-// and would wait for all of them).  The ring body waits for each stage itself (ring_wait); every
-// compiler-visible vector-memory instruction only adds to the counts waited on.  (Loads into
-// VGPRs cannot be hidden the same way: the compiler treats an asm load's output as ready and
-// may copy it before any wait.)
-typedef uint32_t ring_u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void ring_dma16(const void * src, const uint8_t * lds) {
-    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (gemv_lds_t) lds);
-#if MI_WNT
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(m), "v"(src) : "memory", "m0");
-#else
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
-#endif
-}
-template <int PER>
-__device__ __forceinline__ void ring_wait(int later) {   // wait until <= later * PER vmem ops are outstanding
-    switch (later) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PER) : "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * PER) : "memory"); break;
-    }
-}
-
-template <class T, int R, int WPR, int NS, int MODE, bool PRO>
-__global__ __launch_bounds__(256) void k_gemv_ring(const gemv_args p, const int64_t ngroups) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
-    static_assert(NS >= 2 && NS <= 6, "ring depth");
-    kt_enter(p.kt);
-    constexpr int NWV = 4;
-    constexpr int NT = 64 * NWV;
-    constexpr int RPG = (NWV / WPR) * R;
-    using G = os_geo<T>;
-    constexpr int PER = R * G::NI;   // DMA instructions per group and wave
-    static_assert(PER * (NS - 1) <= 63, "vmcnt range");
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int wsub = wave % WPR;
-    const int t = wsub * WAVE + lane;
-    const bool active = t < p.ntasks;
-    const int tt = active ? t : 0;
-    const int nb = p.ntasks / T::per_block;
-    const int rowl0 = (wave / WPR) * R;
-    const int64_t wg0 = blockIdx.x, nwg = gridDim.x;
-    const int kn = (int) ((ngroups - wg0 + nwg - 1) / nwg);   // this workgroup's groups (<= GEMV_MAXG)
-    uint8_t * ring = (uint8_t *) xr + p.wl_off + (size_t) wave * R * G::SLICE;
-    constexpr size_t STAGE = (size_t) NWV * R * G::SLICE;
-    const int nt_w = min(WAVE, p.ntasks - WAVE * wsub);
-    const int seg = (nt_w / T::per_block) * T::blk_bytes;
-    auto dma = [&](int k, int st) __attribute__((always_inline)) {
-        const int64_t g = wg0 + (int64_t) k * nwg;
-        const int mi = gemv_mat(p, g);
-        const int64_t row0 = (g - p.blk0[mi]) * RPG + rowl0, M = p.M[mi];
-        const uint8_t * Wm = p.W[mi];
-        uint8_t * dst = ring + (size_t) st * STAGE;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint8_t * src = Wm + min(row0 + r, M - 1) * p.nb01[mi] + (int64_t) wsub * G::SEG;
-#pragma unroll
-            for (int i = 0; i < G::NI; ++i) {
-                const int off = min(i * 1024 + 16 * lane, seg - 16);
-                ring_dma16(src + off, dst + r * G::SLICE + i * 1024);
-            }
-        }
-    };
-    // the first NS groups' weights, then the activation (the compiler's wait for the prologue's
-    // sources also covers those DMAs: the prologue's arithmetic is the part not overlapped)
-#pragma unroll
-    for (int st = 0; st < NS; ++st) {
-        if (st < kn) dma(st, st);
-    }
-    typename T::act x;
-    if constexpr (PRO) {
-        pro_regs pr;
-        gemv_pro_load(p, pr);
-        gemv_act A = p.A;
-        gemv_pro_finish(p, pr, (uint8_t *) xr + p.pro.lds_off, A);
-        T::load(A, tt, x);
-    } else {
-        T::load(p.A, tt, x);
-    }
-    __shared__ float res[GEMV_MAXG * RPG];
-    const int wr = lane / T::LPR, ws = lane % T::LPR;
-    const int wrc = wr < R ? wr : 0;
-    for (int k = 0; k < kn; ++k) {
-        const int st = k % NS;
-        ring_wait<PER>(min(NS - 1, kn - 1 - k));
-        uint32_t * xb = xr + (size_t) (k & 1) * RPG * nb * T::RS;
-        const uint8_t * mine = ring + (size_t) st * STAGE;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            typename T::raw w;
-            T::template fetch<typename lds_loader<T>::type>(mine + r * G::SLICE - (int64_t) wsub * G::SEG, tt, w);
-            T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * nb * T::RS);
-        }
-        // the slot's bytes are in registers (rec consumed them): refill it NS groups ahead
-        if (k + NS < kn) dma(k + NS, st);
-        if constexpr (WPR > 1) __syncthreads();
-        else wave_lds_sync();
-        if (wsub == 0) {
-            const float v = T::walk(xb + (size_t) (rowl0 + wrc) * nb * T::RS, nb, ws);
-            if (wr < R && ws == 0) res[k * RPG + rowl0 + wr] = v;
-        }
-    }
-    __syncthreads();
-    // ---- after the loop: every row value of this workgroup is in res[] ----
-    if constexpr (MODE >= 1) {
-        __shared__ float2 rtab[GEMV_ROPE_MAXPAIRS];
-        __shared__ uint16_t * f16p[2 * GEMV_MAXMAT];
-        if (threadIdx.x < 2 * GEMV_MAXMAT) {
-            const int m2 = threadIdx.x >> 1;
-            uint16_t * const * slot = (threadIdx.x & 1) ? p.rope_f16[m2] : p.f16out[m2];
-            f16p[threadIdx.x] = slot ? *slot : nullptr;
-        }
-        if (p.need_pairs) {
-            for (int ip = threadIdx.x; ip < p.rp.n_dims / 2; ip += NT) rtab[ip] = p.rtab_g[ip];
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < kn * RPG; i += NT) {
-            const int64_t g = wg0 + (int64_t) (i / RPG) * nwg;
-            int mi = 0;
-#pragma unroll
-            for (int m = 1; m < GEMV_MAXMAT; ++m) mi += g >= p.blk0[m] ? 1 : 0;
-            const int64_t row = (g - p.blk0[mi]) * RPG + i % RPG;
-            if (row < p.M[mi]) gemv_store(p, mi, p.M[mi], row, res[i], res[RPG > 1 ? i ^ 1 : i], rtab, f16p);
-        }
-    } else if (p.rres) {
-        // residual producer: x = v + res (the CPU's single f32 add) and this workgroup's sum of
-        // squares to its shard (no-return atomic; the consumer decides the mean from the sum)
-        double ss = 0.0;
-        for (int i = threadIdx.x; i < kn * RPG; i += NT) {
-            const int64_t row = (wg0 + (int64_t) (i / RPG) * nwg) * RPG + i % RPG;
-            if (row < p.M[0]) {
-                const float xv = __fadd_rn(res[i], p.rres[row]);
-                p.rxsum[row] = xv;
-                ss = __dadd_rn(ss, (double) __fmul_rn(xv, xv));
-            }
-        }
-        ss = wave_sum(ss);
-        __shared__ double rpart[NWV];
-        if (lane == 0) rpart[wave] = ss;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double tot = 0.0;
-#pragma unroll
-            for (int k = 0; k < NWV; ++k) tot = __dadd_rn(tot, rpart[k]);
-            __hip_atomic_fetch_add(p.rsum + RSUM_STRIDE * (wg0 % RSUM_SHARDS), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else {
-        for (int i = threadIdx.x; i < kn * RPG; i += NT) {
-            const int64_t g = wg0 + (int64_t) (i / RPG) * nwg;
-            int mi = 0;
-#pragma unroll
-            for (int m = 1; m < GEMV_MAXMAT; ++m) mi += g >= p.blk0[m] ? 1 : 0;
-            const int64_t row = (g - p.blk0[mi]) * RPG + i % RPG;
-            if (row < p.M[mi] && p.dst[mi]) {
-                if (p.tl.kind) __hip_atomic_store(p.dst[mi] + row, res[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                else p.dst[mi][row] = res[i];
-            }
-        }
-        if (p.tl.kind) gemv_tail(p, kn, wg0, nwg, RPG);
-    }
-    kt_exit(p.kt);
-}
-
-
 // ---- host ----------------------------------------------------------------------------------------
 // kernel-timing mode: the GEMV kernel itself is launched with start/stop events
 // (hipExtLaunchKernel records them at the dispatch's start and completion, without extra
@@ -983,81 +807,8 @@ static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2,
 #undef OS2_LAUNCH
 }
 
-// ---- persistent LDS-ring launches (k_gemv_ring) ----------------------------------------------------
-// Wide matrices (>= 16384 rows in the launch: the FFN gate/up) and K = 14336 (the FFN down):
-// GGML_MI355X_GEMV_RING=0 keeps them on the one-shot kernel (A/B)
-static int ring_mode() {
-    static const int m = getenv("GGML_MI355X_GEMV_RING") ? atoi(getenv("GGML_MI355X_GEMV_RING")) : 0;
-    return m;
-}
-// GGML_MI355X_RING_CFG=<rows per wave><stages><workgroups per CU>, e.g. 143 (A/B)
-static int ring_cfg() {
-    static const int c = getenv("GGML_MI355X_RING_CFG") ? atoi(getenv("GGML_MI355X_RING_CFG")) : 142;
-    return c;
-}
-
-template <class T, int R, int WPR, int NS, int MODE, bool PRO>
-static void launch_ring_m(hipStream_t st, gemv_args & a, int nmat, int64_t ng, int64_t grid, size_t lds) {
-    a.kt = g_kt_ctx ? g_kt_ctx->kt_take(gemv_kt_name(a, MODE), (unsigned) grid, 256) : nullptr;
-    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_ring<T, R, WPR, NS, MODE, PRO>), dim3((unsigned) grid), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a, ng);
-    else hipLaunchKernelGGL((k_gemv_ring<T, R, WPR, NS, MODE, PRO>), dim3((unsigned) grid), dim3(256), lds, st, a, ng);
-}
-
-template <class T, int R, int WPR, int NS>
-static bool launch_ring(hipStream_t st, gemv_args & a, int nmat) {
-    constexpr int RPG = (4 / WPR) * R;
-    const int64_t ng = set_groups(a, nmat, RPG);
-    // LDS: records (two buffers) | prologue activation | NS stages of 4 waves x R slices
-    size_t off = r16((size_t) 4 * xrec_dwords<T>(RPG, a.ntasks / T::per_block));
-    if (a.pro.x) {
-        a.pro.lds_off = (uint32_t) off;
-        off = r16(off + pro_lds_bytes(a.pro.n, a.pro.qmode));
-    }
-    a.wl_off = (uint32_t) off;
-    const size_t lds = off + (size_t) NS * 4 * R * os_geo<T>::SLICE;
-    if (lds > 64 * 1024) return false;
-    const int per_cu = std::max(1, ring_cfg() % 10);
-    const int64_t grid = std::min<int64_t>(ng, std::max<int64_t>((int64_t) per_cu * g_num_cu, ceil_div(ng, GEMV_MAXG)));
-    if (ceil_div(ng, grid) > GEMV_MAXG) return false;
-    const bool epi = needs_epilogue(a, nmat);
-    if (epi && (a.rres || a.tl.kind)) return false;
-    if (a.pro.x) {
-        if (epi) launch_ring_m<T, R, WPR, NS, 1, true>(st, a, nmat, ng, grid, lds);
-        else launch_ring_m<T, R, WPR, NS, 0, true>(st, a, nmat, ng, grid, lds);
-    } else {
-        if (epi) launch_ring_m<T, R, WPR, NS, 1, false>(st, a, nmat, ng, grid, lds);
-        else launch_ring_m<T, R, WPR, NS, 0, false>(st, a, nmat, ng, grid, lds);
-    }
-    return true;
-}
-
-template <class T>
-static bool launch_ring_t(hipStream_t st, gemv_args & a, int nmat) {
-    if (!ring_mode() || !os_aligned<T>(a, nmat)) return false;
-    int64_t Mt = 0;
-    for (int i = 0; i < nmat; ++i) Mt += a.M[i];
-    const int wpr = wpr_of(a.ntasks);
-    const bool wide = Mt >= 16384 && wpr == 1;
-    const bool longk = wpr == 4 && ring_mode() >= 2;   // K = 14336 (down): opt-in until measured
-    if (!wide && !longk) return false;
-    const int rn = ring_cfg() / 10;   // rows per wave x 10 + stages
-    if (wpr == 1) {
-        switch (rn) {
-            case 12: return launch_ring<T, 1, 1, 2>(st, a, nmat);
-            case 13: return launch_ring<T, 1, 1, 3>(st, a, nmat);
-            case 22: return launch_ring<T, 2, 1, 2>(st, a, nmat);
-            case 23: return launch_ring<T, 2, 1, 3>(st, a, nmat);
-            default: return launch_ring<T, 1, 1, 4>(st, a, nmat);
-        }
-    }
-    return launch_ring<T, 1, 4, 4>(st, a, nmat);
-}
-
-bool gemv_ring_wide(int64_t rows) { return ring_mode() && rows >= 16384; }
-
 template <class T>
 static void launch_t(hipStream_t st, gemv_args & a, int nmat) {
-    if (launch_ring_t<T>(st, a, nmat)) return;
     if (launch_os_t<T>(st, a, nmat)) return;
     int64_t Mt = 0;
     for (int i = 0; i < nmat; ++i) Mt += a.M[i];
