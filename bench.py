@@ -40,7 +40,7 @@ MFMA_I8_PEAK_TOPS = 5000.0
 # algorithmic work of one pp512 of Llama-3-8B: 2*6.98e9*512 layer matmuls +
 # output (last token) + attention
 PP512_FLOP = 7.22e12
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02", "pmc_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03", "pmc_traffic.json")
 
 
 def parse():
@@ -344,7 +344,7 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, gpu, n_ctx, r):
                 traffic = None
         roof = {
             "bound": "hbm",
-            "kernel": "k_gemv_pipe (quantized decode GEMV, every decode MUL_MAT)",
+            "kernel": "k_gemv_os / k_gemv_os2 (one-shot LDS-DMA quantized decode GEMV, every decode MUL_MAT)",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -352,7 +352,7 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, gpu, n_ctx, r):
             "peak_measured": round(hbm, 1) if hbm > 0 else None,
             "frac_of_measured": round(achieved / hbm, 4) if achieved and hbm > 0 else None,
             "traffic": traffic,
-            "traffic_source": "profiles/r02/pmc_traffic.json" if traffic else None,
+            "traffic_source": "profiles/r03/pmc_traffic.json: a separate rocprofv3 --pmc FETCH_SIZE pass (scripts/gpu_final.sh), not this run" if traffic else None,
             "launches": mv_n,
             "avg_launch_us": round(1e3 * mv_ms / mv_n, 3) if mv_n else None,
             "algorithmic_bytes_per_launch": round(mv_bytes / mv_n) if mv_n else None,

@@ -54,6 +54,8 @@ __device__ __forceinline__ mh8 i8x8_f16(uint32_t w0, uint32_t w1) {
 
 // ALLG: every token of the grid takes the gemm order.  (Loading the tokens two or three blocks
 // ahead instead of one measured 4-7 % slower: 52.9 / 54.4 vs 50.8 us at M = 4096, T = 512.)
+// (Eight waves of 16 tokens sharing one fold of the 64 rows, one workgroup per CU, measured
+// slower: 176 vs 152 us at M = 14336, T = 512.)
 template <bool ALLG>
 __global__ __launch_bounds__(256, 2) void k_mmq_q4Kh(const mmq_args p) {
     constexpr int NW = 4, BN = 16 * NW;
@@ -160,48 +162,61 @@ __global__ __launch_bounds__(256, 2) void k_mmq_q4Kh(const mmq_args p) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) ib[r][i] = mb[r][i] = 0;
         }
-        // A fragments of (pair pp, row tile r): read one step ahead of their MFMAs
-        mh8 af[2][2];
-        auto lda = [&](int j, int sl) __attribute__((always_inline)) {
-            const int pp = j >> 2, r = j & 3;
+        // the token's pairs as f16 B fragments, and the pair's 16-sums (lanes h == pp)
+        mh8 bf[4][2];
+        mh4 bz[4];
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            bf[pp][0] = i8x8_f16(x.x[pp].x, x.x[pp].y);
+            bf[pp][1] = i8x8_f16(x.x[pp].z, x.x[pp].w);
+            bz[pp] = h == pp ? sf : (mh4){0, 0, 0, 0};
+        }
+        // step j = (pair pp, row tile r): its A fragments are read two steps ahead and its MFMAs
+        // issued one step ahead of the chain FMAs that consume them, so the matrix pipe works
+        // while the VALU runs the previous step's FMAs (not waiting on each result in turn)
+        mh8 af[3][2];
+        auto lda = [&](int j) __attribute__((always_inline)) {
+            const int pp = j >> 2, r = j & 3, sl = j % 3;
             const uint8_t * ar = pl + (16 * r + c16) * 512;
             af[sl][0] = *(const mh8 *) (ar + 16 * mh_slot(c16, 8 * pp + 2 * h));
             af[sl][1] = *(const mh8 *) (ar + 16 * mh_slot(c16, 8 * pp + 2 * h + 1));
         };
-        lda(0, 0);
-        mh8 bf0, bf1;
-        mh4 bz;
+        auto mma = [&](int j, v4f & I, v4f & Im) __attribute__((always_inline)) {
+            const int pp = j >> 2, r = j & 3, sl = j % 3;
+            const v4f z = {0.f, 0.f, 0.f, 0.f};
+            I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][0], bf[pp][0], z, 0, 0, 0);
+            I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][1], bf[pp][1], I, 0, 0, 0);
+            Im = __builtin_amdgcn_mfma_f32_16x16x16f16(mA[r], bz[pp], z, 0, 0, 0);
+        };
+        lda(0);
+        lda(1);
+        v4f Ic, Imc;
+        mma(0, Ic, Imc);
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const int pp = j >> 2, r = j & 3, sl = j & 1;
-            if (r == 0) {
-                bf0 = i8x8_f16(x.x[pp].x, x.x[pp].y);
-                bf1 = i8x8_f16(x.x[pp].z, x.x[pp].w);
-                bz = h == pp ? sf : (mh4){0, 0, 0, 0};
-            }
-            if (j < 15) lda(j + 1, sl ^ 1);
-            const v4f z = {0.f, 0.f, 0.f, 0.f};
-            v4f I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][0], bf0, z, 0, 0, 0);
-            I = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[sl][1], bf1, I, 0, 0, 0);
-            const v4f Im = __builtin_amdgcn_mfma_f32_16x16x16f16(mA[r], bz, z, 0, 0, 0);
+            const int r = j & 3;
+            if (j + 2 < 16) lda(j + 2);
+            v4f In, Imn;
+            if (j + 1 < 16) mma(j + 1, In, Imn);
             if constexpr (ALLG) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    A[r][i] = fmaf(I[i], sA[r][i], A[r][i]);
-                    B[r][i] = fmaf(Im[i], sB[r][i], B[r][i]);
+                    A[r][i] = fmaf(Ic[i], sA[r][i], A[r][i]);
+                    B[r][i] = fmaf(Imc[i], sB[r][i], B[r][i]);
                 }
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     if (gemm) {
-                        A[r][i] = fmaf(I[i], sA[r][i], A[r][i]);
-                        B[r][i] = fmaf(Im[i], sB[r][i], B[r][i]);
+                        A[r][i] = fmaf(Ic[i], sA[r][i], A[r][i]);
+                        B[r][i] = fmaf(Imc[i], sB[r][i], B[r][i]);
                     } else {
-                        ib[r][i] += (int) I[i];
-                        mb[r][i] += (int) Im[i];
+                        ib[r][i] += (int) Ic[i];
+                        mb[r][i] += (int) Imc[i];
                     }
                 }
             }
+            if (j + 1 < 16) { Ic = In; Imc = Imn; }
             __builtin_amdgcn_sched_barrier(0);   // bounded live ranges
         }
         if constexpr (!ALLG) {
