@@ -88,6 +88,18 @@ __device__ __forceinline__ uint32_t f16_mad(uint32_t vbits, float vs, uint32_t y
     return r;
 }
 
+// y = f16(f32(y) * ms): v_fma_mix_f32 with a -0 addend is the product rounded once to f32 (as
+// the CPU's _mm512_mul_ps of the converted halves), then the f16 rounding (vec_scale_f16)
+// (the -0 addend comes in a register: -0.0 is not an inline constant, and a +0 addend would turn
+// a -0 product into +0)
+__device__ __forceinline__ uint32_t f16_scale(uint32_t ybits, float ms, float nz) {
+    float t;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(t) : "v"(ybits), "v"(ms), "v"(nz));
+    uint32_t r;
+    asm("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
 // ggml_vec_dot_f16 (AVX-512) of a K row with q, computed by the 4 lanes of a quad.  Lane q
 // holds, for m < D/16, kh[m] = the 4 halves K[16m + 4q .. 16m + 4q + 3] and qf[m][c] =
 // q[16m + 4q + c] (f16-rounded): the AVX-512 lane partials l = 4q + c (accumulator j = m % 4
@@ -813,27 +825,26 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
                 } else {
                     // the same steps, except: a masked position keeps the state (-0 must
                     // survive); a running-max update first rescales, y = f16(y*ms), S = S*ms —
-                    // the CPU's vec_scale_f16 (ops.cpp:7120-7160).  Uniform branches per event.
+                    // the CPU's vec_scale_f16 (ops.cpp:7120-7160).  Branch-free: every live step
+                    // rescales by its ms, which is exactly 1 where the max does not move (an f16
+                    // value times 1 rounds back to itself, S*1 = S), and a masked step selects
+                    // the old state
 #pragma unroll
                     for (int u = 0; u < PF_U; ++u) {
                         const int j = j0 + u;
                         const float v4[4] = {vs[u].x, vs[u].y, vs[u].z, vs[u].w};
+                        const float4 m4 = *(const float4 *) (cmw + j * PF_P);
+                        const float w4[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
-                            if ((dead[i] >> j) & 1) continue;
-                            if ((upd[i] >> j) & 1) {
-                                const float w = cmw[j * PF_P + i];
-#pragma unroll
-                                for (int e = 0; e < 2; ++e) {
-                                    float t = __fmul_rn(h2f((uint16_t) y[i][e]), w);
-                                    asm("" : "+v"(t));   // two roundings, as f16r
-                                    y[i][e] = (uint32_t) f2h(t);
-                                }
-                                S[i] = __fmul_rn(S[i], w);
-                            }
-                            y[i][0] = f16_mad(vv[u], v4[i], y[i][0]);
-                            y[i][1] = f16_mad_hi(vv[u], v4[i], y[i][1]);
-                            S[i] = __fadd_rn(S[i], v4[i]);
+                            const uint32_t ys0 = f16_scale(y[i][0], w4[i], nz), ys1 = f16_scale(y[i][1], w4[i], nz);
+                            const uint32_t yn0 = f16_mad(vv[u], v4[i], ys0);
+                            const uint32_t yn1 = f16_mad_hi(vv[u], v4[i], ys1);
+                            const float Sn = __fadd_rn(__fmul_rn(S[i], w4[i]), v4[i]);
+                            const bool dd = (dead[i] >> j) & 1;
+                            y[i][0] = dd ? y[i][0] : yn0;
+                            y[i][1] = dd ? y[i][1] : yn1;
+                            S[i] = dd ? S[i] : Sn;
                         }
                     }
                 }
