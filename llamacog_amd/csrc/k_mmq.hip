@@ -315,6 +315,11 @@ template <class W> struct mc_stage {
     static constexpr int BYTES = XS + MQ_BN * 32;
 };
 
+// LDS slot of 8-byte piece s (0..31) of a folded plane row: s ^ 2(row & 15) spreads the MFMA
+// A-fragment reads (rows c16, pieces 4c + h) over all banks; the extra (s >> 4) separates the fold's
+// ds_write_b64 lane groups (two rows x eight classes: pieces 4fc + q), which otherwise met 2-way
+__device__ __forceinline__ int mc_slot(int row, int s) { return s ^ (2 * (row & 15)) ^ (s >> 4); }
+
 __device__ __forceinline__ uint32_t pk_bytes(uint32_t e, uint32_t o) {   // bytes 0,2 from e, 1,3 from o
     return (e & 0x00ff00ffu) | ((o & 0x00ff00ffu) << 8);
 }
@@ -469,30 +474,36 @@ __global__ __launch_bounds__(512, 2) void k_mmq_cls(const mmq_args p) {
         for (int i = 0; i < 4; ++i) summs[n][i] = 0.0f;
 
     issue_x(0, 0);
+    typename W::raw wr1;
     W::load(wsrc, fc, wr);
     const int ra = 16 * rg + c16;   // A row of this lane
-    for (int64_t b = 0; b < p.nblk; ++b) {
+    // block b: its token stage and raw weights were issued at the start of block b-1 (before that
+    // block's fold and MFMAs), so the wait at the top of b covers loads a whole block old
+    auto block = [&](int64_t b, typename W::raw & cur, typename W::raw & nxt) __attribute__((always_inline)) {
         const int s = (int) (b & 1);
         const int8_t * xq = (const int8_t *) st[s];
         const float * xd = (const float *) (st[s] + S::XD);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();   // token stage s and this thread's raw weights landed; block b-1 is done with the planes
+        __syncthreads();   // token stage s and this thread's raw weights landed; block b-1 is done with the planes and stage s^1
+        if (b + 1 < p.nblk) {
+            issue_x(b + 1, s ^ 1);
+            W::load(wsrc + (b + 1) * W::BLK, fc, nxt);
+        }
         {
             uint32_t hi[8], lo[8];
-            W::fold(wr, fc, hi, lo);
-            const int sw = 2 * (fr & 15);
+            W::fold(cur, fc, hi, lo);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {   // 8-byte slot 4c + q of the row, XOR-swizzled
-                const int slot = (4 * fc + q) ^ sw;
+                const int slot = mc_slot(fr, 4 * fc + q);
                 *(uint2 *) (ph + fr * 256 + 8 * slot) = make_uint2(hi[2 * q], hi[2 * q + 1]);
                 *(uint2 *) (pl + fr * 256 + 8 * slot) = make_uint2(lo[2 * q], lo[2 * q + 1]);
             }
             if (fc == 0) {
-                wd[fr] = W::d_of(wr);
-                wdm[fr] = W::dmin_of(wr);
+                wd[fr] = W::d_of(cur);
+                wdm[fr] = W::dmin_of(cur);
                 if constexpr (W::MINS) {
                     int mn[8];
-                    W::mins_of(wr, mn);
+                    W::mins_of(cur, mn);
 #pragma unroll
                     for (int j = 0; j < 8; ++j) wmn[fr][j] = (float) mn[j];
                 }
@@ -506,11 +517,6 @@ __global__ __launch_bounds__(512, 2) void k_mmq_cls(const mmq_args p) {
             }
         }
         __syncthreads();
-        const bool more = b + 1 < p.nblk;
-        if (more) {
-            issue_x(b + 1, s ^ 1);
-            W::load(wsrc + (b + 1) * W::BLK, fc, wr);
-        }
         float f[2][4];   // dy·d, as the CPU forms it
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
@@ -520,7 +526,7 @@ __global__ __launch_bounds__(512, 2) void k_mmq_cls(const mmq_args p) {
         }
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const int slot = (4 * c + h) ^ (2 * c16);
+            const int slot = mc_slot(c16, 4 * c + h);
             const long ahi = *(const long *) (ph + ra * 256 + 8 * slot);
             const long alo = *(const long *) (pl + ra * 256 + 8 * slot);
 #pragma unroll
@@ -552,6 +558,10 @@ __global__ __launch_bounds__(512, 2) void k_mmq_cls(const mmq_args p) {
                 for (int i = 0; i < 4; ++i) summs[n][i] = fmaf(z[i], -dy * wdm[16 * rg + 4 * h + i], summs[n][i]);
             }
         }
+    };
+    for (int64_t b = 0; b < p.nblk; b += 2) {
+        block(b, wr, wr1);
+        if (b + 1 < p.nblk) block(b + 1, wr1, wr);
     }
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
