@@ -921,14 +921,15 @@ struct dc_smem {
     int nrs[2];                         // positions to run, per stage
     float mpub[2];                      // [head]: running max through the first half of the chunk
     int mseq[2];                        // [head]: chunk number + 1 that mpub belongs to
+    int qseq[2][2];                     // [head][half]: chunk number + 1 whose odd-quarter scores are in
     float mcar[2];                      // [head]: running max through the whole chunk
     uint64_t etab[32];                  // expf's table (lx_exp2f_tab)
     float ol[2 * 128];
     uint16_t vl[2][2][DC_CH * 128];     // [head][stage][position][dim]
 };
 
-__global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
-    constexpr int D = 128, NM = D / 16, CH = DC_CH, U = DC_U, NPH = CH / 32;   // NPH: score passes per half
+__global__ __launch_bounds__(768, 1) void k_fattn_dec2(const fa_args a) {
+    constexpr int D = 128, NM = D / 16, CH = DC_CH, U = DC_U, NPQ = CH / 64;   // NPQ: score passes per quarter
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     kt_enter(a.kt);
     const int64_t hp = blockIdx.x;          // head pair: heads 2 hp, 2 hp + 1
@@ -940,24 +941,26 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
     const char * mrow = a.mask ? a.mask + (0 % a.mask_ne1) * a.nbm1 : nullptr;
     if (tid < 32) sm.etab[tid] = lx_exp2f_tab[tid];
     if (tid < 2) { sm.mseq[tid] = 0; sm.mcar[tid] = -INFINITY; }
+    if (tid < 4) sm.qseq[tid >> 1][tid & 1] = 0;
     __syncthreads();
 
     if (wave >= 4) {
-        // ===== producers: head ph, positions 64 hf .. 64 hf + 63 of each chunk =====
-        const int pw = wave - 4, ph = pw >> 1, hf = pw & 1;
+        // ===== producers: head ph, quarter qt (positions 32 qt .. 32 qt + 31) of each chunk; the
+        // even quarters also form the prefix max and coefficients of their half (64 hf .. +63) =====
+        const int pw = wave - 4, ph = pw >> 2, qt = pw & 3, hf = qt >> 1;
+        const bool cw = (qt & 1) == 0;   // the coefficient wave of half hf
         const int64_t h = 2 * hp + ph, hk = h / G;
         const int qd = lane & 3;
         const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
         const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
-        const bool dma = ph == 0 || !vsh;
         auto mask_at = [&](int64_t j) -> uint16_t {   // f16 bits; 0xfc00 (-inf) past the cache
             if (j >= a.n_kv) return 0xfc00;
             return mrow ? *(const uint16_t *) (mrow + 2 * j) : (uint16_t) 0;
         };
-        auto load_k = [&](int64_t c0, int jmax, uint2 (&kh)[NPH][NM]) {   // this half's K rows (<= jmax)
+        auto load_k = [&](int64_t c0, int jmax, uint2 (&kh)[NPQ][NM]) {   // this quarter's K rows (<= jmax)
 #pragma unroll
-            for (int p = 0; p < NPH; ++p) {
-                const int j = min(64 * hf + 16 * p + (lane >> 2), jmax);
+            for (int p = 0; p < NPQ; ++p) {
+                const int j = min(32 * qt + 16 * p + (lane >> 2), jmax);
                 const char * krow = kbase + (c0 + j) * a.nbk1 + 8 * qd;
 #pragma unroll
                 for (int m = 0; m < NM; ++m) kh[p][m] = ld8(krow + 32 * m);
@@ -969,7 +972,7 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
         };
         // chunk 0's K rows go out with q and the mask (bounded by the cache, not yet by the mask);
         // later chunks' go out right after the previous chunk's scores
-        uint2 kh[NPH][NM];
+        uint2 kh[NPQ][NM];
         if (nchunk > 0) load_k(0, (int) min<int64_t>(CH, a.n_kv) - 1, kh);
         uint16_t mc0 = mask_at(lane), mc1 = mask_at(64 + lane);
         float qf[NM][4];
@@ -1004,22 +1007,23 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
                 // the next chunk's mask, in flight under this one
                 mc0 = mask_at(c0 + CH + lane);
                 mc1 = mask_at(c0 + CH + 64 + lane);
-                const float mv = h2f(hf ? m1b : m0b);   // this half's positions: jl = 64 hf + lane
+                const float mv = h2f(hf ? m1b : m0b);   // lane's position 64 hf + lane (the coefficient wave's)
                 const int jl = 64 * hf + lane;
                 float * mkp = sm.mk[ph][st];
                 float * scp = sm.sc[ph][st];
                 float * cmp = sm.cm[ph][st];
-                mkp[jl] = mv;
-                if (hf && lane < 2 * U) { mkp[CH + lane] = -INFINITY; cmp[CH + lane] = 1.0f; scp[CH + lane] = 0.0f; }
+                // this quarter's mask values: position 32 qt + i is lane (32 (qt & 1) + i)'s value of half hf
+                if ((lane >> 5) == (qt & 1)) mkp[jl] = mv;
+                if (qt == 3 && lane < 2 * U) { mkp[CH + lane] = -INFINITY; cmp[CH + lane] = 1.0f; scp[CH + lane] = 0.0f; }
                 const float mcarry = sm.mcar[ph];   // through the previous chunk (published before the last barrier)
                 float tot = mcarry;
                 if (nrun > 0) {
-                    const int lo = 64 * hf, hi = min(nrun, lo + 64);   // this half's rows to run: [lo, hi)
+                    const int lo = 32 * qt;   // this quarter's rows to score: [lo, min(nrun, lo + 32))
                     mark(0);
-                    // V rows this wave stages: its half of the chunk, or with one KV head for both
-                    // heads a quarter (LDS-DMA issue runs at ~25 GB/s per wave)
-                    const int vlo = vsh ? 32 * pw : lo, vhi = min(nrun, vsh ? vlo + 32 : lo + 64);
-                    if ((vsh || dma) && vhi > vlo) {
+                    // V rows this wave stages: with one KV head for both heads 16 rows per producer
+                    // wave, else its quarter of its head's stage (LDS-DMA issue runs at ~25 GB/s per wave)
+                    const int vlo = vsh ? 16 * pw : lo, vhi = min(nrun, vsh ? vlo + 16 : lo + 32);
+                    if (vhi > vlo) {
                         // 4 rows per instruction; the row address advances by addition (a 64-bit
                         // multiply per instruction made the issue loop ~100 cycles per KiB)
                         const int r_in = lane >> 4, col = lane & 15;
@@ -1037,13 +1041,11 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
                     }
                     dc_wave_lds_order();                        // mask values, read back by other lanes
                     mark(1);
-                    // the mask values of this lane's positions in one LDS round trip, then the
-                    // passes up to nrun (computing all four at small depth cost more than it hid)
-                    float mj[NPH];
+                    float mj[NPQ];
 #pragma unroll
-                    for (int p = 0; p < NPH; ++p) mj[p] = mkp[lo + 16 * p + (lane >> 2)];
+                    for (int p = 0; p < NPQ; ++p) mj[p] = mkp[lo + 16 * p + (lane >> 2)];
 #pragma unroll
-                    for (int p = 0; p < NPH; ++p) {
+                    for (int p = 0; p < NPQ; ++p) {
                         if (lo + 16 * p >= nrun) break;
                         const int j = lo + 16 * p + (lane >> 2);
                         const float w = dot_f16_mix_d128(kh[p], qf, nz);
@@ -1053,64 +1055,72 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dec2(const fa_args a) {
                             scp[j] = __fadd_rn(sv, __fmul_rn(slope, mj[p]));
                         }
                     }
-                    // the next chunk's K rows, in flight under this chunk's coefficients and the
-                    // chains' recurrence
-                    // (bounded by the cache only: waiting for the next chunk's mask here would also
-                    // wait for this chunk's V DMA, issued after it)
+                    // the next chunk's K rows, in flight under the coefficients and the chains'
+                    // recurrence (bounded by the cache only: waiting for the next chunk's mask here
+                    // would also wait for this chunk's V DMA, issued after it)
                     if (c + 1 < nchunk) {
                         load_k(c0 + CH, (int) min<int64_t>(CH, a.n_kv - c0 - CH) - 1, kh);
                         kout = true;
                     }
                     dc_wave_lds_order();
-                    mark(2);
-                    // prefix max over the chunk: this half's scan, the first half's total from LDS
-                    const bool live = mv != -INFINITY && jl < nrun;
-                    const float sj = live ? scp[jl] : -INFINITY;
-                    const float smx = wave_scan_max(sj);
-                    const float th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(smx), 63));
-                    float base = mcarry;   // running max before this half
-                    if (hf == 0) {
-                        if (lane == 0) {
-                            // LDS only, in order: the value, its write done, then the sequence word
-                            // (a workgroup-scope fence would also wait for this wave's V DMA and K loads)
-                            lds_st(&sm.mpub[ph], fmaxf(mcarry, th));
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                            lds_st(&sm.mseq[ph], (int) c + 1);
-                        }
-                    } else {
-                        // the first half of the same head publishes its max within its own chunk work
-                        int guard = 0;
-                        while (lds_ld(&sm.mseq[ph]) != (int) c + 1 && ++guard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
-                        base = lds_ld(&sm.mpub[ph]);
+                    if (!cw) {
+                        // the odd quarter hands its scores and mask values to its half's coefficient wave
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        if (lane == 0) lds_st(&sm.qseq[ph][hf], (int) c + 1);
                     }
-                    const float M = fmaxf(base, dpp_ninf<0x138>(smx));   // max over every position before jl
-                    float msv, vsv;
-                    if (!live) { msv = 1.0f; vsv = 0.0f; }
-                    else if (sj > M) { msv = M == -INFINITY ? 0.0f : lx_expf_t(M - sj, (const uint64_t *) sm.etab); vsv = 1.0f; }
-                    else { msv = 1.0f; vsv = lx_expf_t(sj - M, (const uint64_t *) sm.etab); }
-                    cmp[jl] = msv;
-                    scp[jl] = vsv;
-                    // batch flags: a dead position, a max update or padding past nrun
-                    const bool gen = jl < nrun ? (!live || sj > M) : (jl < nrun + U);
-                    const unsigned long long wb = __ballot(gen);
-                    uint32_t f = 0;
-#pragma unroll
-                    for (int bb = 0; bb < 64 / U; ++bb) f |= ((wb >> (U * bb)) & ((1ull << U) - 1)) ? 1u << bb : 0u;
-                    if (lane == 0) sm.bfl[ph][st][hf] = f;
-                    tot = fmaxf(base, th);
+                    mark(2);
+                    if (cw) {
+                        int qguard = 0;
+                        while (lds_ld(&sm.qseq[ph][hf]) != (int) c + 1 && ++qguard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
+                        // prefix max over the chunk: this half's scan, the first half's total from LDS
+                        const bool live = mv != -INFINITY && jl < nrun;
+                        const float sj = live ? scp[jl] : -INFINITY;
+                        const float smx = wave_scan_max(sj);
+                        const float th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(smx), 63));
+                        float base = mcarry;   // running max before this half
+                        if (hf == 0) {
+                            if (lane == 0) {
+                                // LDS only, in order: the value, its write done, then the sequence word
+                                // (a workgroup-scope fence would also wait for this wave's V DMA and K loads)
+                                lds_st(&sm.mpub[ph], fmaxf(mcarry, th));
+                                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                                lds_st(&sm.mseq[ph], (int) c + 1);
+                            }
+                        } else {
+                            // the first half of the same head publishes its max within its own chunk work
+                            int guard = 0;
+                            while (lds_ld(&sm.mseq[ph]) != (int) c + 1 && ++guard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
+                            base = lds_ld(&sm.mpub[ph]);
+                        }
+                        const float M = fmaxf(base, dpp_ninf<0x138>(smx));   // max over every position before jl
+                        float msv, vsv;
+                        if (!live) { msv = 1.0f; vsv = 0.0f; }
+                        else if (sj > M) { msv = M == -INFINITY ? 0.0f : lx_expf_t(M - sj, (const uint64_t *) sm.etab); vsv = 1.0f; }
+                        else { msv = 1.0f; vsv = lx_expf_t(sj - M, (const uint64_t *) sm.etab); }
+                        cmp[jl] = msv;
+                        scp[jl] = vsv;
+                        // batch flags: a dead position, a max update or padding past nrun
+                        const bool gen = jl < nrun ? (!live || sj > M) : (jl < nrun + U);
+                        const unsigned long long wb = __ballot(gen);
+                        uint32_t f = 0;
+    #pragma unroll
+                        for (int bb = 0; bb < 64 / U; ++bb) f |= ((wb >> (U * bb)) & ((1ull << U) - 1)) ? 1u << bb : 0u;
+                        if (lane == 0) sm.bfl[ph][st][hf] = f;
+                        tot = fmaxf(base, th);
+                    }
                     mark(3);
                 } else {
-                    if (hf == 0 && lane == 0) lds_st(&sm.mseq[ph], (int) c + 1);
+                    if (cw && hf == 0 && lane == 0) lds_st(&sm.mseq[ph], (int) c + 1);
                     if (c + 1 < nchunk) {
                         load_k(c0 + CH, (int) min<int64_t>(CH, a.n_kv - c0 - CH) - 1, kh);
                         kout = true;
                     }
                 }
-                if (hf == 1 && lane == 0) sm.mcar[ph] = nrun > 0 ? tot : mcarry;   // read after the barrier
+                if (cw && hf == 1 && lane == 0) sm.mcar[ph] = nrun > 0 ? tot : mcarry;   // read after the barrier
                 if (pw == 0 && lane == 0) sm.nrs[st] = nrun;
                 // this wave's V rows are in LDS: everything but the next chunk's K loads (the
-                // NPH x NM loads of load_k, the only vector-memory instructions after the V DMA)
-                if (kout) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPH * NM) : "memory");
+                // NPQ x NM loads of load_k, the only vector-memory instructions after the V DMA)
+                if (kout) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPQ * NM) : "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 mark(4);
             }
@@ -1240,7 +1250,7 @@ bool fattn_dec2_ok(const fa_args & a, int64_t nq3) {
 }
 
 void launch_fattn_dec2(hipStream_t st, const fa_args & a, int64_t nq3) {
-    hipLaunchKernelGGL(k_fattn_dec2, dim3((unsigned) (a.H / 2), (unsigned) nq3), dim3(512), 0, st, a);
+    hipLaunchKernelGGL(k_fattn_dec2, dim3((unsigned) (a.H / 2), (unsigned) nq3), dim3(768), 0, st, a);
 }
 
 void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
