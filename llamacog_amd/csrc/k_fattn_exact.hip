@@ -928,7 +928,7 @@ struct dc_smem {
     uint16_t vl[2][2][DC_CH * 128];     // [head][stage][position][dim]
 };
 
-__global__ __launch_bounds__(768, 1) void k_fattn_dec2(const fa_args a) {
+__global__ __launch_bounds__(FA_DEC2_THREADS, 1) void k_fattn_dec2(const fa_args a) {
     constexpr int D = 128, NM = D / 16, CH = DC_CH, U = DC_U, NPQ = CH / 64;   // NPQ: score passes per quarter
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     kt_enter(a.kt);
@@ -1250,7 +1250,7 @@ bool fattn_dec2_ok(const fa_args & a, int64_t nq3) {
 }
 
 void launch_fattn_dec2(hipStream_t st, const fa_args & a, int64_t nq3) {
-    hipLaunchKernelGGL(k_fattn_dec2, dim3((unsigned) (a.H / 2), (unsigned) nq3), dim3(768), 0, st, a);
+    hipLaunchKernelGGL(k_fattn_dec2, dim3((unsigned) (a.H / 2), (unsigned) nq3), dim3(FA_DEC2_THREADS), 0, st, a);
 }
 
 void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
