@@ -756,7 +756,7 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
         const uint16_t * ks = kl[s];
         const uint16_t * ms = ml[s];
         // ---- phase 1: scores of the wave's 4 pairs x 64 positions --------------------------
-#pragma unroll 2
+#pragma unroll 4
         for (int r = 0; r < PF_CH / 4; ++r) {
             const int j = 4 * r + r1;
             uint2 kh[NM];
