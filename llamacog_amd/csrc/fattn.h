@@ -37,8 +37,9 @@ extern unsigned long long * g_fa_prof;
 // launch the CPU-exact f16 kernel (k_fattn_exact.hip); D in {64, 128, 256}
 void launch_fattn_exact(hipStream_t stream, const fa_args & a, int64_t nq3);
 // decode, D = 128, f16 cache: two heads per workgroup, scores produced under the recurrence
-// (4 chain waves + 8 producer waves)
-constexpr int FA_DEC2_THREADS = 768;
+// (4 chain waves + 2 or 4 producer waves per head: four above FA_DEC2_NQ4_MIN cache positions)
+constexpr int FA_DEC2_NQ4_MIN = 256;
+int fattn_dec2_threads(const fa_args & a);   // the launch's workgroup size (timeline slots)
 bool fattn_dec2_ok(const fa_args & a, int64_t nq3);
 void launch_fattn_dec2(hipStream_t stream, const fa_args & a, int64_t nq3);
 void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int64_t n, float * s);

@@ -100,7 +100,7 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     // recurrence (k_fattn_dec2) where it applies, else k_fattn_exact, one workgroup per head;
     // batches: k_fattn_exact's prefill tiles
     if (fattn_dec2_ok(a, nq3)) {
-        a.kt = ctx.kt_take("fa_dec2", (unsigned) (a.H / 2 * nq3), FA_DEC2_THREADS);
+        a.kt = ctx.kt_take("fa_dec2", (unsigned) (a.H / 2 * nq3), (unsigned) fattn_dec2_threads(a));
         launch_fattn_dec2(ctx.stream, a, nq3);
     } else {
         if (a.n_q == 1) a.kt = ctx.kt_take("fa_exact", (unsigned) (a.H * nq3), 256);

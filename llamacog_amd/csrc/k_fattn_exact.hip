@@ -928,8 +928,13 @@ struct dc_smem {
     uint16_t vl[2][2][DC_CH * 128];     // [head][stage][position][dim]
 };
 
-__global__ __launch_bounds__(FA_DEC2_THREADS, 1) void k_fattn_dec2(const fa_args a) {
-    constexpr int D = 128, NM = D / 16, CH = DC_CH, U = DC_U, NPQ = CH / 64;   // NPQ: score passes per quarter
+// NQ producer waves per head: 4 (768 threads) for long caches, 2 (512) where one or two chunks
+// leave the producers little to overlap (four cost ~0.6 us per layer more at 136 positions and
+// save ~9 us at 4096)
+template <int NQ>
+__global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_args a) {
+    constexpr int D = 128, NM = D / 16, CH = DC_CH, U = DC_U;
+    constexpr int PQ = CH / NQ, NPQ = PQ / 16;   // positions per producer wave, score passes over them
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     kt_enter(a.kt);
     const int64_t hp = blockIdx.x;          // head pair: heads 2 hp, 2 hp + 1
@@ -947,8 +952,8 @@ __global__ __launch_bounds__(FA_DEC2_THREADS, 1) void k_fattn_dec2(const fa_args
     if (wave >= 4) {
         // ===== producers: head ph, quarter qt (positions 32 qt .. 32 qt + 31) of each chunk; the
         // even quarters also form the prefix max and coefficients of their half (64 hf .. +63) =====
-        const int pw = wave - 4, ph = pw >> 2, qt = pw & 3, hf = qt >> 1;
-        const bool cw = (qt & 1) == 0;   // the coefficient wave of half hf
+        const int pw = wave - 4, ph = pw / NQ, qt = pw % NQ, hf = qt / (NQ / 2);
+        const bool cw = NQ == 2 || (qt & 1) == 0;   // the coefficient wave of half hf
         const int64_t h = 2 * hp + ph, hk = h / G;
         const int qd = lane & 3;
         const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
@@ -960,7 +965,7 @@ __global__ __launch_bounds__(FA_DEC2_THREADS, 1) void k_fattn_dec2(const fa_args
         auto load_k = [&](int64_t c0, int jmax, uint2 (&kh)[NPQ][NM]) {   // this quarter's K rows (<= jmax)
 #pragma unroll
             for (int p = 0; p < NPQ; ++p) {
-                const int j = min(32 * qt + 16 * p + (lane >> 2), jmax);
+                const int j = min(PQ * qt + 16 * p + (lane >> 2), jmax);
                 const char * krow = kbase + (c0 + j) * a.nbk1 + 8 * qd;
 #pragma unroll
                 for (int m = 0; m < NM; ++m) kh[p][m] = ld8(krow + 32 * m);
@@ -1013,16 +1018,16 @@ __global__ __launch_bounds__(FA_DEC2_THREADS, 1) void k_fattn_dec2(const fa_args
                 float * scp = sm.sc[ph][st];
                 float * cmp = sm.cm[ph][st];
                 // this quarter's mask values: position 32 qt + i is lane (32 (qt & 1) + i)'s value of half hf
-                if ((lane >> 5) == (qt & 1)) mkp[jl] = mv;
-                if (qt == 3 && lane < 2 * U) { mkp[CH + lane] = -INFINITY; cmp[CH + lane] = 1.0f; scp[CH + lane] = 0.0f; }
+                if (NQ == 2 || (lane >> 5) == (qt & 1)) mkp[jl] = mv;
+                if (qt == NQ - 1 && lane < 2 * U) { mkp[CH + lane] = -INFINITY; cmp[CH + lane] = 1.0f; scp[CH + lane] = 0.0f; }
                 const float mcarry = sm.mcar[ph];   // through the previous chunk (published before the last barrier)
                 float tot = mcarry;
                 if (nrun > 0) {
-                    const int lo = 32 * qt;   // this quarter's rows to score: [lo, min(nrun, lo + 32))
+                    const int lo = PQ * qt;   // this wave's rows to score: [lo, min(nrun, lo + PQ))
                     mark(0);
                     // V rows this wave stages: with one KV head for both heads 16 rows per producer
                     // wave, else its quarter of its head's stage (LDS-DMA issue runs at ~25 GB/s per wave)
-                    const int vlo = vsh ? 16 * pw : lo, vhi = min(nrun, vsh ? vlo + 16 : lo + 32);
+                    const int vlo = vsh ? (PQ / 2) * pw : lo, vhi = min(nrun, vsh ? vlo + PQ / 2 : lo + PQ);
                     if (vhi > vlo) {
                         // 4 rows per instruction; the row address advances by addition (a 64-bit
                         // multiply per instruction made the issue loop ~100 cycles per KiB)
@@ -1063,7 +1068,7 @@ __global__ __launch_bounds__(FA_DEC2_THREADS, 1) void k_fattn_dec2(const fa_args
                         kout = true;
                     }
                     dc_wave_lds_order();
-                    if (!cw) {
+                    if (NQ == 4 && !cw) {
                         // the odd quarter hands its scores and mask values to its half's coefficient wave
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         if (lane == 0) lds_st(&sm.qseq[ph][hf], (int) c + 1);
@@ -1071,7 +1076,8 @@ __global__ __launch_bounds__(FA_DEC2_THREADS, 1) void k_fattn_dec2(const fa_args
                     mark(2);
                     if (cw) {
                         int qguard = 0;
-                        while (lds_ld(&sm.qseq[ph][hf]) != (int) c + 1 && ++qguard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
+                        if (NQ == 4)
+                            while (lds_ld(&sm.qseq[ph][hf]) != (int) c + 1 && ++qguard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
                         // prefix max over the chunk: this half's scan, the first half's total from LDS
                         const bool live = mv != -INFINITY && jl < nrun;
                         const float sj = live ? scp[jl] : -INFINITY;
@@ -1249,8 +1255,12 @@ bool fattn_dec2_ok(const fa_args & a, int64_t nq3) {
            (a.qmode == 0 || nq3 == 1);
 }
 
+int fattn_dec2_threads(const fa_args & a) { return a.n_kv > FA_DEC2_NQ4_MIN ? 64 * (4 + 2 * 4) : 64 * (4 + 2 * 2); }
+
 void launch_fattn_dec2(hipStream_t st, const fa_args & a, int64_t nq3) {
-    hipLaunchKernelGGL(k_fattn_dec2, dim3((unsigned) (a.H / 2), (unsigned) nq3), dim3(FA_DEC2_THREADS), 0, st, a);
+    const dim3 grid((unsigned) (a.H / 2), (unsigned) nq3);
+    if (a.n_kv > FA_DEC2_NQ4_MIN) hipLaunchKernelGGL(k_fattn_dec2<4>, grid, dim3(64 * (4 + 2 * 4)), 0, st, a);
+    else hipLaunchKernelGGL(k_fattn_dec2<2>, grid, dim3(64 * (4 + 2 * 2)), 0, st, a);
 }
 
 void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
