@@ -66,6 +66,7 @@ def parse():
     ap.add_argument("--split-config", default="llama3-70b-q4km")
     ap.add_argument("--split-steps", type=int, default=32)
     ap.add_argument("--split-warmup", type=int, default=4)
+    ap.add_argument("--split-timeout", type=int, default=900, help="seconds before the split child is killed")
     ap.add_argument("--split-only", action="store_true", help=argparse.SUPPRESS)   # the series' child process
     return ap.parse_args()
 
@@ -207,7 +208,13 @@ def split_child(a, n: int, visible) -> dict:
            "--steps", str(a.split_steps), "--warmup", str(a.split_warmup), "--model-dir", a.model_dir, "--fa", str(a.fa),
            "--kv", a.kv] + (["--cpu"] if a.cpu else [])
     t0 = time.time()
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=1800, env=env)
+    try:
+        # bounded: a stuck split child (e.g. a hand-off that never completes) costs the series,
+        # never the replica line this process prints afterwards
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=a.split_timeout, env=env)
+    except subprocess.TimeoutExpired as e:
+        err = e.stderr.decode(errors="replace") if isinstance(e.stderr, bytes) else (e.stderr or "")
+        return {"error": f"timed out after {a.split_timeout} s: {err[-400:]}"}
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     if out.returncode != 0 or not lines:
         return {"error": f"rc={out.returncode}: {out.stderr[-400:]}"}
