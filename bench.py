@@ -66,7 +66,9 @@ def parse():
     ap.add_argument("--split-config", default="llama3-70b-q4km")
     ap.add_argument("--split-steps", type=int, default=32)
     ap.add_argument("--split-warmup", type=int, default=4)
-    ap.add_argument("--split-timeout", type=int, default=900, help="seconds before the split child is killed")
+    # the driver bounds the whole bench (600 s): a stuck split child must cost only the series
+    ap.add_argument("--split-timeout", type=int, default=240, help="seconds before the split child is killed")
+    ap.add_argument("--split-pp", type=int, default=512, help="prompt length of the split series' pp figure (0 = skip)")
     ap.add_argument("--split-only", action="store_true", help=argparse.SUPPRESS)   # the series' child process
     return ap.parse_args()
 
@@ -206,7 +208,7 @@ def split_child(a, n: int, visible) -> dict:
         env["HIP_VISIBLE_DEVICES"] = visible
     cmd = [sys.executable, os.path.abspath(__file__), "--split-only", "--gpus", str(n), "--config", a.split_config,
            "--steps", str(a.split_steps), "--warmup", str(a.split_warmup), "--model-dir", a.model_dir, "--fa", str(a.fa),
-           "--kv", a.kv] + (["--cpu"] if a.cpu else [])
+           "--kv", a.kv, "--split-pp", str(a.split_pp)] + (["--cpu"] if a.cpu else [])
     t0 = time.time()
     try:
         # bounded: a stuck split child (e.g. a hand-off that never completes) costs the series,
@@ -233,7 +235,7 @@ def split_only(a):
         gguf_synth.ensure(a.config, path, seed=0)
     t_write = time.time() - t0
     gpu = not a.cpu
-    n_ctx = ((a.warmup + a.steps + 255) // 256 + 1) * 256
+    n_ctx = ((a.warmup + a.steps + max(a.split_pp, 0) + 255) // 256 + 1) * 256
     m = la.Model(path, gpu=gpu, n_ctx=n_ctx, flash_attn=bool(a.fa), kv_type=a.kv,
                  n_gpus=a.gpus if gpu else None, split_mode=1)
     devs = [n for _, n, t in la.devices(m.lib) if n.startswith("MI355X")][:a.gpus] if gpu else ["CPU"]
@@ -241,13 +243,26 @@ def split_only(a):
     if a.warmup > 0:
         m.time_gen(a.warmup)
     t = m.time_gen(a.steps)
+    # pp at this N (one ubatch of split_pp tokens through the layer pipeline, after one warm run)
+    pp_tps = None
+    if a.split_pp > 0:
+        m.clear()
+        m.time_prompt(a.split_pp)
+        m.clear()
+        pp_tps = a.split_pp / m.time_prompt(a.split_pp)
     h1 = la.handoff_stats() if gpu else (0, 0, 0)
     m.close()
     cfg = gguf_synth.CONFIGS[a.config]
+    wb = gguf_synth.weight_bytes_per_token(cfg)
+    tg = a.steps / t
     print(json.dumps({
         "model": a.config, "n_devices": len(devs), "devices": devs, "steps": a.steps, "warmup": a.warmup,
-        "tg_tok_s": round(a.steps / t, 3), "ms_per_token": round(1e3 * t / a.steps, 4),
-        "weight_bytes_per_token": gguf_synth.weight_bytes_per_token(cfg),
+        "tg_tok_s": round(tg, 3), "ms_per_token": round(1e3 * t / a.steps, 4),
+        "pp_tok_s": round(pp_tps, 2) if pp_tps else None, "pp_tokens": a.split_pp,
+        "weight_bytes_per_token": wb,
+        # decode reads every weight byte once per token, one stage after another: the fraction of
+        # ONE GPU's 8 TB/s the pipeline's byte rate reaches (the stages do not stream concurrently)
+        "tg_frac_of_8TBs": round(wb * tg / 8e12, 4),
         "stage_handoffs": dict(zip(("rccl", "peer", "d2d"), (h1[i] - h0[i] for i in range(3)))),
         "gguf_write_s": round(t_write, 1),
         "partition": f"libllama -sm layer over {len(devs)} device(s): contiguous layer ranges, output on the last",

@@ -393,7 +393,11 @@ static ggml_backend_buffer_type_t mi_host_buft() {
 struct mi_hostptr_ctx { void * host; void * dev; size_t size; int device; };
 
 static const char * mi_hostptr_buft_get_name(ggml_backend_buffer_type_t) { return MI355X_NAME "_Mapped"; }
-static bool mi_hostptr_buft_is_host(ggml_backend_buffer_type_t) { return true; }
+// tensor->data in this buffer is the DEVICE mapping of the host range (hipHostGetDevicePointer),
+// which the CPU may not dereference: the buffer is not a host buffer to ggml (the CPU backend's
+// supports_buft and the scheduler's host shortcuts key on is_host); host access goes through
+// get_tensor, at the same offset from the host base
+static bool mi_hostptr_buft_is_host(ggml_backend_buffer_type_t) { return false; }
 
 static void mi_hostptr_free(ggml_backend_buffer_t buffer) {
     auto * c = (mi_hostptr_ctx *) buffer->context;
@@ -407,10 +411,15 @@ static char * mi_hostptr_host_addr(ggml_backend_buffer_t buffer, const ggml_tens
     auto * c = (mi_hostptr_ctx *) buffer->context;
     return (char *) c->host + ((const char *) t->data - (const char *) c->dev);
 }
-static void mi_hostptr_memset(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size_t off, size_t n) { memset(mi_hostptr_host_addr(b, t) + off, v, n); }
-static void mi_hostptr_set(ggml_backend_buffer_t b, ggml_tensor * t, const void * d, size_t off, size_t n) { memcpy(mi_hostptr_host_addr(b, t) + off, d, n); }
+// the wrapped range is the caller's (libllama's read-only model mmap, src/llama-model.cpp:4311-4337):
+// the backend only reads it, and refuses to write into it
+static void mi_hostptr_refuse_write(const char * what) {
+    GGML_ABORT("mi355x: %s on a buffer_from_host_ptr buffer: the wrapped host memory is the caller's and is read-only here", what);
+}
+static void mi_hostptr_memset(ggml_backend_buffer_t, ggml_tensor *, uint8_t, size_t, size_t) { mi_hostptr_refuse_write("memset_tensor"); }
+static void mi_hostptr_set(ggml_backend_buffer_t, ggml_tensor *, const void *, size_t, size_t) { mi_hostptr_refuse_write("set_tensor"); }
 static void mi_hostptr_get(ggml_backend_buffer_t b, const ggml_tensor * t, void * d, size_t off, size_t n) { memcpy(d, mi_hostptr_host_addr(b, t) + off, n); }
-static void mi_hostptr_clear(ggml_backend_buffer_t b, uint8_t v) { auto * c = (mi_hostptr_ctx *) b->context; memset(c->host, v, c->size); }
+static void mi_hostptr_clear(ggml_backend_buffer_t, uint8_t) { mi_hostptr_refuse_write("clear"); }
 
 static const ggml_backend_buffer_i mi_hostptr_iface = {
     /* .free_buffer   = */ mi_hostptr_free,
@@ -509,6 +518,7 @@ static enum ggml_status mi_split_buf_init_tensor(ggml_backend_buffer_t buffer, g
     auto * e = new mi_split_extra{};
     const int64_t nrows = ggml_nrows(tensor);
     const size_t rs = ggml_row_size(tensor->type, tensor->ne[0]);
+    GGML_ASSERT(b->split.size() <= (size_t) MI_MAX_DEV);
     for (int d = 0; d < (int) b->split.size(); ++d) {
         int64_t lo, hi;
         mi_split_rows(b, nrows, d, lo, hi);
@@ -611,6 +621,10 @@ static ggml_backend_buffer_type_t mi_split_buffer_type(int main_device, const fl
     std::lock_guard<std::mutex> lk(mtx);
     const int nd = (int) mi_reg_get_device_count(mi_reg());
     if (main_device < 0 || main_device >= nd) return nullptr;
+    if (nd > MI_MAX_DEV) {   // split_parts holds MI_MAX_DEV slices
+        MI_LOG_WARN("mi355x: row split over %d devices exceeds the %d-device limit\n", nd, MI_MAX_DEV);
+        return nullptr;
+    }
     std::vector<float> w(nd, 0.0f);
     bool any = false;
     for (int i = 0; i < nd; ++i) {
@@ -882,7 +896,8 @@ namespace mi355x {
 bool ktrace_enabled() { return g_ktrace.load(std::memory_order_relaxed) != 0; }
 
 unsigned long long * exec_ctx::kt_take(const char * name, unsigned nwg, unsigned threads) {
-    if (!kt_buf) return nullptr;
+    // the buffer outlives a traced run; untraced launches get no region (no stamps, no perturbation)
+    if (!kt_buf || !ktrace_enabled()) return nullptr;
     const unsigned stride = 1 + threads / 64;
     const size_t n = (size_t) nwg * stride;
     if (kt_off + n > kt_cap) return nullptr;
@@ -1408,8 +1423,8 @@ static ggml_backend_reg_t mi_reg() {
         // GGML_MI355X_VDEV=k (k > 1): k ggml devices over HIP device 0 — libllama's multi-device
         // paths (layer split with the scheduler's pipeline copies and cpy_tensor_async hand-offs,
         // row split) then run on a one-GPU box; each virtual device has its own buffers and streams
-        const int vdev = getenv("GGML_MI355X_VDEV") ? atoi(getenv("GGML_MI355X_VDEV")) : 0;
-        const int nd = (vdev > 1 && n >= 1) ? vdev : n;
+        const int vdev = getenv("GGML_MI355X_VDEV") ? std::min(atoi(getenv("GGML_MI355X_VDEV")), MI_MAX_DEV) : 0;
+        const int nd = (vdev > 1 && n >= 1) ? vdev : std::min(n, MI_MAX_DEV);
         ctx->dev_ctx.reserve(nd);
         ctx->devices.reserve(nd);
         for (int i = 0; i < nd; ++i) {

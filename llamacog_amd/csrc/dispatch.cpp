@@ -155,7 +155,11 @@ void op_mul_mat(exec_ctx & ctx, ggml_tensor * dst) {
 // ---- row-split weights ------------------------------------------------------------------------
 // One helper execution context per physical device for the slices that live on another GPU
 // than the computing backend's (each has its own stream and scratch; enqueueing is serialised)
-struct split_helper { exec_ctx ex; std::mutex mtx; bool init = false; };
+// ein[d]: recorded on device d's computing stream, waited on by the helper; eout: recorded on the
+// helper stream, waited on by the computing stream.  Reused from slice to slice (a stream wait
+// takes the event's most recent record at the time of the wait), so no event is created per
+// slice and no host sync is needed: buffer reuse is ordered by the two streams' waits
+struct split_helper { exec_ctx ex; std::mutex mtx; bool init = false; hipEvent_t eout = nullptr; hipEvent_t ein[MI_MAX_DEV] = {}; };
 static split_helper g_split_helpers[MI_MAX_DEV];
 
 static exec_ctx & split_helper_ctx(int hip, std::unique_lock<std::mutex> & lk) {
@@ -166,6 +170,7 @@ static exec_ctx & split_helper_ctx(int hip, std::unique_lock<std::mutex> & lk) {
         MI_CHECK(hipSetDevice(hip));
         h.ex.device = hip;
         MI_CHECK(hipStreamCreateWithFlags(&h.ex.stream, hipStreamNonBlocking));
+        MI_CHECK(hipEventCreateWithFlags(&h.eout, hipEventDisableTiming));
         h.init = true;
     }
     return h.ex;
@@ -231,9 +236,11 @@ void op_mul_mat_split(exec_ctx & ctx, ggml_tensor * dst) {
         g_split_foreign.fetch_add(1);
         std::unique_lock<std::mutex> lk;
         exec_ctx & hx = split_helper_ctx(p.hip, lk);
-        hipEvent_t ein, eout;
+        split_helper & hh = g_split_helpers[p.hip];
+        GGML_ASSERT(ctx.device >= 0 && ctx.device < MI_MAX_DEV);
         MI_CHECK(hipSetDevice(ctx.device));
-        MI_CHECK(hipEventCreateWithFlags(&ein, hipEventDisableTiming));
+        if (!hh.ein[ctx.device]) MI_CHECK(hipEventCreateWithFlags(&hh.ein[ctx.device], hipEventDisableTiming));
+        hipEvent_t ein = hh.ein[ctx.device], eout = hh.eout;
         MI_CHECK(hipEventRecord(ein, ctx.stream));
         MI_CHECK(hipSetDevice(p.hip));
         MI_CHECK(hipStreamWaitEvent(hx.stream, ein, 0));
@@ -247,16 +254,13 @@ void op_mul_mat_split(exec_ctx & ctx, ggml_tensor * dst) {
         hx.qcache_clear();
         mul_mat_slice(hx, dst, p, &x, hbuf + ((b1 + 255) / 256) * 256);
         MI_CHECK(hipMemcpyPeerAsync(tmp, ctx.device, hbuf + ((b1 + 255) / 256) * 256, p.hip, bo, hx.stream));
-        MI_CHECK(hipEventCreateWithFlags(&eout, hipEventDisableTiming));
         MI_CHECK(hipEventRecord(eout, hx.stream));
         MI_CHECK(hipSetDevice(ctx.device));
         MI_CHECK(hipStreamWaitEvent(ctx.stream, eout, 0));
+        // tmp is rewritten by the next foreign slice only after that slice's ein, recorded on
+        // this stream behind the gather below
         MI_CHECK(hipMemcpy2DAsync((char *) dst->data + p.lo * sizeof(float), M * sizeof(float), tmp, rows * sizeof(float),
                                   rows * sizeof(float), T, hipMemcpyDeviceToDevice, ctx.stream));
-        // the events are released once the stream has passed them
-        MI_CHECK(hipStreamSynchronize(ctx.stream));
-        MI_CHECK(hipEventDestroy(ein));
-        MI_CHECK(hipEventDestroy(eout));
     }
 }
 

@@ -1076,8 +1076,14 @@ __global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_ar
                     mark(2);
                     if (cw) {
                         int qguard = 0;
-                        if (NQ == 4)
-                            while (lds_ld(&sm.qseq[ph][hf]) != (int) c + 1 && ++qguard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
+                        if (NQ == 4) {
+                            // bounded: a hand-off that never completes traps rather than reading stale scores
+                            while (lds_ld(&sm.qseq[ph][hf]) != (int) c + 1) {
+                                __builtin_amdgcn_s_sleep(1);
+                                if (++qguard > (1 << 24)) __builtin_trap();
+                            }
+                            asm volatile("" ::: "memory");   // the score reads stay after the wait
+                        }
                         // prefix max over the chunk: this half's scan, the first half's total from LDS
                         const bool live = mv != -INFINITY && jl < nrun;
                         const float sj = live ? scp[jl] : -INFINITY;
@@ -1095,7 +1101,11 @@ __global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_ar
                         } else {
                             // the first half of the same head publishes its max within its own chunk work
                             int guard = 0;
-                            while (lds_ld(&sm.mseq[ph]) != (int) c + 1 && ++guard < (1 << 22)) __builtin_amdgcn_s_sleep(1);
+                            while (lds_ld(&sm.mseq[ph]) != (int) c + 1) {
+                                __builtin_amdgcn_s_sleep(1);
+                                if (++guard > (1 << 24)) __builtin_trap();
+                            }
+                            asm volatile("" ::: "memory");
                             base = lds_ld(&sm.mpub[ph]);
                         }
                         const float M = fmaxf(base, dpp_ninf<0x138>(smx));   // max over every position before jl

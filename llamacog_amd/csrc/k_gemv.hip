@@ -611,6 +611,334 @@ __global__ __launch_bounds__(256) void k_gemv_os2(const gemv_args p1, const int6
 }
 
 
+// ---- persistent loader / consumer engine (k_gemv_eng) --------------------------------------------
+// One workgroup per CU streams a contiguous range of rows (over the launch's matrices) through an
+// LDS ring, with the roles of MI355X_MICROARCH.md's ldsdma-fill / engine rows:
+//   * wave 0, the loader, walks the workgroup's CHUNKS in order (a chunk = 64 tasks of one row:
+//     16 K-quant super-blocks or 64 Q8_0 / Q4_0 blocks, the one-shot kernel's wave slice) and
+//     copies each HBM -> ring slot k % ns with LDS-DMA (1 KiB per wave instruction, nt), keeping
+//     L = 60 / P chunks in flight (P instructions per chunk; vmcnt counts at most 63); after
+//     issuing chunk k it waits vmcnt(L * P), i.e. for chunk k - L, and publishes it (full[slot]);
+//     before reusing a slot it waits for the consumer that read it (fre[slot]);
+//   * waves 1 .. NC, the consumers, own rows c, c + NC, ... of the workgroup; per chunk they wait
+//     for full[slot], read their task's bytes into registers, hand the slot back, and run the
+//     unchanged records (qtypes.h) and the walker, whose fp32 chain carries from chunk to chunk in
+//     block order — the row's bits are the one-shot kernel's.
+// The activation lives in LDS, formed once per workgroup while the loader's first chunks are in
+// flight: a copy of the quantized activation, the RMS-norm prologue from the residual producer's
+// partial sums, or the SwiGLU product silu(gate) * up of the FFN (the k_mul_quant arithmetic).
+// The weight stream therefore never waits for a prologue, and no launch of its own forms one.
+constexpr int ENG_LDS = 160 * 1024;
+constexpr int ENG_NSMAX = 96;
+constexpr int ENG_CTRL = 1024;   // bytes of control words in front of the activation
+
+struct eng_geo {
+    int64_t rows;        // rows over the launch's matrices
+    int ns;              // ring slots
+    int nch;             // chunks per row
+    int last_bytes;      // weight bytes of a row's last chunk
+    int act_mode;        // 0: copy p.A; 1: RMS-norm prologue (p.pro); 2: SwiGLU prologue
+    int qmode;           // activation quantization: 1 Q8_K, 2 Q8_0
+    int64_t n;           // activation length (K)
+    uint32_t rec_off, ring_off, slot;
+    const float * sw_gate; const float * sw_up;   // act_mode 2
+};
+
+// LDS layout of the control words
+struct eng_ctrl {
+    int full[ENG_NSMAX];   // chunk number last landed in the slot
+    int fre[ENG_NSMAX];    // chunk number last consumed from the slot
+    int rdy;               // consumer waves done forming the activation
+    float pmean;
+    double rpart[16];      // residual producer: sum of squares per consumer wave
+};
+static_assert(sizeof(eng_ctrl) <= ENG_CTRL, "engine control words");
+
+template <class V> __device__ __forceinline__ V eng_ld(V * p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+template <class V> __device__ __forceinline__ void eng_st(V * p, V v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+// 16 B per lane HBM -> LDS as inline asm: the compiler sees no LDS write in flight and adds no
+// vmcnt(0) before the loader's LDS flag accesses (k_fattn_exact.hip lds_dma16); nt: read once
+__device__ __forceinline__ void eng_dma16(const void * src, const void * lds) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (gemv_lds_t) lds);
+#if MI_WNT
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(m), "v"(src) : "memory", "m0");
+#else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+#endif
+}
+
+// bounded LDS spin: a hand-off that never completes traps instead of hanging the device
+__device__ __forceinline__ void eng_wait_eq(int * w, int v) {
+    for (int it = 0; eng_ld(w) != v; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        if (it > (1 << 24)) __builtin_trap();
+    }
+}
+
+// the fp32 chain of one row carried over its chunks (qtypes.h walk(), split at chunk bounds)
+template <class T> struct eng_walk;
+template <> struct eng_walk<g_q4_K> {
+    float A = 0.0f, B = 0.0f;
+    __device__ void step(const uint32_t * rr, int nb, int) {
+        for (int b = 0; b < nb; ++b) {
+            const uint4 r = *(const uint4 *) (rr + b * g_q4_K::RS);
+            A = fmaf((float) (int) r.x, asf(r.z), A);
+            B = fmaf((float) (int) r.y, asf(r.w), B);
+        }
+    }
+    __device__ float result() const { return __fsub_rn(A, B); }
+};
+template <> struct eng_walk<g_q4_0> {
+    float A = 0.0f;
+    __device__ void step(const uint32_t * rr, int nb, int) {
+        for (int b = 0; b < nb; ++b) {
+            const uint2 r = *(const uint2 *) (rr + b * g_q4_0::RS);
+            A = fmaf((float) (int) r.x, asf(r.y), A);
+        }
+    }
+    __device__ float result() const { return A; }
+};
+template <class T, int FO> struct eng_walk_cls {   // class chains (LPR = 8), scale product at dword FO
+    float acc = 0.0f;
+    __device__ void step(const uint32_t * rr, int nb, int s) {
+        for (int b = 0; b < nb; ++b) acc = fmaf(asf(rr[b * T::RS + FO]), (float) (int) rr[b * T::RS + s], acc);
+    }
+    __device__ float result() const { return hsum8_lanes(acc); }
+};
+template <> struct eng_walk<g_q6_K> : eng_walk_cls<g_q6_K, 8> {};
+template <> struct eng_walk<g_q8_0> : eng_walk_cls<g_q8_0, 8> {};
+template <> struct eng_walk<g_q5_K> {
+    float acc = 0.0f, summs = 0.0f;
+    __device__ void step(const uint32_t * rr, int nb, int s) {
+        for (int b = 0; b < nb; ++b) {
+            acc = fmaf(asf(rr[b * g_q5_K::RS + 9]), (float) (int) rr[b * g_q5_K::RS + s], acc);
+            summs = fmaf((float) (int) rr[b * g_q5_K::RS + 8], asf(rr[b * g_q5_K::RS + 10]), summs);
+        }
+    }
+    __device__ float result() const { return __fadd_rn(hsum8_lanes(acc), summs); }
+};
+
+// the activation of consumer wave cw (of NC) into LDS, in the gemv_act layout at buf
+template <int NC>
+__device__ __forceinline__ void eng_act(const gemv_args & p, const eng_geo & e, uint8_t * buf, int cw, int lane, eng_ctrl * cc) {
+    const int64_t n = e.n;
+    const bool kq = e.qmode == 1;
+    const int64_t nd = kq ? n / 256 : n / 32, nsum = kq ? n / 16 : n / 32;
+    int8_t * qs = (int8_t *) buf;
+    float * qd = (float *) (buf + n);
+    int16_t * qsum = (int16_t *) (buf + n + 4 * nd);
+    const int NB = (int) (n / 256);
+    if (e.act_mode == 0) {
+        const int tc = cw * 64 + lane;
+        for (int64_t o = 16 * (int64_t) tc; o < n; o += 16 * 64 * NC) *(uint4 *) (qs + o) = *(const uint4 *) (p.A.qs + o);
+        for (int64_t o = tc; o < nd; o += 64 * NC) qd[o] = p.A.d[o];
+        for (int64_t o = tc; o < nsum; o += 64 * NC) qsum[o] = p.A.s[o];
+        return;
+    }
+    float scale = 1.0f;
+    if (e.act_mode == 1) {
+        const auto & r = p.pro;
+        const double s = wave_sum(r.sum[RSUM_STRIDE * lane]);   // a fixed tree: the same s in every wave
+        float mean;
+        if (!rms_mean_decided(s, n, mean)) mean = rms_mean_sequential(r.x, nullptr, n);   // rare (~1e-5 of rows)
+        scale = 1.0f / sqrtf(mean + r.eps);
+    }
+    // wave cw, row of 16 lanes (lane >> 4): 256-element block b, lane owns 16 elements
+    for (int b0 = 0; b0 < NB; b0 += 4 * NC) {
+        const int b = b0 + 4 * cw + (lane >> 4);
+        if (b >= NB) continue;   // whole rows of 16 lanes
+        const int64_t e0 = 256 * (int64_t) b + 16 * (lane & 15);
+        float y[16];
+        if (e.act_mode == 1) {
+            const auto & r = p.pro;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 xv = *(const float4 *) (r.x + e0 + 4 * k);
+                const float4 wv = r.w ? *(const float4 *) (r.w + e0 + 4 * k) : make_float4(1.f, 1.f, 1.f, 1.f);
+                const float xx[4] = {xv.x, xv.y, xv.z, xv.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float yn = __fmul_rn(xx[c], scale);
+                    y[4 * k + c] = r.w ? __fmul_rn(yn, ww[c]) : yn;
+                }
+            }
+        } else {
+            // silu(gate) * up: ggml_vec_silu_f32's AVX-512 ggml_v_silu on the 16-element chunks
+            // (vec.cpp:233; n is a multiple of 256), then the MUL (k_mul_quant's arithmetic)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 gv = *(const float4 *) (e.sw_gate + e0 + 4 * k);
+                const float4 uv = *(const float4 *) (e.sw_up + e0 + 4 * k);
+                const float gg[4] = {gv.x, gv.y, gv.z, gv.w}, uu[4] = {uv.x, uv.y, uv.z, uv.w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float sv = gg[c] / (1.0f + v_expf_avx512(-gg[c]));
+                    y[4 * k + c] = __fmul_rn(sv, uu[c]);
+                }
+            }
+        }
+        if (kq) q8K_row16(y, lane, qs + 256 * (int64_t) b, qsum + 16 * (int64_t) b, qd + b);
+        else q8_0_row16(y, lane, qs + 256 * (int64_t) b, qd + 8 * (int64_t) b, qsum + 8 * (int64_t) b);
+    }
+}
+
+// the weight chunks are reached by scalar arithmetic only (no kernel-argument loads in the loop):
+// the row's matrix, base and stride from SGPR copies of the launch's (up to three) matrices
+struct eng_cursor {
+    const uint8_t * wm; int64_t nbm, row;
+    __device__ void locate(const gemv_args & p, int64_t gr) {
+        if (gr >= p.blk0[2]) { wm = p.W[2]; nbm = p.nb01[2]; row = gr - p.blk0[2]; }
+        else if (gr >= p.blk0[1]) { wm = p.W[1]; nbm = p.nb01[1]; row = gr - p.blk0[1]; }
+        else { wm = p.W[0]; nbm = p.nb01[0]; row = gr; }
+    }
+};
+
+template <class T, int NL, int NC, bool ONECH>
+__global__ __launch_bounds__(64 * (NL + NC)) void k_gemv_eng(const gemv_args p, const eng_geo e) {
+    using G = os_geo<T>;
+    constexpr int P = G::NI;                 // DMA instructions per chunk
+    constexpr int LL = 60 / P / NL;          // chunks in flight per loader (vmcnt holds at most 63)
+    constexpr int BPC = WAVE / T::per_block; // blocks (records) per full chunk
+    __shared__ __attribute__((aligned(16))) uint8_t lds[ENG_LDS];
+    eng_ctrl * cc = (eng_ctrl *) lds;
+    uint8_t * act = lds + ENG_CTRL;
+    uint8_t * ring = lds + e.ring_off;
+    kt_enter(p.kt);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ns = e.ns, nch = e.nch;
+    const int64_t w = blockIdx.x, nwg = gridDim.x;
+    const int64_t r0 = w * e.rows / nwg, r1 = (w + 1) * e.rows / nwg;
+    const int nrows = (int) (r1 - r0);
+    const int nck = nrows * nch;
+    if (threadIdx.x < ENG_NSMAX) {
+        cc->full[threadIdx.x] = -1;
+        cc->fre[threadIdx.x] = (int) threadIdx.x - ns;   // "slot s held chunk s - ns": the first round is free
+    }
+    if (threadIdx.x == 0) cc->rdy = 0;
+    __syncthreads();
+
+    if (wave < NL) {
+        // ---- loader l: chunks l, l + NL, ... ----
+        const int l = wave;
+        // per-lane byte offsets of the P pieces, for a full chunk and for a row's last chunk
+        int ofull[P], olast[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            ofull[q] = min(q * 1024 + 16 * lane, G::SEG - 16);
+            olast[q] = min(q * 1024 + 16 * lane, e.last_bytes - 16);
+        }
+        int j = l;
+        int64_t gr = r0;
+        while (j >= nch) { j -= nch; ++gr; }
+        eng_cursor cu;
+        cu.locate(p, gr);
+        int s = l % ns;
+        int frep = 0;   // fre[] of this loader's next slot, read one chunk ahead
+        int it = 0;
+        for (int k = l; k < nck; k += NL, ++it) {
+            if (k >= ns && frep != k - ns) eng_wait_eq(&cc->fre[s], k - ns);
+            const uint8_t * src = cu.wm + cu.row * cu.nbm + (int64_t) j * G::SEG;
+            uint8_t * dst = ring + (size_t) s * e.slot;
+            const bool lastc = j == nch - 1;
+#pragma unroll
+            for (int q = 0; q < P; ++q) eng_dma16(src + (lastc ? olast[q] : ofull[q]), dst + q * 1024);
+            // advance to this loader's next chunk
+            const int kn = k + NL;
+            s += NL;
+            if (s >= ns) s -= ns;
+            if (kn >= ns && kn < nck) frep = eng_ld(&cc->fre[s]);
+            j += NL;
+            if (j >= nch) {
+                while (j >= nch) { j -= nch; ++gr; }
+                if (gr < r1) cu.locate(p, gr);
+            }
+            if (it >= LL) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LL * P) : "memory");
+                const int kp = k - LL * NL;
+                if (lane == 0) eng_st(&cc->full[kp % ns], kp);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            for (int kk = l + NL * max(0, it - LL); kk < nck; kk += NL) eng_st(&cc->full[kk % ns], kk);
+        }
+    } else {
+        // ---- consumers ----
+        const int cw = wave - NL;
+        eng_act<NC>(p, e, act, cw, lane, cc);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(&cc->rdy, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        eng_wait_eq(&cc->rdy, NC);
+        const bool kq = e.qmode == 1;
+        const int64_t nd = kq ? e.n / 256 : e.n / 32;
+        const gemv_act A = {(const int8_t *) act, (const float *) (act + e.n), (const int16_t *) (act + e.n + 4 * nd)};
+        uint32_t * rr = (uint32_t *) (lds + e.rec_off) + (size_t) cw * BPC * T::RS;
+        const int nblk = p.ntasks / T::per_block;
+        const int ws = lane % T::LPR;
+        typename T::act x0;
+        if constexpr (ONECH) T::load(A, lane < p.ntasks ? lane : 0, x0);
+        double ss = 0.0;
+        for (int i = cw; i < nrows; i += NC) {
+            const int64_t gr = r0 + i;
+            eng_cursor cu;
+            cu.locate(p, gr);
+            const int64_t row = cu.row;
+            const float rc = p.rres ? p.rres[row] : 0.0f;
+            eng_walk<T> wk;
+            for (int j = 0; j < nch; ++j) {
+                const int k = i * nch + j;
+                const int s = k % ns;
+                const int tg = WAVE * j + lane;            // the task in the row
+                const bool active = tg < p.ntasks;
+                eng_wait_eq(&cc->full[s], k);
+                typename T::raw wraw;
+                T::template fetch<typename lds_loader<T>::type>(ring + (size_t) s * e.slot, active ? lane : 0, wraw);
+                // the slot's bytes are in registers (a wave's LDS accesses complete in order)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) eng_st(&cc->fre[s], k);
+                if constexpr (ONECH) {
+                    T::rec(wraw, lane, x0, active, rr);
+                } else {
+                    typename T::act x;
+                    T::load(A, active ? tg : 0, x);
+                    T::rec(wraw, lane, x, active, rr);
+                }
+                wave_lds_sync();
+                wk.step(rr, min(BPC, nblk - BPC * j), ws);
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+            }
+            const float v = wk.result();
+            if (lane == 0) {
+                if (p.rres) {   // ADD(v, res): the CPU's single f32 add
+                    const float xv = __fadd_rn(v, rc);
+                    p.rxsum[row] = xv;
+                    ss = __dadd_rn(ss, (double) __fmul_rn(xv, xv));
+                } else if (gr >= p.blk0[2]) {
+                    p.dst[2][row] = v;
+                } else if (gr >= p.blk0[1]) {
+                    p.dst[1][row] = v;
+                } else {
+                    p.dst[0][row] = v;
+                }
+            }
+        }
+        if (p.rres && lane == 0) cc->rpart[cw] = ss;
+    }
+    if (p.rres) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double tot = 0.0;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) tot = __dadd_rn(tot, cc->rpart[c]);
+            __hip_atomic_fetch_add(p.rsum + RSUM_STRIDE * (w % RSUM_SHARDS), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    kt_exit(p.kt);
+}
+
 // ---- host ----------------------------------------------------------------------------------------
 // kernel-timing mode: the GEMV kernel itself is launched with start/stop events
 // (hipExtLaunchKernel records them at the dispatch's start and completion, without extra
@@ -807,8 +1135,100 @@ static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2,
 #undef OS2_LAUNCH
 }
 
+// ---- engine launches (k_gemv_eng) -----------------------------------------------------------------
+// GGML_MI355X_GEMV_ENG=1 selects the engine (A/B while it is measured); GGML_MI355X_ENG_NC = consumer waves (3, 7, 15)
+static bool eng_enabled() {
+    static const bool on = getenv("GGML_MI355X_GEMV_ENG") && atoi(getenv("GGML_MI355X_GEMV_ENG")) != 0;
+    return on;
+}
+// loader / consumer waves per workgroup: GGML_MI355X_ENG_CFG = 17 (1 + 7), 26, 214 (default), 412
+static int eng_cfg() {
+    static const int c = [] {
+        const int v = getenv("GGML_MI355X_ENG_CFG") ? atoi(getenv("GGML_MI355X_ENG_CFG")) : 214;
+        return v == 17 || v == 26 || v == 412 ? v : 214;
+    }();
+    return c;
+}
+static int eng_nc() { const int c = eng_cfg(); return c == 17 ? 7 : (c == 26 ? 6 : (c == 412 ? 12 : 14)); }
+// the SwiGLU prologue's sources for the next engine launch (gemv_group sets them)
+static thread_local const float * g_sw_gate = nullptr;
+static thread_local const float * g_sw_up = nullptr;
+
+template <class T>
+static bool eng_geometry(const gemv_args & a, int nc, eng_geo & e) {
+    using G = os_geo<T>;
+    constexpr int BPC = WAVE / T::per_block;
+    e.nch = (int) ceil_div(a.ntasks, WAVE);
+    const int last_tasks = a.ntasks - WAVE * (e.nch - 1);
+    e.last_bytes = (last_tasks / T::per_block) * T::blk_bytes;
+    constexpr bool kq = T::per_block == 4;
+    e.qmode = kq ? 1 : 2;
+    e.n = (int64_t) (a.ntasks / T::per_block) * (kq ? 256 : 32);
+    if (e.n % 256 != 0 || e.n > 16384 || e.last_bytes % 16 != 0) return false;
+    e.rec_off = (uint32_t) (ENG_CTRL + r16(pro_lds_bytes(e.n, e.qmode)));
+    e.ring_off = (uint32_t) ((e.rec_off + (size_t) nc * BPC * T::RS * 4 + 1023) / 1024 * 1024);
+    e.slot = (uint32_t) G::SLICE;
+    e.ns = (int) std::min<int64_t>(ENG_NSMAX, (ENG_LDS - (int64_t) e.ring_off) / e.slot);
+    return e.ns >= 60 / G::NI + 4;
+}
+
+template <class T, int NL, int NC>
+static void launch_eng_v(hipStream_t st, gemv_args & a, const eng_geo & e) {
+    const unsigned grid = (unsigned) g_num_cu;
+    a.kt = g_kt_ctx ? g_kt_ctx->kt_take(a.rres ? "eng+resid" : (e.act_mode == 1 ? "eng+pro" : (e.act_mode == 2 ? "eng+swiglu" : "eng")),
+                                        grid, 64 * (NL + NC)) : nullptr;
+#define ENG_LAUNCH(OC)                                                                                                  \
+    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_eng<T, NL, NC, OC>), dim3(grid), dim3(64 * (NL + NC)), 0, st, t_ev_beg, t_ev_end, 0, a, e); \
+    else hipLaunchKernelGGL((k_gemv_eng<T, NL, NC, OC>), dim3(grid), dim3(64 * (NL + NC)), 0, st, a, e)
+    if (e.nch == 1) { ENG_LAUNCH(true); } else { ENG_LAUNCH(false); }
+#undef ENG_LAUNCH
+}
+
+template <class T>
+static bool launch_eng_t(hipStream_t st, gemv_args & a, int nmat) {
+    if (!eng_enabled() || a.tl.kind || needs_epilogue(a, nmat) || !os_aligned<T>(a, nmat)) return false;
+    const int nc = eng_nc();
+    eng_geo e = {};
+    if (!eng_geometry<T>(a, nc, e)) return false;
+    e.rows = set_groups(a, nmat, 1);
+    e.act_mode = g_sw_gate ? 2 : (a.pro.x ? 1 : 0);
+    e.sw_gate = g_sw_gate;
+    e.sw_up = g_sw_up;
+    if (e.act_mode == 1 && a.pro.qmode != e.qmode) return false;
+    switch (eng_cfg()) {
+        case 17:  launch_eng_v<T, 1, 7>(st, a, e); break;
+        case 26:  launch_eng_v<T, 2, 6>(st, a, e); break;
+        case 412: launch_eng_v<T, 4, 12>(st, a, e); break;
+        default:  launch_eng_v<T, 2, 14>(st, a, e); break;
+    }
+    return true;
+}
+
+// the engine takes this mat-vec (one activation column, no register epilogues) — the
+// dispatcher's test before it plans a prologue (norm / SwiGLU) that only the engine forms
+bool gemv_engine_ok(const ggml_tensor * mm) {
+    if (!eng_enabled() || !gemv_supported(mm)) return false;
+    const ggml_tensor * w = mm->src[0];
+    gemv_args a = {};
+    a.W[0] = (const uint8_t *) w->data;
+    a.nb01[0] = w->nb[1];
+    a.M[0] = w->ne[1];
+    const int64_t nblk = w->ne[0] / ggml_blck_size(w->type);
+    eng_geo e = {};
+    switch (w->type) {
+        case GGML_TYPE_Q4_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q4_K>(a, 1) && eng_geometry<g_q4_K>(a, eng_nc(), e);
+        case GGML_TYPE_Q5_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q5_K>(a, 1) && eng_geometry<g_q5_K>(a, eng_nc(), e);
+        case GGML_TYPE_Q6_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q6_K>(a, 1) && eng_geometry<g_q6_K>(a, eng_nc(), e);
+        case GGML_TYPE_Q8_0: a.ntasks = (int) nblk;       return os_aligned<g_q8_0>(a, 1) && eng_geometry<g_q8_0>(a, eng_nc(), e);
+        case GGML_TYPE_Q4_0: a.ntasks = (int) nblk;       return os_aligned<g_q4_0>(a, 1) && eng_geometry<g_q4_0>(a, eng_nc(), e);
+        default: return false;
+    }
+}
+
 template <class T>
 static void launch_t(hipStream_t st, gemv_args & a, int nmat) {
+    if (launch_eng_t<T>(st, a, nmat)) return;
+    GGML_ASSERT(!g_sw_gate && "mi355x: SwiGLU prologue without the engine");
     if (launch_os_t<T>(st, a, nmat)) return;
     int64_t Mt = 0;
     for (int i = 0; i < nmat; ++i) Mt += a.M[i];
@@ -934,7 +1354,7 @@ bool gemv_epilogue_ok(const ggml_tensor * mm) { return gemv_supported(mm); }
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi) {
     GGML_ASSERT(nmat >= 1 && nmat <= GEMV_MAXMAT);
     gemv_init();
-    g_kt_ctx = ctx.kt_buf ? &ctx : nullptr;
+    g_kt_ctx = ctx.kt_buf && ktrace_enabled() ? &ctx : nullptr;
     const ggml_tensor * src1 = mms[0]->src[1];
     const ggml_type wt = mms[0]->src[0]->type;
     const bool kq = is_kq(wt);

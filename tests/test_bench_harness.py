@@ -33,7 +33,7 @@ def tiny_dir(tmp_path_factory):
 def _run(tiny_dir, gpus, nproc=2):
     bench = [os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--cpu", "--config", "tiny-q4km",
              "--steps", "4", "--warmup", "1", "--pp", "0", "--roofline-steps", "0", "--no-cpu-baseline",
-             "--model-dir", tiny_dir, "--split-config", "tiny-q4km", "--split-steps", "3", "--split-warmup", "1"]
+             "--model-dir", tiny_dir, "--split-config", "tiny-q4km", "--split-steps", "3", "--split-warmup", "1", "--split-pp", "32"]
     if nproc > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + bench
@@ -57,6 +57,8 @@ def test_replicas_two_ranks_with_split_series(tiny_dir):
     sp = d["split_series"]
     assert sp and "error" not in sp, sp
     assert sp["model"] == "tiny-q4km" and sp["steps"] == 3 and sp["tg_tok_s"] > 0
+    # pp at N and the roofline fraction ride on the series (BASELINE.json metric: pp and tg at N)
+    assert sp["pp_tokens"] == 32 and sp["pp_tok_s"] > 0 and sp["tg_frac_of_8TBs"] > 0
 
 
 def test_single_process_with_split_series(tiny_dir):

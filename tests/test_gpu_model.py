@@ -144,7 +144,7 @@ def _vdev_greedy(tmp_path, cfg, n_prompt, n_gen, split_mode=1, p2p=None):
     return info
 
 
-@pytest.mark.parametrize("cfg", ["tiny-q4km", "llama3-8b-2l-q4km"])
+@pytest.mark.parametrize("cfg", ["tiny-q4km", "llama3-8b-2l-q4km", "llama3-70b-2l-q4km"])
 def test_greedy_layer_split_virtual_devices_bit_identical(cfg, tmp_path):
     """libllama's -sm layer pipeline (BASELINE.json configs[3]'s partition) over two ggml devices
     on this one GPU: contiguous layer ranges per device, the scheduler's n_copies = 4 pipeline
@@ -157,11 +157,13 @@ def test_greedy_layer_split_virtual_devices_bit_identical(cfg, tmp_path):
     assert any("pipeline parallelism enabled" in l for l in info["pipeline"]), info
 
 
-def test_greedy_layer_split_virtual_devices_rccl(tmp_path):
+@pytest.mark.parametrize("cfg", ["tiny-q4km", "llama3-70b-2l-q4km"])
+def test_greedy_layer_split_virtual_devices_rccl(cfg, tmp_path):
     """The same split with GGML_MI355X_P2P=rccl: every same-GPU stage hand-off goes through RCCL
     (a one-rank communicator, ncclSend + ncclRecv to self in one group on the source stream), so
-    the RCCL transport runs on a one-GPU box; bit-identical logits."""
-    info = _vdev_greedy(tmp_path, "tiny-q4km", 16, 16, p2p="rccl")
+    the RCCL transport runs on a one-GPU box; bit-identical logits.  The 70B shapes (8192-wide
+    residual hand-offs, BASELINE.json configs[3]) go through the same transport."""
+    info = _vdev_greedy(tmp_path, cfg, 16, 16, p2p="rccl")
     rccl, peer, d2d = info["handoffs"]
     assert rccl > 0 and d2d == 0, info
 
