@@ -1076,6 +1076,7 @@ static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.done.clear();
     ex.silu_defer = ex.silu_mul = nullptr;
     ex.pro = {};
+    ex.swiglu = {};
     ex.nsite = 0;
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) i += op_compute(ex, cgraph, i);
@@ -1086,6 +1087,7 @@ static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     // the residual sums of this graph, read by now: zero for the next graph
     if (ex.nsite) MI_CHECK(hipMemsetAsync(ex.rsum_buf, 0, (size_t) ex.nsite * exec_ctx::SITE_DOUBLES * sizeof(double), ex.stream));
     ex.pro = {};
+    ex.swiglu = {};
 }
 
 // returns true when the graph was launched as (or captured into) a hipGraph

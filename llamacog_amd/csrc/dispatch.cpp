@@ -468,7 +468,10 @@ static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tenso
     // timeline: gate/up 27.0 us with the prologue vs 15 + 4 without); Q/K/V keep it.  A persistent
     // LDS-ring kernel that forms it once per resident workgroup measured slower still (round 3:
     // gate/up + prologue 22.0 us, tg 393-415 vs 420-430 tok/s over five ring geometries)
-    if (rows > 16384) return;
+    // ... unless every reader runs on the persistent engine, which forms it once per CU
+    bool all_engine = !readers.empty();
+    for (const ggml_tensor * c : readers) all_engine = all_engine && gemv_engine_ok(c);
+    if (rows > 16384 && !all_engine) return;
     if (!dead_after(g, n, pl + 1, last, readers)) return;
     if (mul && !dead_after(g, n, pn + 1, nm, {mul})) return;
     double * site = gemv_rsum_site(ctx);
@@ -555,6 +558,12 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     if (ctx.pro.last && ctx.pro.last == mm0->src[1] && ctx.pro.data == mm0->src[1]->data) {
         epi.px = ctx.pro.x; epi.pw = ctx.pro.w; epi.psum = ctx.pro.sum; epi.peps = ctx.pro.eps; epi.pn = ctx.pro.n;
     }
+    // the SwiGLU product this launch forms in its prologue (planned at the SILU node)
+    if (ctx.swiglu.key && ctx.swiglu.key == mm0->src[1] && ctx.swiglu.data == mm0->src[1]->data) {
+        epi.sw_gate = ctx.swiglu.gate;
+        epi.sw_up = ctx.swiglu.up;
+        ctx.swiglu = {};
+    }
     std::vector<const ggml_tensor *> absorbed;   // nodes this launch computes (besides node i)
     std::vector<const ggml_tensor *> outs = {mm0};
 
@@ -608,7 +617,7 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     add_epilogues(0, i);
     settle(0, i);
 
-    for (int j = i + 1; j < n && j <= i + 12 && nm < 3; ++j) {
+    for (int j = i + 1; j < n && j <= i + 12 && nm < 3 && !epi.sw_gate; ++j) {
         ggml_tensor * c = ggml_graph_node(g, j);
         if (c->op != GGML_OP_MUL_MAT || c->src[1] != mm0->src[1] || !gemv_supported(c)) continue;
         if (std::find(ctx.done.begin(), ctx.done.end(), c) != ctx.done.end()) continue;
@@ -961,6 +970,15 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                         ggml_tensor * mm = at(cgraph, j + 1, n);
                         const bool ssilu = !dead_after(cgraph, n, i + 1, node, {c});
                         const bool smul = !(mm && mm->op == GGML_OP_MUL_MAT && dead_after(cgraph, n, j + 1, c, {mm}));
+                        // the down projection right behind, on the engine, and nothing else reading the
+                        // SILU or the product: the engine forms silu(gate) * up in its prologue
+                        const ggml_tensor * gate = node->src[0], * up = c->src[1];
+                        if (j == i + 1 && !ssilu && !smul && mm->src[1] == c && f32c(gate) && f32c(up) && f32c(c) &&
+                            ggml_are_same_shape(gate, up) && ggml_are_same_shape(c, gate) && ggml_nrows(c) == 1 &&
+                            c->ne[0] % 256 == 0 && c->ne[0] <= 16384 && gemv_engine_ok(mm)) {
+                            ctx.swiglu = {c, c->data, (const float *) gate->data, (const float *) up->data};
+                            return 2;
+                        }
                         if (fused_silu_mul_quant(ctx, node, c, mm, ssilu, smul)) {
                             if (j == i + 1) return 2;
                             ctx.done.push_back(c);

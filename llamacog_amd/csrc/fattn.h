@@ -43,5 +43,11 @@ int fattn_dec2_threads(const fa_args & a);   // the launch's workgroup size (tim
 bool fattn_dec2_ok(const fa_args & a, int64_t nq3);
 void launch_fattn_dec2(hipStream_t stream, const fa_args & a, int64_t nq3);
 void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int64_t n, float * s);
+// long-context decode (D = 128): the scores of every position by a (position block x KV head)
+// grid into sco [H][n_kv], then one chain workgroup per head (coefficients of all positions in
+// LDS, V streamed by stager waves); from FA_LONG_MIN cached positions (GGML_MI355X_FA_LONG)
+constexpr int FA_LONG_MIN = 1024;
+bool fattn_long_ok(const fa_args & a, int64_t nq3);
+void launch_fattn_long(hipStream_t stream, const fa_args & a, float * sco, unsigned long long * kt_scores);
 
 }  // namespace mi355x

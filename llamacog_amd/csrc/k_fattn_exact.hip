@@ -1330,6 +1330,466 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     }
 }
 
+// ---- long-context decode: the scores in one launch, the exact recurrence in another --------------
+// At thousands of cached positions the per-head workgroups above are bound by one CU's intake: a
+// head's K and V (1-2 MB at 4096 positions) pass through the one CU that also runs the serial
+// chain.  Here the scores — independent per position — are computed first by a grid over
+// (256-position block, KV head), every K row read once for the G query heads that share it
+// (k_fal_scores); then one workgroup per query head (k_fal_chain) forms the prefix max and the
+// (ms, vs) coefficients of ALL positions in LDS (a scan, then expf per position: parallel), and
+// its chain waves run the recurrence while its stager waves stream the next V chunk into LDS.
+// The arithmetic of every step is k_fattn_exact's (the CPU's ops.cpp:7015-7232), so the bits are.
+constexpr int FAL_PB = 256;       // positions per scores workgroup
+constexpr int FAL_NMAX = 8192;    // positions the chain's coefficient arrays hold
+constexpr int FAL_GMAX = 8;       // query heads per KV head (GQA) the scores kernel takes
+constexpr int FAL_U = 8;          // chain batch
+
+template <int KT>   // K type: 0 f16, 1 q8_0, 2 q4_0
+__global__ __launch_bounds__(256) void k_fal_scores(const fa_args a, float * __restrict__ sco) {
+    constexpr int D = 128, NM = D / 16, NB = D / 32, NP = FAL_PB / 64;
+    constexpr int KB = KT == 2 ? 18 : 34;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qd = tid & 3;
+    kt_enter(a.kt);
+    const int64_t j0 = (int64_t) blockIdx.x * FAL_PB;
+    const int64_t hk = blockIdx.y % a.Hkv, iq3 = blockIdx.y / a.Hkv;
+    const int G = (int) (a.H / a.Hkv);
+    const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
+    const char * mrow = a.mask;   // decode: mask row 0
+    // Q of the group as q8_0 (quantized K: Q is converted to K's vec_dot_type, ops.cpp:7147)
+    __shared__ __attribute__((aligned(16))) int8_t qq[KT ? FAL_GMAX * D : 1];
+    __shared__ float qqd[KT ? FAL_GMAX * NB : 1];
+    __shared__ int16_t qqs[KT ? FAL_GMAX * NB : 1];
+    if constexpr (KT != 0) {
+        for (int g = wave; g < G; g += 4) {
+            const float * qrow = (const float *) (a.q + (hk * G + g) * a.nbq2 + iq3 * a.nbq3);
+            const bool valid = 4 * lane < D;
+            float qv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (valid) { const float4 t = *(const float4 *) (qrow + 4 * lane); qv[0] = t.x; qv[1] = t.y; qv[2] = t.z; qv[3] = t.w; }
+            q8_0_wave(qv, lane, valid, qq + g * D, qqd + g * NB, qqs + g * NB);
+        }
+        __syncthreads();
+    }
+    // this block's K rows, 4 lanes per position (the layout of k_fattn_exact's phase 1)
+    uint2 kh[KT ? 1 : NP][KT ? 1 : NM];
+    uint2 kb[KT ? NP : 1][KT ? NB : 1];
+    uint32_t kd[KT ? NP : 1][KT ? NB : 1];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int64_t j = min(j0 + 64 * p + (tid >> 2), a.n_kv - 1);
+        if constexpr (KT == 0) {
+            const char * krow = kbase + j * a.nbk1 + 8 * qd;
+#pragma unroll
+            for (int m = 0; m < NM; ++m) kh[p][m] = ld8(krow + 32 * m);
+        } else {
+            const uint8_t * krow = (const uint8_t *) kbase + j * a.nbk1;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                if constexpr (KT == 2) {
+                    const uint2 q = ld8(krow + KB * b + 2 + 8 * (qd & 1));
+                    const int sh = 4 * (qd >> 1);
+                    kb[p][b] = make_uint2((((q.x >> sh) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u,
+                                          (((q.y >> sh) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u);
+                } else {
+                    kb[p][b] = ld8(krow + KB * b + 2 + 8 * qd);
+                }
+                kd[p][b] = ld2(krow + KB * b);
+            }
+        }
+    }
+    float mv[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int64_t j = j0 + 64 * p + (tid >> 2);
+        mv[p] = j < a.n_kv && mrow ? h2f(*(const uint16_t *) (mrow + 2 * j)) : 0.0f;
+    }
+    for (int g = 0; g < G; ++g) {
+        const int64_t h = hk * G + g;
+        const float slope = a.max_bias > 0.0f
+            ? (float) ((uint32_t) h < a.n_head_log2 ? pow((double) a.m0, (double) (h + 1))
+                                                   : pow((double) a.m1, (double) (2 * ((uint32_t) h - a.n_head_log2) + 1)))
+            : 1.0f;
+        float * out = sco + (iq3 * a.H + h) * a.n_kv;
+        float w[NP];
+        if constexpr (KT == 0) {
+            float qf[NM][4];
+            const float * qrow = (const float *) (a.q + h * a.nbq2 + iq3 * a.nbq3);
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                const float4 q4 = *(const float4 *) (qrow + 16 * m + 4 * qd);
+                qf[m][0] = f16r(q4.x); qf[m][1] = f16r(q4.y); qf[m][2] = f16r(q4.z); qf[m][3] = f16r(q4.w);
+            }
+#pragma unroll
+            for (int p = 0; p < NP; ++p) w[p] = dot_f16_avx512_q4<D>(kh[p], qf);
+        } else {
+            uint2 qb[NB];
+            float qdb[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                qb[b] = *(const uint2 *) (qq + g * D + 32 * b + 8 * qd);
+                qdb[b] = qqd[g * NB + b];
+            }
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                float ae = 0.0f, ao = 0.0f;
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    const float dd = __fmul_rn(h2f((uint16_t) kd[p][b]), qdb[b]);
+                    ae = fmaf(dd, (float) dot4((int) kb[p][b].x, (int) qb[b].x, 0), ae);
+                    ao = fmaf(dd, (float) dot4((int) kb[p][b].y, (int) qb[b].y, 0), ao);
+                }
+                ae = __fadd_rn(ae, quad_from_plus2(ae));
+                ao = __fadd_rn(ao, quad_from_plus2(ao));
+                ae = __fadd_rn(ae, quad_from_plus1(ae));
+                ao = __fadd_rn(ao, quad_from_plus1(ao));
+                w[p] = __fadd_rn(ae, ao);
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            const int64_t j = j0 + 64 * p + (tid >> 2);
+            if (qd == 0 && j < a.n_kv) {
+                float sv = __fmul_rn(w[p], a.scale);
+                if (a.softcap != 0.0f) sv = __fmul_rn(a.softcap, tanhf(sv));
+                out[j] = __fadd_rn(sv, __fmul_rn(slope, mv[p]));
+            }
+        }
+    }
+    kt_exit(a.kt);
+}
+
+// LDS of the chain kernel
+template <int VT> struct fal_smem {
+    static constexpr int D = 128, NB = D / 32;
+    static constexpr int CV = VT ? 256 : 128;   // V positions per stage (32 KiB of f16 / int8 values)
+    float cm[FAL_NMAX + 2 * FAL_U];             // ms coefficient (1 where dead)
+    float sc[FAL_NMAX + 2 * FAL_U];             // vs coefficient (0 where dead)
+    uint32_t dead[FAL_NMAX / 32 + 2];           // bit per position: masked (the state is kept)
+    uint8_t gb[FAL_NMAX / 64 + 4];              // per 64 positions: its 8 batches taking the general step
+    float wmax[4];
+    int wlast[4];
+    float ol[128];
+    __attribute__((aligned(16))) uint16_t vl[2][VT ? 1 : CV * D];
+    __attribute__((aligned(16))) int8_t vq[2][VT ? CV * D : 1];
+    float vd[2][VT ? CV * NB : 1];
+};
+
+template <int VT>   // V type: 0 f16, 1 q8_0, 2 q4_0
+__global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const float * __restrict__ sco) {
+    using SM = fal_smem<VT>;
+    constexpr int D = 128, NB = D / 32, CV = SM::CV, U = FAL_U;
+    constexpr int KB = VT == 2 ? 18 : 34;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    kt_enter(a.kt);
+    const int64_t h = blockIdx.x, iq3 = blockIdx.y;
+    const int64_t hk = h / (a.H / a.Hkv);
+    __shared__ __attribute__((aligned(16))) SM sm;
+    const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
+    const char * mrow = a.mask;
+    const float * srow = sco + (iq3 * a.H + h) * a.n_kv;
+
+    // ---- stage V rows [c0, c0 + n) into buffer st: waves 2-3 ----
+    auto stage = [&](int st, int64_t c0, int n) {
+        const int t = tid - 128;
+        if constexpr (VT == 0) {
+            // 4 rows of 256 B per 1 KiB LDS-DMA instruction
+            const int r_in = (t & 63) >> 4, col = t & 15;
+            for (int p = t >> 6; 4 * p < n; p += 2) {
+                const int row = min(4 * p + r_in, n - 1);
+                lds_dma16(vbase + (c0 + row) * a.nbv1 + 16 * col, sm.vl[st] + p * 512);
+            }
+        } else {
+            for (int i = t; i < n * NB; i += 128) {
+                const int row = i / NB, b = i % NB;
+                const uint8_t * src = (const uint8_t *) vbase + (c0 + row) * a.nbv1 + KB * b;
+                int8_t * vq = sm.vq[st];
+                if constexpr (VT == 2) {
+                    const uint4 q = ld16(src + 2);
+                    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+                    uint32_t lo[4], hi[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        lo[k] = ((w[k] & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
+                        hi[k] = (((w[k] >> 4) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
+                    }
+                    *(uint4 *) (vq + row * D + 32 * b) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+                    *(uint4 *) (vq + row * D + 32 * b + 16) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+                } else {
+                    *(uint4 *) (vq + row * D + 32 * b) = ld16(src + 2);
+                    *(uint4 *) (vq + row * D + 32 * b + 16) = ld16(src + 18);
+                }
+                sm.vd[st][row * NB + b] = h2f(ld2(src));
+            }
+        }
+    };
+    // chunk 0's V goes out first (bounded by the cache; the mask bounds it later)
+    const int64_t n_kv = a.n_kv;
+    if (wave >= 2) stage(0, 0, (int) min<int64_t>(CV, n_kv));
+
+    // ---- coefficients of every position (all waves) ----
+    float carry = -INFINITY;
+    int nrun = 0;
+    for (int64_t t0 = 0; t0 < n_kv; t0 += 256) {
+        const int64_t j = t0 + tid;
+        const float m = j < n_kv ? (mrow ? h2f(*(const uint16_t *) (mrow + 2 * j)) : 0.0f) : -INFINITY;
+        const bool live = m != -INFINITY;
+        const float sj = live ? srow[j] : -INFINITY;
+        float smx = sj;   // inclusive max-scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const float tt = __shfl_up(smx, o, WAVE);
+            if (lane >= o) smx = fmaxf(smx, tt);
+        }
+        const unsigned long long lb = __ballot(live);
+        if (lane == 63) sm.wmax[wave] = smx;
+        if (lane == 0) sm.wlast[wave] = lb ? (int) (t0 + 64 * wave + 63 - __clzll(lb)) : -1;
+        __syncthreads();
+        float M = carry;
+        for (int w2 = 0; w2 < wave; ++w2) M = fmaxf(M, sm.wmax[w2]);
+        const float ex = __shfl_up(smx, 1, WAVE);
+        if (lane > 0) M = fmaxf(M, ex);
+        float cmv = 1.0f, scv = 0.0f;
+        const bool upd = live && sj > M;
+        if (live) {
+            if (upd) { cmv = M == -INFINITY ? 0.0f : expf_cr(M - sj); scv = 1.0f; }
+            else scv = expf_cr(sj - M);
+        }
+        if (j < FAL_NMAX) { sm.cm[j] = cmv; sm.sc[j] = scv; }
+        const unsigned long long gw = __ballot(!live || upd);
+        const unsigned long long dw = __ballot(!live);
+        if (lane == 0) {
+            sm.dead[(t0 + 64 * wave) / 32] = (uint32_t) dw;
+            sm.dead[(t0 + 64 * wave) / 32 + 1] = (uint32_t) (dw >> 32);
+            uint32_t f = 0;
+#pragma unroll
+            for (int b = 0; b < 64 / U; ++b) f |= ((gw >> (U * b)) & ((1ull << U) - 1)) ? 1u << b : 0u;
+            sm.gb[(t0 + 64 * wave) / 64] = (uint8_t) f;
+        }
+        const int lastw = max(max(sm.wlast[0], sm.wlast[1]), max(sm.wlast[2], sm.wlast[3]));
+        nrun = max(nrun, lastw + 1);
+        carry = fmaxf(fmaxf(carry, fmaxf(sm.wmax[0], sm.wmax[1])), fmaxf(sm.wmax[2], sm.wmax[3]));
+        __syncthreads();
+    }
+    // the batch past the last live position reads dead padding
+    __syncthreads();
+    if (tid < 2 * U) {
+        const int j = nrun + tid;
+        sm.cm[j] = 1.0f; sm.sc[j] = 0.0f;
+    }
+    if (tid == 0) {
+        // positions past the last live one are dead (the last batch reads up to U - 1 of them)
+        for (int j = nrun; j < ((nrun + U - 1) / U) * U + U; ++j) sm.dead[j / 32] |= 1u << (j % 32);
+        sm.gb[nrun / 64] |= (uint8_t) (1u << ((nrun % 64) / U));   // the partial batch (if any)
+    }
+    __syncthreads();
+
+    // ---- the recurrence: waves 0-1 one output dim per lane; waves 2-3 stage the next V chunk ----
+    const int d = tid;
+    uint32_t yb = 0;     // f16 bits (f16 V)
+    float yf = 0.0f;     // f32 accumulator (quantized V)
+    float S = 0.0f;
+    const int nchunk = (nrun + CV - 1) / CV;
+    for (int c = 0; c < nchunk; ++c) {
+        const int st = c & 1;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // stage st is in; every chain lane is done with stage st ^ 1
+        if (wave >= 2) {
+            if (c + 1 < nchunk) stage(st ^ 1, (int64_t) (c + 1) * CV, min(CV, nrun - (c + 1) * CV));
+            continue;
+        }
+        const int jc = c * CV;                  // first position of the chunk
+        const int nr = min(CV, nrun - jc);      // positions to run
+        const int nb = (nr + U - 1) / U;
+        // batch flags of the chunk: CV / U batches from the per-64 bytes
+        uint32_t flags = 0;
+#pragma unroll
+        for (int k = 0; k < CV / 64; ++k) flags |= (uint32_t) sm.gb[jc / 64 + k] << (8 * k);
+        flags = __builtin_amdgcn_readfirstlane(flags);
+        const float * scp = sm.sc + jc;
+        const float * cmp = sm.cm + jc;
+        // the U dead bits of the batch at chunk position j (j a multiple of U)
+        auto deadb = [&](int j) { return (sm.dead[(jc + j) / 32] >> ((jc + j) % 32)) & ((1u << U) - 1); };
+        auto ld4 = [&](const float * p, float (&o)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; u += 4) {
+                const float4 t = *(const float4 *) (p + u);
+                o[u] = t.x; o[u + 1] = t.y; o[u + 2] = t.z; o[u + 3] = t.w;
+            }
+        };
+        if constexpr (VT == 0) {
+            const uint16_t * vrow = sm.vl[st] + d;
+            auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) vv[u] = vrow[(j + u) * D];
+                ld4(scp + j, vs);
+            };
+            auto run = [&](const uint32_t (&vv)[U], const float (&vs)[U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    yb = f16_mad(vv[u], vs[u], yb);
+                    S = __fadd_rn(S, vs[u]);   // not contracted on the CPU
+                }
+            };
+            auto fast_run = [&](int j0, int nf) {
+                uint32_t va[U], vb[U];
+                float sa[U], sb[U];
+                ldb(j0, va, sa);
+                for (int k = 0; k < nf; k += 2) {
+                    ldb(j0 + (k + 1) * U, vb, sb);
+                    run(va, sa);
+                    if (k + 1 >= nf) break;
+                    ldb(j0 + (k + 2) * U, va, sa);
+                    run(vb, sb);
+                }
+            };
+            auto general = [&](int j) {
+                uint32_t vv[U];
+                float vs[U], ms[U];
+                ldb(j, vv, vs);
+                ld4(cmp + j, ms);
+                const uint32_t db = deadb(j);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const bool live = ((db >> u) & 1u) == 0;
+                    const bool upd = __float_as_uint(ms[u]) != 0x3f800000u;
+                    float t = __fmul_rn(h2f((uint16_t) yb), ms[u]);
+                    asm("" : "+v"(t));   // two roundings, as f16r
+                    const uint32_t ys = upd ? (uint32_t) f2h(t) : yb;
+                    const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
+                    const uint32_t yn = f16_mad(vv[u], vs[u], ys);
+                    const float Sn = __fadd_rn(Ss, vs[u]);
+                    yb = live ? yn : yb;
+                    S = live ? Sn : S;
+                }
+            };
+            int b = 0;
+            while (b < nb) {
+                const uint32_t rest = flags >> b;
+                const int nf = min(rest ? __builtin_ctz(rest) : 32, nb - b);
+                if (nf > 0) { fast_run(b * U, nf); b += nf; }
+                if (b < nb) { general(b * U); ++b; }
+            }
+        } else {
+            // f32 recurrence on dequantized V: v = (float) q * d (dequantize_row_q8_0 / _q4_0)
+            const int8_t * vq = sm.vq[st] + d;
+            const float * vdp = sm.vd[st] + d / 32;
+            auto ldb = [&](int j, float (&vv)[U], float (&vs)[U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) vv[u] = __fmul_rn((float) vq[(j + u) * D], vdp[(j + u) * NB]);
+                ld4(scp + j, vs);
+            };
+            auto run = [&](const float (&vv)[U], const float (&vs)[U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    yf = fmaf(vv[u], vs[u], yf);   // ggml_vec_mad_f32
+                    S = __fadd_rn(S, vs[u]);
+                }
+            };
+            auto fast_run = [&](int j0, int nf) {
+                float va[U], vb[U], sa[U], sb[U];
+                ldb(j0, va, sa);
+                for (int k = 0; k < nf; k += 2) {
+                    ldb(j0 + (k + 1) * U, vb, sb);
+                    run(va, sa);
+                    if (k + 1 >= nf) break;
+                    ldb(j0 + (k + 2) * U, va, sa);
+                    run(vb, sb);
+                }
+            };
+            auto general = [&](int j) {
+                float vv[U], vs[U], ms[U];
+                ldb(j, vv, vs);
+                ld4(cmp + j, ms);
+                const uint32_t db = deadb(j);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const bool live = ((db >> u) & 1u) == 0;
+                    const bool upd = __float_as_uint(ms[u]) != 0x3f800000u;
+                    const float ys = upd ? __fmul_rn(yf, ms[u]) : yf;   // ggml_vec_scale_f32
+                    const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
+                    yf = live ? fmaf(vv[u], vs[u], ys) : yf;
+                    S = live ? __fadd_rn(Ss, vs[u]) : S;
+                }
+            };
+            int b = 0;
+            while (b < nb) {
+                const uint32_t rest = flags >> b;
+                const int nf = min(rest ? __builtin_ctz(rest) : 32, nb - b);
+                if (nf > 0) { fast_run(b * U, nf); b += nf; }
+                if (b < nb) { general(b * U); ++b; }
+            }
+        }
+    }
+
+    // ---- output and its optional quantization (k_fattn_exact's epilogue) ----
+    float * drow = (float *) ((char *) a.dst + h * a.nb1_dst + iq3 * a.nb2_dst);
+    const float o = d < D ? __fmul_rn(VT ? yf : h2f((uint16_t) yb), 1.0f / S) : 0.0f;
+    if (d < D) {
+        if (a.qmode == 1) __hip_atomic_store(drow + d, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else drow[d] = o;
+    }
+    if (a.qmode == 2) {
+        __syncthreads();
+        if (d < D) sm.ol[d] = o;
+        __syncthreads();
+        if (wave == 0) {
+            const bool valid = 4 * lane < D;
+            float q[4] = {0.f, 0.f, 0.f, 0.f};
+            if (valid) { const float4 v4 = *(const float4 *) (sm.ol + 4 * lane); q[0] = v4.x; q[1] = v4.y; q[2] = v4.z; q[3] = v4.w; }
+            const int64_t c0 = h * D;
+            q8_0_wave(q, lane, valid, a.qs + c0, a.qd + c0 / 32, a.qsum + c0 / 32);
+        }
+    } else if (a.qmode == 1) {
+        // Q8_K: a block of 256 = two heads; the second of their workgroups to finish quantizes it
+        // (write-through outputs drained before the counter add, read back with sc1 loads)
+        const int64_t blk = (h * D) / 256;
+        __shared__ int is_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const int prev = __hip_atomic_fetch_add(a.cnt + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            is_last = prev == 1;
+            if (is_last) __hip_atomic_store(a.cnt + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (is_last && wave == 0) {
+            const float * brow = (const float *) a.dst + 256 * blk;
+            float q[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) q[c] = __hip_atomic_load(brow + 4 * lane + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int64_t c0 = 256 * blk;
+            q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
+        }
+    }
+    kt_exit(a.kt);
+}
+
+// the long-context pair applies: one query row, D = 128, a cache longer than FA_LONG_MIN (and
+// within the chain's coefficient arrays), a GQA group the scores kernel takes, one batch
+bool fattn_long_ok(const fa_args & a, int64_t nq3) {
+    static const int lmin = getenv("GGML_MI355X_FA_LONG") ? atoi(getenv("GGML_MI355X_FA_LONG")) : FA_LONG_MIN;
+    return lmin > 0 && a.n_q == 1 && a.D == 128 && nq3 == 1 && a.n_kv >= lmin && a.n_kv <= FAL_NMAX &&
+           a.H % a.Hkv == 0 && a.H / a.Hkv <= FAL_GMAX && (a.qmode != 1 || a.H % 2 == 0) &&
+           (a.k_type == GGML_TYPE_F16 || a.k_type == GGML_TYPE_Q8_0 || a.k_type == GGML_TYPE_Q4_0);
+}
+
+void launch_fattn_long(hipStream_t st, const fa_args & a0, float * sco, unsigned long long * kt_scores) {
+    fa_args a = a0;
+    a.kt = kt_scores;
+    const dim3 gs((unsigned) ceil_div(a.n_kv, (int64_t) FAL_PB), (unsigned) a.Hkv);
+    switch (a.k_type) {
+        case GGML_TYPE_F16:  hipLaunchKernelGGL(k_fal_scores<0>, gs, dim3(256), 0, st, a, sco); break;
+        case GGML_TYPE_Q8_0: hipLaunchKernelGGL(k_fal_scores<1>, gs, dim3(256), 0, st, a, sco); break;
+        default:             hipLaunchKernelGGL(k_fal_scores<2>, gs, dim3(256), 0, st, a, sco); break;
+    }
+    a.kt = a0.kt;
+    const dim3 gc((unsigned) a.H, 1);
+    switch (a.v_type) {
+        case GGML_TYPE_F16:  hipLaunchKernelGGL(k_fal_chain<0>, gc, dim3(256), 0, st, a, (const float *) sco); break;
+        case GGML_TYPE_Q8_0: hipLaunchKernelGGL(k_fal_chain<1>, gc, dim3(256), 0, st, a, (const float *) sco); break;
+        default:             hipLaunchKernelGGL(k_fal_chain<2>, gc, dim3(256), 0, st, a, (const float *) sco); break;
+    }
+}
+
 // test hook: the K·Q scores exactly as phase 1 of k_fattn_exact computes them
 // (q [D] f32 is f16-rounded first), 4 lanes per cache row; D = 128
 __global__ void k_fattn_scores_d128(const float * q, const uint16_t * k, int64_t n, float * s) {

@@ -640,9 +640,22 @@ struct eng_geo {
     int act_mode;        // 0: copy p.A; 1: RMS-norm prologue (p.pro); 2: SwiGLU prologue
     int qmode;           // activation quantization: 1 Q8_K, 2 Q8_0
     int64_t n;           // activation length (K)
-    uint32_t rec_off, ring_off, slot;
+    uint32_t rec_off, ring_off, slot, trash_off;
+    int ll;              // chunks in flight per loader wave (ll * P <= 63: vmcnt's range)
     const float * sw_gate; const float * sw_up;   // act_mode 2
 };
+
+// s_waitcnt vmcnt(ll * P) for a runtime ll (an immediate operand: one case per depth)
+template <int P>
+__device__ __forceinline__ void eng_vmwait(int ll) {
+#define EW(n) case n: if constexpr (n * P <= 63) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n * P) : "memory"); } break;
+    switch (ll) {
+        EW(1) EW(2) EW(3) EW(4) EW(5) EW(6) EW(7) EW(8) EW(9) EW(10) EW(11)
+        EW(12) EW(13) EW(14) EW(15) EW(16) EW(17) EW(18) EW(19) EW(20) EW(21)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef EW
+}
 
 // LDS layout of the control words
 struct eng_ctrl {
@@ -668,6 +681,66 @@ __device__ __forceinline__ void eng_dma16(const void * src, const void * lds) {
 #endif
 }
 
+// the same as a buffer load: the chunk's address in the resource's base, the lane's 16-B offset
+// in a VGPR that never changes, the piece's 1 KiB step in the immediate — two instructions a piece
+typedef int eng_rsrc __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ eng_rsrc eng_rsrc_of(const void * base) {
+    const uint64_t a = (uint64_t) (uintptr_t) base;
+    eng_rsrc r;
+    r.x = __builtin_amdgcn_readfirstlane((int) (uint32_t) a);
+    r.y = __builtin_amdgcn_readfirstlane((int) ((uint32_t) (a >> 32) & 0xffffu));   // stride 0
+    r.z = -1;                                                                          // no range check
+    r.w = 0x00020000;                                                                  // raw dword access (gfx9)
+    return r;
+}
+template <int IMM>
+__device__ __forceinline__ void eng_bdma(eng_rsrc r, uint32_t voff, const void * lds) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (gemv_lds_t) lds);
+#if MI_WNT
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen offset:%3 nt lds" ::"v"(voff), "s"(r), "s"(m), "n"(IMM)
+                 : "memory", "m0");
+#else
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen offset:%3 lds" ::"v"(voff), "s"(r), "s"(m), "n"(IMM)
+                 : "memory", "m0");
+#endif
+}
+template <int P, int SEG>
+__device__ __forceinline__ void eng_issue(eng_rsrc r, uint8_t * dst, int cb, int lane, uint8_t * trash) {
+    const uint32_t vo = 16u * (uint32_t) lane;
+    if (cb == SEG) {   // a full chunk: the piece count and the last piece's lanes are compile-time
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            constexpr int dummy = 0;
+            (void) dummy;
+            const int rem = SEG - 1024 * q;
+            if (rem >= 1024) {
+                if (q == 0) eng_bdma<0>(r, vo, dst);
+                else if (q == 1) eng_bdma<1024>(r, vo, dst + 1024);
+                else if (q == 2) eng_bdma<2048>(r, vo, dst + 2048);
+                else eng_bdma<3072>(r, vo, dst + 3072);
+            } else if (16 * lane < rem) {
+                if (q == 1) eng_bdma<1024>(r, vo, dst + 1024);
+                else if (q == 2) eng_bdma<2048>(r, vo, dst + 2048);
+                else if (q == 3) eng_bdma<3072>(r, vo, dst + 3072);
+                else eng_bdma<0>(r, vo, dst);
+            }
+        }
+    } else {           // a row's short last chunk: pieces wholly past it land in the trash line
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const int rem = cb - 1024 * q;
+            if (rem <= 0) {
+                eng_bdma<0>(r, (uint32_t) (cb - 16), trash);
+            } else if (16 * lane < rem) {
+                if (q == 0) eng_bdma<0>(r, vo, dst);
+                else if (q == 1) eng_bdma<1024>(r, vo, dst + 1024);
+                else if (q == 2) eng_bdma<2048>(r, vo, dst + 2048);
+                else eng_bdma<3072>(r, vo, dst + 3072);
+            }
+        }
+    }
+}
+
 // bounded LDS spin: a hand-off that never completes traps instead of hanging the device
 __device__ __forceinline__ void eng_wait_eq(int * w, int v) {
     for (int it = 0; eng_ld(w) != v; ++it) {
@@ -676,15 +749,26 @@ __device__ __forceinline__ void eng_wait_eq(int * w, int v) {
     }
 }
 
-// the fp32 chain of one row carried over its chunks (qtypes.h walk(), split at chunk bounds)
+// the fp32 chain of one row carried over its chunks (qtypes.h walk(), split at chunk bounds).
+// The records of a chunk are read 16 at a time before the chain consumes them: a loop that waits
+// for each record's LDS read in turn made a consumer wave's chunk ~3.5k cycles (16 dependent LDS
+// round trips), the engine's bound at 3-7 consumer waves
+constexpr int ENG_WG = 16;
 template <class T> struct eng_walk;
 template <> struct eng_walk<g_q4_K> {
     float A = 0.0f, B = 0.0f;
     __device__ void step(const uint32_t * rr, int nb, int) {
-        for (int b = 0; b < nb; ++b) {
-            const uint4 r = *(const uint4 *) (rr + b * g_q4_K::RS);
-            A = fmaf((float) (int) r.x, asf(r.z), A);
-            B = fmaf((float) (int) r.y, asf(r.w), B);
+        for (int b0 = 0; b0 < nb; b0 += ENG_WG) {
+            uint4 r[ENG_WG];
+#pragma unroll
+            for (int b = 0; b < ENG_WG; ++b) r[b] = *(const uint4 *) (rr + (b0 + b) * g_q4_K::RS);
+#pragma unroll
+            for (int b = 0; b < ENG_WG; ++b) {
+                if (b0 + b < nb) {
+                    A = fmaf((float) (int) r[b].x, asf(r[b].z), A);
+                    B = fmaf((float) (int) r[b].y, asf(r[b].w), B);
+                }
+            }
         }
     }
     __device__ float result() const { return __fsub_rn(A, B); }
@@ -692,9 +776,14 @@ template <> struct eng_walk<g_q4_K> {
 template <> struct eng_walk<g_q4_0> {
     float A = 0.0f;
     __device__ void step(const uint32_t * rr, int nb, int) {
-        for (int b = 0; b < nb; ++b) {
-            const uint2 r = *(const uint2 *) (rr + b * g_q4_0::RS);
-            A = fmaf((float) (int) r.x, asf(r.y), A);
+        for (int b0 = 0; b0 < nb; b0 += ENG_WG) {
+            uint2 r[ENG_WG];
+#pragma unroll
+            for (int b = 0; b < ENG_WG; ++b) r[b] = *(const uint2 *) (rr + (b0 + b) * g_q4_0::RS);
+#pragma unroll
+            for (int b = 0; b < ENG_WG; ++b) {
+                if (b0 + b < nb) A = fmaf((float) (int) r[b].x, asf(r[b].y), A);
+            }
         }
     }
     __device__ float result() const { return A; }
@@ -702,7 +791,19 @@ template <> struct eng_walk<g_q4_0> {
 template <class T, int FO> struct eng_walk_cls {   // class chains (LPR = 8), scale product at dword FO
     float acc = 0.0f;
     __device__ void step(const uint32_t * rr, int nb, int s) {
-        for (int b = 0; b < nb; ++b) acc = fmaf(asf(rr[b * T::RS + FO]), (float) (int) rr[b * T::RS + s], acc);
+        for (int b0 = 0; b0 < nb; b0 += ENG_WG) {
+            float f[ENG_WG];
+            int c[ENG_WG];
+#pragma unroll
+            for (int b = 0; b < ENG_WG; ++b) {
+                f[b] = asf(rr[(b0 + b) * T::RS + FO]);
+                c[b] = (int) rr[(b0 + b) * T::RS + s];
+            }
+#pragma unroll
+            for (int b = 0; b < ENG_WG; ++b) {
+                if (b0 + b < nb) acc = fmaf(f[b], (float) c[b], acc);
+            }
+        }
     }
     __device__ float result() const { return hsum8_lanes(acc); }
 };
@@ -711,9 +812,21 @@ template <> struct eng_walk<g_q8_0> : eng_walk_cls<g_q8_0, 8> {};
 template <> struct eng_walk<g_q5_K> {
     float acc = 0.0f, summs = 0.0f;
     __device__ void step(const uint32_t * rr, int nb, int s) {
-        for (int b = 0; b < nb; ++b) {
-            acc = fmaf(asf(rr[b * g_q5_K::RS + 9]), (float) (int) rr[b * g_q5_K::RS + s], acc);
-            summs = fmaf((float) (int) rr[b * g_q5_K::RS + 8], asf(rr[b * g_q5_K::RS + 10]), summs);
+        for (int b0 = 0; b0 < nb; b0 += ENG_WG) {
+            float f[ENG_WG], fm[ENG_WG];
+            int c[ENG_WG], im[ENG_WG];
+#pragma unroll
+            for (int b = 0; b < ENG_WG; ++b) {
+                const uint32_t * r = rr + (b0 + b) * g_q5_K::RS;
+                f[b] = asf(r[9]); c[b] = (int) r[s]; im[b] = (int) r[8]; fm[b] = asf(r[10]);
+            }
+#pragma unroll
+            for (int b = 0; b < ENG_WG; ++b) {
+                if (b0 + b < nb) {
+                    acc = fmaf(f[b], (float) c[b], acc);
+                    summs = fmaf((float) im[b], fm[b], summs);
+                }
+            }
         }
     }
     __device__ float result() const { return __fadd_rn(hsum8_lanes(acc), summs); }
@@ -798,7 +911,6 @@ template <class T, int NL, int NC, bool ONECH>
 __global__ __launch_bounds__(64 * (NL + NC)) void k_gemv_eng(const gemv_args p, const eng_geo e) {
     using G = os_geo<T>;
     constexpr int P = G::NI;                 // DMA instructions per chunk
-    constexpr int LL = 60 / P / NL;          // chunks in flight per loader (vmcnt holds at most 63)
     constexpr int BPC = WAVE / T::per_block; // blocks (records) per full chunk
     __shared__ __attribute__((aligned(16))) uint8_t lds[ENG_LDS];
     eng_ctrl * cc = (eng_ctrl *) lds;
@@ -820,14 +932,11 @@ __global__ __launch_bounds__(64 * (NL + NC)) void k_gemv_eng(const gemv_args p, 
 
     if (wave < NL) {
         // ---- loader l: chunks l, l + NL, ... ----
+        // Slots are packed (slot = chunk bytes): a piece's lanes past the chunk end are masked, and
+        // a piece wholly past a short chunk (a row's last) lands in the trash line, so every chunk
+        // is P instructions and vmcnt counts chunks exactly
         const int l = wave;
-        // per-lane byte offsets of the P pieces, for a full chunk and for a row's last chunk
-        int ofull[P], olast[P];
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            ofull[q] = min(q * 1024 + 16 * lane, G::SEG - 16);
-            olast[q] = min(q * 1024 + 16 * lane, e.last_bytes - 16);
-        }
+        const int ll = e.ll;
         int j = l;
         int64_t gr = r0;
         while (j >= nch) { j -= nch; ++gr; }
@@ -840,9 +949,8 @@ __global__ __launch_bounds__(64 * (NL + NC)) void k_gemv_eng(const gemv_args p, 
             if (k >= ns && frep != k - ns) eng_wait_eq(&cc->fre[s], k - ns);
             const uint8_t * src = cu.wm + cu.row * cu.nbm + (int64_t) j * G::SEG;
             uint8_t * dst = ring + (size_t) s * e.slot;
-            const bool lastc = j == nch - 1;
-#pragma unroll
-            for (int q = 0; q < P; ++q) eng_dma16(src + (lastc ? olast[q] : ofull[q]), dst + q * 1024);
+            const int cb = j == nch - 1 ? e.last_bytes : G::SEG;
+            eng_issue<P, G::SEG>(eng_rsrc_of(src), dst, cb, lane, lds + e.trash_off);
             // advance to this loader's next chunk
             const int kn = k + NL;
             s += NL;
@@ -853,15 +961,15 @@ __global__ __launch_bounds__(64 * (NL + NC)) void k_gemv_eng(const gemv_args p, 
                 while (j >= nch) { j -= nch; ++gr; }
                 if (gr < r1) cu.locate(p, gr);
             }
-            if (it >= LL) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LL * P) : "memory");
-                const int kp = k - LL * NL;
+            if (it >= ll) {
+                eng_vmwait<P>(ll);
+                const int kp = k - ll * NL;
                 if (lane == 0) eng_st(&cc->full[kp % ns], kp);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
-            for (int kk = l + NL * max(0, it - LL); kk < nck; kk += NL) eng_st(&cc->full[kk % ns], kk);
+            for (int kk = l + NL * max(0, it - ll); kk < nck; kk += NL) eng_st(&cc->full[kk % ns], kk);
         }
     } else {
         // ---- consumers ----
@@ -1144,12 +1252,13 @@ static bool eng_enabled() {
 // loader / consumer waves per workgroup: GGML_MI355X_ENG_CFG = 17 (1 + 7), 26, 214 (default), 412
 static int eng_cfg() {
     static const int c = [] {
-        const int v = getenv("GGML_MI355X_ENG_CFG") ? atoi(getenv("GGML_MI355X_ENG_CFG")) : 214;
-        return v == 17 || v == 26 || v == 412 ? v : 214;
+        const int v = getenv("GGML_MI355X_ENG_CFG") ? atoi(getenv("GGML_MI355X_ENG_CFG")) : 412;
+        return v == 214 || v == 88 || v == 610 ? v : 412;
     }();
     return c;
 }
-static int eng_nc() { const int c = eng_cfg(); return c == 17 ? 7 : (c == 26 ? 6 : (c == 412 ? 12 : 14)); }
+static int eng_nc() { const int c = eng_cfg(); return c == 214 ? 14 : (c == 88 ? 8 : (c == 610 ? 10 : 12)); }
+static int eng_nl() { const int c = eng_cfg(); return c == 214 ? 2 : (c == 88 ? 8 : (c == 610 ? 6 : 4)); }
 // the SwiGLU prologue's sources for the next engine launch (gemv_group sets them)
 static thread_local const float * g_sw_gate = nullptr;
 static thread_local const float * g_sw_up = nullptr;
@@ -1167,9 +1276,14 @@ static bool eng_geometry(const gemv_args & a, int nc, eng_geo & e) {
     if (e.n % 256 != 0 || e.n > 16384 || e.last_bytes % 16 != 0) return false;
     e.rec_off = (uint32_t) (ENG_CTRL + r16(pro_lds_bytes(e.n, e.qmode)));
     e.ring_off = (uint32_t) ((e.rec_off + (size_t) nc * BPC * T::RS * 4 + 1023) / 1024 * 1024);
-    e.slot = (uint32_t) G::SLICE;
-    e.ns = (int) std::min<int64_t>(ENG_NSMAX, (ENG_LDS - (int64_t) e.ring_off) / e.slot);
-    return e.ns >= 60 / G::NI + 4;
+    e.slot = (uint32_t) G::SEG;   // packed: the loader masks a piece's lanes past the chunk
+    e.trash_off = (uint32_t) (ENG_LDS - 1024);
+    e.ns = (int) std::min<int64_t>(ENG_NSMAX, (ENG_LDS - 1024 - (int64_t) e.ring_off) / e.slot);
+    // chunks in flight: as many as the ring holds beside the consumers' working set, within
+    // vmcnt's 63 instructions per loader wave
+    const int nl = eng_nl();
+    e.ll = std::min(63 / G::NI, (e.ns - nc / 2 - 2) / nl);
+    return e.ll >= 2;
 }
 
 template <class T, int NL, int NC>
@@ -1196,10 +1310,10 @@ static bool launch_eng_t(hipStream_t st, gemv_args & a, int nmat) {
     e.sw_up = g_sw_up;
     if (e.act_mode == 1 && a.pro.qmode != e.qmode) return false;
     switch (eng_cfg()) {
-        case 17:  launch_eng_v<T, 1, 7>(st, a, e); break;
-        case 26:  launch_eng_v<T, 2, 6>(st, a, e); break;
-        case 412: launch_eng_v<T, 4, 12>(st, a, e); break;
-        default:  launch_eng_v<T, 2, 14>(st, a, e); break;
+        case 214: launch_eng_v<T, 2, 14>(st, a, e); break;
+        case 88:  launch_eng_v<T, 8, 8>(st, a, e); break;
+        case 610: launch_eng_v<T, 6, 10>(st, a, e); break;
+        default:  launch_eng_v<T, 4, 12>(st, a, e); break;
     }
     return true;
 }
@@ -1363,8 +1477,10 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
     bytes += (double) src1->ne[0] * (kq ? 1.14 : 1.0);
 
     const bool pro = epi && epi->px;
+    const bool swp = epi && epi->sw_gate;
+    GGML_ASSERT(!(pro && swp));
     q8_act act = {};
-    if (!pro && !ctx.qcache_get(src1, kq, act)) {
+    if (!pro && !swp && !ctx.qcache_get(src1, kq, act)) {
         quantize_act(ctx, src1, kq, act, exec_ctx::QSLOT);
         ctx.qcache_put(src1, kq, act);
     }
@@ -1427,6 +1543,11 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         t.cnt = ctx.tail_cnt;
     }
     const int64_t nblk = src1->ne[0] / ggml_blck_size(wt);
+    if (swp) {
+        GGML_ASSERT(nmat == 1 && !a.tl.kind);
+        g_sw_gate = epi->sw_gate;
+        g_sw_up = epi->sw_up;
+    }
     if (ctx.timing) {
         t_ev_beg = ctx.get_event();
         t_ev_end = ctx.get_event();
@@ -1483,6 +1604,7 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         t_ev_beg = t_ev_end = nullptr;
     }
     if (a.tl.qmode) ctx.qcache_put(epi->tq_key, tkq, tact);
+    g_sw_gate = g_sw_up = nullptr;
     g_kt_ctx = nullptr;
 }
 

@@ -56,6 +56,11 @@ struct exec_ctx {
     struct pro_pending { const ggml_tensor * last; const void * data; const float * x; const float * w; const double * sum;
                          float eps; int64_t n; };
     pro_pending pro = {};
+    // SwiGLU prologue pending for the down projection that reads `key` (the MUL of silu(gate)
+    // and up): its engine launch forms silu(gate) * up and the quantized activation itself, so
+    // the SILU and the MUL never run as nodes (dispatch.cpp, GGML_OP_UNARY)
+    struct swiglu_pending { const ggml_tensor * key; const void * data; const float * gate; const float * up; };
+    swiglu_pending swiglu = {};
 
     void * scratch(int slot, size_t bytes);
     void   free_scratch();
@@ -228,12 +233,14 @@ struct gemv_epi {
     // norm prologue: the activation is quant(RMS_NORM(px) [* pw]) with the producer's sums psum
     const float * px = nullptr; const float * pw = nullptr; const double * psum = nullptr;
     float peps = 0.0f; int64_t pn = 0;
+    // SwiGLU prologue (engine only): the activation is quant(silu(sw_gate) * sw_up)
+    const float * sw_gate = nullptr; const float * sw_up = nullptr;
 };
 bool gemv_supported(const ggml_tensor * mm);
 bool gemv_tail_ready(exec_ctx & ctx);
 double * gemv_rsum_site(exec_ctx & ctx);   // a zeroed site of rsum_buf, or nullptr
-bool gemv_ring_wide(int64_t rows);          // a launch of this many rows takes the persistent ring kernel
 bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
+bool gemv_engine_ok(const ggml_tensor * mm);     // the persistent engine (k_gemv_eng) takes this mat-vec
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi);
 bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c);   // c may join mm0's launch as a second weight type
 

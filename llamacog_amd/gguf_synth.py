@@ -80,6 +80,11 @@ CONFIGS = {
     # configs[4]: Mixtral-8x7B Q5_K_M
     "mixtral-8x7b-q5km": ModelConfig("Mixtral-8x7B-synthetic", 4096, 32, 32, 8, 14336, 32000, "q5_k_m",
                                      n_ctx_train=32768, rope_base=1000000.0, n_expert=8, n_expert_used=2),
+    # fast parity model: full Mixtral-8x7B layer shapes (4096 / 14336, 32 / 8 heads, 8 experts,
+    # top-2, Q5_K_M with the Q8_0 attn_k / attn_v of llama-quant.cpp:300-311), 2 layers: layer 0
+    # Q5_K experts, layer 1 the use_more_bits Q6_K ffn_down
+    "mixtral-2l-q5km": ModelConfig("Mixtral-8x7B-2layer-synthetic", 4096, 2, 32, 8, 14336, 32000, "q5_k_m",
+                                   n_ctx_train=32768, rope_base=1000000.0, n_expert=8, n_expert_used=2),
     # fast parity models: full Llama-3-8B layer shapes, 2 layers
     "llama3-8b-2l-q4km": ModelConfig("Llama-3-8B-2layer-synthetic", 4096, 2, 32, 8, 14336, 128256, "q4_k_m"),
     "llama3-8b-2l-q8_0": ModelConfig("Llama-3-8B-2layer-q8-synthetic", 4096, 2, 32, 8, 14336, 128256, "q8_0"),

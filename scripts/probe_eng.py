@@ -37,9 +37,8 @@ def child():
 def main():
     if "--child" in sys.argv:
         return child()
-    variants = [("one-shot", {"GGML_MI355X_GEMV_ENG": "0"}), ("eng 1+7", {"GGML_MI355X_GEMV_ENG": "1", "GGML_MI355X_ENG_CFG": "17"}),
-                ("eng 2+6", {"GGML_MI355X_GEMV_ENG": "1", "GGML_MI355X_ENG_CFG": "26"}), ("eng 2+14", {"GGML_MI355X_GEMV_ENG": "1", "GGML_MI355X_ENG_CFG": "214"}),
-                ("eng 4+12", {"GGML_MI355X_GEMV_ENG": "1", "GGML_MI355X_ENG_CFG": "412"})]
+    variants = [("one-shot", {"GGML_MI355X_GEMV_ENG": "0"})] + [
+        (f"eng {c}", {"GGML_MI355X_GEMV_ENG": "1", "GGML_MI355X_ENG_CFG": c}) for c in ("214", "412", "610", "88")]
     for label, env in variants:
         print(f"== {label}", flush=True)
         e = dict(os.environ)

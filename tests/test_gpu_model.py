@@ -76,6 +76,14 @@ def test_greedy_tiny_moe_q5km():
     _check(_greedy("tiny-moe-q5km", 16, 16, True))
 
 
+def test_greedy_mixtral_2layer_q5km():
+    """Mixtral-8x7B layer shapes (BASELINE.json configs[4]): 8 experts of 4096 x 14336, top-2
+    routing, Q5_K experts with a Q6_K ffn_down on layer 1, Q8_0 attn_k / attn_v (the n_expert == 8
+    rule of src/llama-quant.cpp:300-311); a 32-token prompt (expert-sorted batch MUL_MAT_ID) then
+    decode (per-pair MUL_MAT_ID), bit-identical to the CPU backend."""
+    _check(_greedy("mixtral-2l-q5km", 32, 16, True))
+
+
 def test_greedy_llama3_8b_2layer_q4km():
     _check(_greedy("llama3-8b-2l-q4km", 32, 16, True))
 
@@ -331,3 +339,12 @@ def test_greedy_llama3_8b_2layer_depth1536_bit_identical():
     missed the CPU's f16 VKQ rounding; on this model at this depth its logits differed by 1.56
     max |diff| / max |logit|, which is why it was removed — DESIGN.md §3.)"""
     _check(_greedy("llama3-8b-2l-q4km", 1536, 12, True))
+
+
+@pytest.mark.parametrize("kv", ["q8_0", "q4_0"])
+def test_greedy_llama3_8b_2layer_depth1536_quantized_kv(kv):
+    """Decode at 1536 positions over a q8_0 / q4_0 KV cache (-ctk/-ctv, the north star's flash
+    attention over the quantized KV cache): the long-context pair of kernels (scores by a wide
+    grid with ggml_vec_dot_q8_0_q8_0 / _q4_0_q8_0's class chains, then the f32 recurrence on
+    dequantized V in the CPU's order), bit-identical to the CPU backend."""
+    _check(_greedy("llama3-8b-2l-q4km", 1536, 12, True, kv=kv))
