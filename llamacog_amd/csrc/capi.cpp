@@ -290,8 +290,18 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv(int wtype, int64_t K, int64
 // epi_kind: 0 plain; 1 SiLU of matrix 0; 2 f16 (KV-cache) store of every matrix through a
 // dynamic-pointer slot; 3 NORM rope (Llama-3 parameters, head dim 128) of matrix 0 with its
 // f16 store
+namespace mi355x { extern unsigned long long * g_eng_prof; }
 extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int64_t M, int nmat, int copies, int iters, int epi_kind) {
     const ggml_type t = (ggml_type) wtype;
+    // GGML_MI355X_ENG_PROF=1: the engine's per-workgroup phase counters, averaged over the timed
+    // launches, go to stderr (loader waits for free slots / for landed packets; consumer waits)
+    static const bool eprof = getenv("GGML_MI355X_ENG_PROF") && atoi(getenv("GGML_MI355X_ENG_PROF")) != 0;
+    unsigned long long * ep = nullptr;
+    if (eprof) {
+        MI_CHECK(hipMalloc(&ep, 8 * 4096 * sizeof(unsigned long long)));
+        MI_CHECK(hipMemset(ep, 0, 8 * 4096 * sizeof(unsigned long long)));
+        g_eng_prof = ep;
+    }
     const size_t row = ggml_row_size(t, K);
     const size_t mat = row * (size_t) M;
     std::vector<char *> pool((size_t) copies * nmat);
@@ -420,12 +430,37 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int6
     };
     run(0);   // quantizes X into the cache; later launches reuse it
     for (int i = 1; i < 4; ++i) run(i);
+    if (ep) {
+        MI_CHECK(hipStreamSynchronize(sc.ex.stream));
+        MI_CHECK(hipMemset(ep, 0, 8 * 4096 * sizeof(unsigned long long)));
+    }
     MI_CHECK(hipEventRecord(e0, sc.ex.stream));
     for (int i = 0; i < iters; ++i) run(i);
     MI_CHECK(hipEventRecord(e1, sc.ex.stream));
     MI_CHECK(hipEventSynchronize(e1));
     float ms = 0;
     MI_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    if (ep) {
+        // per launch, averaged over workgroups: loader (per loader wave) fre-wait / vmcnt-wait / total
+        // ticks and packets; consumer (per consumer wave) full-wait / total ticks and rows
+        std::vector<unsigned long long> h(8 * 4096);
+        MI_CHECK(hipMemcpy(h.data(), ep, h.size() * 8, hipMemcpyDeviceToHost));
+        double acc[8] = {0};
+        int nw = 0;
+        for (int w = 0; w < 4096; ++w) {
+            if (h[8 * w + 2] == 0 && h[8 * w + 5] == 0) continue;
+            ++nw;
+            for (int k = 0; k < 8; ++k) acc[k] += (double) h[8 * w + k];
+        }
+        if (nw) {
+            const double f = 1.0 / ((double) nw * iters);
+            fprintf(stderr, "[eng-prof] wg %d: loader waves: fre-wait %.0f vm-wait %.0f total %.0f ticks, %.1f packets | "
+                            "consumer waves: full-wait %.0f total %.0f ticks, %.1f rows (sums over the workgroup's waves)\n",
+                    nw, acc[0] * f, acc[1] * f, acc[2] * f, acc[3] * f, acc[4] * f, acc[5] * f, acc[6] * f);
+        }
+        g_eng_prof = nullptr;
+        MI_CHECK(hipFree(ep));
+    }
     MI_CHECK(hipEventDestroy(e0));
     MI_CHECK(hipEventDestroy(e1));
     for (auto p : pool) MI_CHECK(hipFree(p));
@@ -557,6 +592,9 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
     std::function<void()> run;
     ggml_tensor Q, K, V, Mk, O, X, R, A, N, Wt, Mu;
     unsigned long long * prof = nullptr;
+    // 3: the decode flash attention of 0 over a q8_0 cache
+    const ggml_type fa_kv = which == 3 ? GGML_TYPE_Q8_0 : GGML_TYPE_F16;
+    if (which == 3) which = 0;
     if (which == 2) {
         MI_CHECK(hipMalloc(&prof, 8 * sizeof(unsigned long long)));
         MI_CHECK(hipMemset(prof, 0, 8 * sizeof(unsigned long long)));
@@ -655,8 +693,8 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
     } else if (which == 0) {
         const int64_t D = 128, H = 32, Hkv = 8, n_kv = a;
         float * q = (float *) dalloc(D * H * 4, 0x3c);
-        void * k = dalloc(D * Hkv * n_kv * 2, 0x3c);
-        void * v = dalloc(D * Hkv * n_kv * 2, 0x3c);
+        void * k = dalloc(ggml_row_size(fa_kv, D) * Hkv * n_kv, 0x3c);
+        void * v = dalloc(ggml_row_size(fa_kv, D) * Hkv * n_kv, 0x3c);
         std::vector<uint16_t> hm(n_kv);
         for (int64_t i = 0; i < n_kv; ++i) hm[i] = i < b ? 0 : 0xFC00;
         uint16_t * m = (uint16_t *) dalloc(n_kv * 2, 0);
@@ -666,9 +704,9 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
         init_tensor(Q, GGML_TYPE_F32, neq, q);
         std::swap(Q.ne[1], Q.ne[2]); std::swap(Q.nb[1], Q.nb[2]);
         const int64_t nek[4] = {D, Hkv, n_kv, 1};
-        init_tensor(K, GGML_TYPE_F16, nek, k);
+        init_tensor(K, fa_kv, nek, k);
         std::swap(K.ne[1], K.ne[2]); std::swap(K.nb[1], K.nb[2]);
-        init_tensor(V, GGML_TYPE_F16, nek, v);
+        init_tensor(V, fa_kv, nek, v);
         std::swap(V.ne[1], V.ne[2]); std::swap(V.nb[1], V.nb[2]);
         const int64_t nem[4] = {n_kv, 1, 1, 1}, neo[4] = {D, H, 1, 1};
         init_tensor(Mk, GGML_TYPE_F16, nem, m);

@@ -1498,26 +1498,43 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
                 lds_dma16(vbase + (c0 + row) * a.nbv1 + 16 * col, sm.vl[st] + p * 512);
             }
         } else {
-            for (int i = t; i < n * NB; i += 128) {
-                const int row = i / NB, b = i % NB;
-                const uint8_t * src = (const uint8_t *) vbase + (c0 + row) * a.nbv1 + KB * b;
-                int8_t * vq = sm.vq[st];
-                if constexpr (VT == 2) {
-                    const uint4 q = ld16(src + 2);
-                    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-                    uint32_t lo[4], hi[4];
+            // every load of the chunk in flight before the first LDS store (a loop that stores
+            // each block as it arrives waits one memory round trip per block)
+            constexpr int NPT = CV * NB / 128;   // blocks per stager thread
+            uint4 lo[NPT], hi[NPT];
+            uint32_t dd[NPT];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        lo[k] = ((w[k] & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
-                        hi[k] = (((w[k] >> 4) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
-                    }
-                    *(uint4 *) (vq + row * D + 32 * b) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
-                    *(uint4 *) (vq + row * D + 32 * b + 16) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+            for (int k = 0; k < NPT; ++k) {
+                const int i = t + 128 * k, row = min(i / NB, n - 1), b = i % NB;
+                const uint8_t * src = (const uint8_t *) vbase + (c0 + row) * a.nbv1 + KB * b;
+                if constexpr (VT == 2) {
+                    lo[k] = ld16(src + 2);
                 } else {
-                    *(uint4 *) (vq + row * D + 32 * b) = ld16(src + 2);
-                    *(uint4 *) (vq + row * D + 32 * b + 16) = ld16(src + 18);
+                    lo[k] = ld16(src + 2);
+                    hi[k] = ld16(src + 18);
                 }
-                sm.vd[st][row * NB + b] = h2f(ld2(src));
+                dd[k] = ld2(src);
+            }
+            int8_t * vq = sm.vq[st];
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                const int i = t + 128 * k, row = i / NB, b = i % NB;
+                if (row >= n) continue;
+                if constexpr (VT == 2) {
+                    const uint32_t w[4] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w};
+                    uint32_t l4[4], h4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        l4[u] = ((w[u] & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
+                        h4[u] = (((w[u] >> 4) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
+                    }
+                    *(uint4 *) (vq + row * D + 32 * b) = make_uint4(l4[0], l4[1], l4[2], l4[3]);
+                    *(uint4 *) (vq + row * D + 32 * b + 16) = make_uint4(h4[0], h4[1], h4[2], h4[3]);
+                } else {
+                    *(uint4 *) (vq + row * D + 32 * b) = lo[k];
+                    *(uint4 *) (vq + row * D + 32 * b + 16) = hi[k];
+                }
+                sm.vd[st][row * NB + b] = h2f((uint16_t) dd[k]);
             }
         }
     };
@@ -1526,13 +1543,30 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
     if (wave >= 2) stage(0, 0, (int) min<int64_t>(CV, n_kv));
 
     // ---- coefficients of every position (all waves) ----
+    // every score and mask value of the thread's positions is loaded first, then the passes
+    // scan them (a load per pass would put one memory round trip in each of up to 32 passes)
+    constexpr int NT = FAL_NMAX / 256;
+    float sv[NT];
+    uint16_t mvb[NT];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+        const int64_t j = 256 * k + tid;
+        if (256 * k < n_kv) {
+            const int64_t jc = min(j, n_kv - 1);
+            mvb[k] = mrow ? *(const uint16_t *) (mrow + 2 * jc) : (uint16_t) 0;
+            sv[k] = srow[jc];
+        }
+    }
     float carry = -INFINITY;
     int nrun = 0;
-    for (int64_t t0 = 0; t0 < n_kv; t0 += 256) {
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+        const int64_t t0 = 256 * k;
+        if (t0 >= n_kv) break;
         const int64_t j = t0 + tid;
-        const float m = j < n_kv ? (mrow ? h2f(*(const uint16_t *) (mrow + 2 * j)) : 0.0f) : -INFINITY;
+        const float m = j < n_kv ? h2f(mvb[k]) : -INFINITY;
         const bool live = m != -INFINITY;
-        const float sj = live ? srow[j] : -INFINITY;
+        const float sj = live ? sv[k] : -INFINITY;
         float smx = sj;   // inclusive max-scan over the wave
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1672,20 +1706,25 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
             // f32 recurrence on dequantized V: v = (float) q * d (dequantize_row_q8_0 / _q4_0)
             const int8_t * vq = sm.vq[st] + d;
             const float * vdp = sm.vd[st] + d / 32;
-            auto ldb = [&](int j, float (&vv)[U], float (&vs)[U]) {
+            // a batch's raw int8 values and block scales are read one batch ahead; the dequant
+            // (off the chain) happens in run, so a read's wait never precedes the previous batch
+            struct vraw { int q[U]; float dv[U]; };
+            auto ldb = [&](int j, vraw & vv, float (&vs)[U]) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) vv[u] = __fmul_rn((float) vq[(j + u) * D], vdp[(j + u) * NB]);
+                for (int u = 0; u < U; ++u) { vv.q[u] = vq[(j + u) * D]; vv.dv[u] = vdp[(j + u) * NB]; }
                 ld4(scp + j, vs);
             };
-            auto run = [&](const float (&vv)[U], const float (&vs)[U]) {
+            auto deq = [&](const vraw & vv, int u) { return __fmul_rn((float) vv.q[u], vv.dv[u]); };
+            auto run = [&](const vraw & vv, const float (&vs)[U]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    yf = fmaf(vv[u], vs[u], yf);   // ggml_vec_mad_f32
+                    yf = fmaf(deq(vv, u), vs[u], yf);   // ggml_vec_mad_f32
                     S = __fadd_rn(S, vs[u]);
                 }
             };
             auto fast_run = [&](int j0, int nf) {
-                float va[U], vb[U], sa[U], sb[U];
+                vraw va, vb;
+                float sa[U], sb[U];
                 ldb(j0, va, sa);
                 for (int k = 0; k < nf; k += 2) {
                     ldb(j0 + (k + 1) * U, vb, sb);
@@ -1696,7 +1735,8 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
                 }
             };
             auto general = [&](int j) {
-                float vv[U], vs[U], ms[U];
+                vraw vv;
+                float vs[U], ms[U];
                 ldb(j, vv, vs);
                 ld4(cmp + j, ms);
                 const uint32_t db = deadb(j);
@@ -1706,7 +1746,7 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
                     const bool upd = __float_as_uint(ms[u]) != 0x3f800000u;
                     const float ys = upd ? __fmul_rn(yf, ms[u]) : yf;   // ggml_vec_scale_f32
                     const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
-                    yf = live ? fmaf(vv[u], vs[u], ys) : yf;
+                    yf = live ? fmaf(deq(vv, u), vs[u], ys) : yf;
                     S = live ? __fadd_rn(Ss, vs[u]) : S;
                 }
             };

@@ -69,6 +69,7 @@ struct gemv_args {
     } pro;
     unsigned long long * kt;              // in-graph kernel timeline region (nullable)
     uint32_t wl_off;                      // one-shot kernel: LDS byte offset of the weight slices
+    unsigned long long * eprof;           // engine phase counters (microbenchmark only; nullable)
 };
 
 // the producer's partial sums: no-return f64 atomics serialize per 128-B line at the memory
@@ -629,41 +630,48 @@ __global__ __launch_bounds__(256) void k_gemv_os2(const gemv_args p1, const int6
 // partial sums, or the SwiGLU product silu(gate) * up of the FFN (the k_mul_quant arithmetic).
 // The weight stream therefore never waits for a prologue, and no launch of its own forms one.
 constexpr int ENG_LDS = 160 * 1024;
-constexpr int ENG_NSMAX = 96;
-constexpr int ENG_CTRL = 1024;   // bytes of control words in front of the activation
+constexpr int ENG_NSMAX = 64;
+constexpr int ENG_CTRL = 2048;   // bytes of control words in front of the activation
+constexpr int ENG_RMAX = 128;    // residual rows per workgroup staged in LDS
+constexpr int ENG_GPMAX = 4;     // rows per packet
 
 struct eng_geo {
-    int64_t rows;        // rows over the launch's matrices
-    int ns;              // ring slots
-    int nch;             // chunks per row
+    int ns;              // ring slots (one packet each)
+    int nch;             // chunks (64 tasks) per row
     int last_bytes;      // weight bytes of a row's last chunk
+    int gp;              // rows per packet
+    int pk;              // DMA pieces (KiB) per packet slot
+    int rowb;            // bytes per row (== nb01 of every matrix)
+    int ll;              // packets in flight per loader wave (ll * pk <= 63: vmcnt's range)
     int act_mode;        // 0: copy p.A; 1: RMS-norm prologue (p.pro); 2: SwiGLU prologue
     int qmode;           // activation quantization: 1 Q8_K, 2 Q8_0
+    int nmat;
     int64_t n;           // activation length (K)
     uint32_t rec_off, ring_off, slot, trash_off;
-    int ll;              // chunks in flight per loader wave (ll * P <= 63: vmcnt's range)
     const float * sw_gate; const float * sw_up;   // act_mode 2
 };
 
-// s_waitcnt vmcnt(ll * P) for a runtime ll (an immediate operand: one case per depth)
-template <int P>
-__device__ __forceinline__ void eng_vmwait(int ll) {
-#define EW(n) case n: if constexpr (n * P <= 63) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n * P) : "memory"); } break;
-    switch (ll) {
-        EW(1) EW(2) EW(3) EW(4) EW(5) EW(6) EW(7) EW(8) EW(9) EW(10) EW(11)
-        EW(12) EW(13) EW(14) EW(15) EW(16) EW(17) EW(18) EW(19) EW(20) EW(21)
+// s_waitcnt vmcnt(n) for a runtime n <= 63 (an immediate operand: one case per count)
+__device__ __forceinline__ void eng_vmwait(int n) {
+#define EW(k) case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(k) : "memory"); break;
+#define EW8(k) EW(k) EW(k + 1) EW(k + 2) EW(k + 3) EW(k + 4) EW(k + 5) EW(k + 6) EW(k + 7)
+    switch (n) {
+        EW8(0) EW8(8) EW8(16) EW8(24) EW8(32) EW8(40) EW8(48) EW(56) EW(57) EW(58) EW(59) EW(60) EW(61) EW(62) EW(63)
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
+#undef EW8
 #undef EW
 }
 
 // LDS layout of the control words
 struct eng_ctrl {
-    int full[ENG_NSMAX];   // chunk number last landed in the slot
-    int fre[ENG_NSMAX];    // chunk number last consumed from the slot
+    int full[ENG_NSMAX];   // packet number last landed in the slot
+    int fre[ENG_NSMAX];    // packet number last consumed from the slot
+    int cnt[ENG_NSMAX];    // rows of the slot's packet consumed so far
     int rdy;               // consumer waves done forming the activation
     float pmean;
     double rpart[16];      // residual producer: sum of squares per consumer wave
+    float rres[ENG_RMAX];  // residual producer: the workgroup's residual rows
 };
 static_assert(sizeof(eng_ctrl) <= ENG_CTRL, "engine control words");
 
@@ -704,38 +712,28 @@ __device__ __forceinline__ void eng_bdma(eng_rsrc r, uint32_t voff, const void *
                  : "memory", "m0");
 #endif
 }
-template <int P, int SEG>
-__device__ __forceinline__ void eng_issue(eng_rsrc r, uint8_t * dst, int cb, int lane, uint8_t * trash) {
+// one packet: `bytes` contiguous bytes from src into the slot at dst as pk KiB pieces (pieces
+// wholly past a short packet land in the trash line, a piece's lanes past its end are masked),
+// so every packet is exactly pk instructions and vmcnt counts packets
+__device__ __forceinline__ void eng_issue(const uint8_t * src, uint8_t * dst, int bytes, int pk, int lane, uint8_t * trash) {
     const uint32_t vo = 16u * (uint32_t) lane;
-    if (cb == SEG) {   // a full chunk: the piece count and the last piece's lanes are compile-time
+    for (int q0 = 0; q0 < pk; q0 += 4) {
+        const eng_rsrc r = eng_rsrc_of(src + 1024 * q0);
 #pragma unroll
-        for (int q = 0; q < P; ++q) {
-            constexpr int dummy = 0;
-            (void) dummy;
-            const int rem = SEG - 1024 * q;
-            if (rem >= 1024) {
-                if (q == 0) eng_bdma<0>(r, vo, dst);
-                else if (q == 1) eng_bdma<1024>(r, vo, dst + 1024);
-                else if (q == 2) eng_bdma<2048>(r, vo, dst + 2048);
-                else eng_bdma<3072>(r, vo, dst + 3072);
-            } else if (16 * lane < rem) {
-                if (q == 1) eng_bdma<1024>(r, vo, dst + 1024);
-                else if (q == 2) eng_bdma<2048>(r, vo, dst + 2048);
-                else if (q == 3) eng_bdma<3072>(r, vo, dst + 3072);
-                else eng_bdma<0>(r, vo, dst);
-            }
-        }
-    } else {           // a row's short last chunk: pieces wholly past it land in the trash line
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const int rem = cb - 1024 * q;
-            if (rem <= 0) {
-                eng_bdma<0>(r, (uint32_t) (cb - 16), trash);
-            } else if (16 * lane < rem) {
-                if (q == 0) eng_bdma<0>(r, vo, dst);
-                else if (q == 1) eng_bdma<1024>(r, vo, dst + 1024);
-                else if (q == 2) eng_bdma<2048>(r, vo, dst + 2048);
-                else eng_bdma<3072>(r, vo, dst + 3072);
+        for (int u = 0; u < 4; ++u) {
+            const int q = q0 + u;
+            if (q >= pk) break;
+            const int rem = bytes - 1024 * q;
+            // the instruction offset moves the LDS destination as well as the source
+            // (tools/lds_dma_probe.hip): M0 stays at the group's base
+            uint8_t * d = dst + 1024 * q0;
+            if (rem >= 1024 || 16 * lane < rem) {
+                if (u == 0) eng_bdma<0>(r, vo, d);
+                else if (u == 1) eng_bdma<1024>(r, vo, d);
+                else if (u == 2) eng_bdma<2048>(r, vo, d);
+                else eng_bdma<3072>(r, vo, d);
+            } else if (rem <= 0 && lane == 0) {
+                eng_bdma<0>(eng_rsrc_of(src), 0u, trash);   // keeps the instruction count
             }
         }
     }
@@ -753,7 +751,7 @@ __device__ __forceinline__ void eng_wait_eq(int * w, int v) {
 // The records of a chunk are read 16 at a time before the chain consumes them: a loop that waits
 // for each record's LDS read in turn made a consumer wave's chunk ~3.5k cycles (16 dependent LDS
 // round trips), the engine's bound at 3-7 consumer waves
-constexpr int ENG_WG = 16;
+constexpr int ENG_WG = 8;
 template <class T> struct eng_walk;
 template <> struct eng_walk<g_q4_K> {
     float A = 0.0f, B = 0.0f;
@@ -896,144 +894,174 @@ __device__ __forceinline__ void eng_act(const gemv_args & p, const eng_geo & e, 
     }
 }
 
-// the weight chunks are reached by scalar arithmetic only (no kernel-argument loads in the loop):
-// the row's matrix, base and stride from SGPR copies of the launch's (up to three) matrices
-struct eng_cursor {
-    const uint8_t * wm; int64_t nbm, row;
-    __device__ void locate(const gemv_args & p, int64_t gr) {
-        if (gr >= p.blk0[2]) { wm = p.W[2]; nbm = p.nb01[2]; row = gr - p.blk0[2]; }
-        else if (gr >= p.blk0[1]) { wm = p.W[1]; nbm = p.nb01[1]; row = gr - p.blk0[1]; }
-        else { wm = p.W[0]; nbm = p.nb01[0]; row = gr; }
+// The work of workgroup w: rows [w M / nwg, (w + 1) M / nwg) of EACH matrix (the same rows of
+// gate and up), cut into packets of up to gp rows that never cross a matrix; a packet is one
+// contiguous byte range (rows are nb01 apart and nb01 is the row size)
+struct eng_work {
+    int64_t r0[GEMV_MAXMAT], nr[GEMV_MAXMAT];
+    int np[GEMV_MAXMAT + 1];   // packets before matrix m
+    __device__ void init(const gemv_args & p, const eng_geo & e, int64_t w, int64_t nwg) {
+        np[0] = 0;
+#pragma unroll
+        for (int m = 0; m < GEMV_MAXMAT; ++m) {
+            const int64_t M = m < e.nmat ? p.M[m] : 0;
+            r0[m] = w * M / nwg;
+            nr[m] = (w + 1) * M / nwg - r0[m];
+            np[m + 1] = np[m] + (int) ((nr[m] + e.gp - 1) / e.gp);
+        }
+    }
+    // element m of a three-entry array by selects: a runtime index into a private array would
+    // put the array in scratch memory
+    template <class V> __device__ static V sel(const V (&a)[GEMV_MAXMAT], int m) { return m == 0 ? a[0] : (m == 1 ? a[1] : a[2]); }
+    // packet k: its matrix, first row (in the matrix) and row count
+    __device__ void packet(const eng_geo & e, int k, int & m, int64_t & row, int & n) const {
+        m = k >= np[2] ? 2 : (k >= np[1] ? 1 : 0);
+        const int npm = m == 0 ? 0 : (m == 1 ? np[1] : np[2]);
+        const int64_t i = (int64_t) (k - npm) * e.gp;
+        row = sel(r0, m) + i;
+        n = (int) min<int64_t>(e.gp, sel(nr, m) - i);
     }
 };
 
 template <class T, int NL, int NC, bool ONECH>
 __global__ __launch_bounds__(64 * (NL + NC)) void k_gemv_eng(const gemv_args p, const eng_geo e) {
     using G = os_geo<T>;
-    constexpr int P = G::NI;                 // DMA instructions per chunk
     constexpr int BPC = WAVE / T::per_block; // blocks (records) per full chunk
     __shared__ __attribute__((aligned(16))) uint8_t lds[ENG_LDS];
     eng_ctrl * cc = (eng_ctrl *) lds;
     uint8_t * act = lds + ENG_CTRL;
     uint8_t * ring = lds + e.ring_off;
     kt_enter(p.kt);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ns = e.ns, nch = e.nch;
+    // the wave index as a wave-uniform (SGPR) value: every row / packet / slot computation of the
+    // roles below is then scalar (derived from threadIdx it was VGPR math with quarter-rate
+    // 32-bit multiplies, hundreds of cycles per row)
+    const int wave = __builtin_amdgcn_readfirstlane((int) (threadIdx.x >> 6)), lane = threadIdx.x & 63;
+    const int ns = e.ns, nch = e.nch, gp = e.gp;
     const int64_t w = blockIdx.x, nwg = gridDim.x;
-    const int64_t r0 = w * e.rows / nwg, r1 = (w + 1) * e.rows / nwg;
-    const int nrows = (int) (r1 - r0);
-    const int nck = nrows * nch;
+    eng_work wk;
+    wk.init(p, e, w, nwg);
+    const int npk = wk.np[GEMV_MAXMAT];
     if (threadIdx.x < ENG_NSMAX) {
         cc->full[threadIdx.x] = -1;
-        cc->fre[threadIdx.x] = (int) threadIdx.x - ns;   // "slot s held chunk s - ns": the first round is free
+        cc->fre[threadIdx.x] = (int) threadIdx.x - ns;   // "slot s held packet s - ns": the first round is free
+        cc->cnt[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) cc->rdy = 0;
     __syncthreads();
 
     if (wave < NL) {
-        // ---- loader l: chunks l, l + NL, ... ----
-        // Slots are packed (slot = chunk bytes): a piece's lanes past the chunk end are masked, and
-        // a piece wholly past a short chunk (a row's last) lands in the trash line, so every chunk
-        // is P instructions and vmcnt counts chunks exactly
+        // ---- loader l: packets l, l + NL, ... ----
         const int l = wave;
-        const int ll = e.ll;
-        int j = l;
-        int64_t gr = r0;
-        while (j >= nch) { j -= nch; ++gr; }
-        eng_cursor cu;
-        cu.locate(p, gr);
-        int s = l % ns;
-        int frep = 0;   // fre[] of this loader's next slot, read one chunk ahead
+        const int ll = e.ll, pk = e.pk;
         int it = 0;
-        for (int k = l; k < nck; k += NL, ++it) {
-            if (k >= ns && frep != k - ns) eng_wait_eq(&cc->fre[s], k - ns);
-            const uint8_t * src = cu.wm + cu.row * cu.nbm + (int64_t) j * G::SEG;
-            uint8_t * dst = ring + (size_t) s * e.slot;
-            const int cb = j == nch - 1 ? e.last_bytes : G::SEG;
-            eng_issue<P, G::SEG>(eng_rsrc_of(src), dst, cb, lane, lds + e.trash_off);
-            // advance to this loader's next chunk
-            const int kn = k + NL;
-            s += NL;
-            if (s >= ns) s -= ns;
-            if (kn >= ns && kn < nck) frep = eng_ld(&cc->fre[s]);
-            j += NL;
-            if (j >= nch) {
-                while (j >= nch) { j -= nch; ++gr; }
-                if (gr < r1) cu.locate(p, gr);
-            }
+        const bool prof = p.eprof != nullptr && lane == 0;
+        unsigned long long tw0 = prof ? __builtin_amdgcn_s_memtime() : 0, t_fre = 0, t_vm = 0;
+        for (int k = l; k < npk; k += NL, ++it) {
+            const int s = k % ns;
+            if (prof) { const unsigned long long t = __builtin_amdgcn_s_memtime(); if (k >= ns) eng_wait_eq(&cc->fre[s], k - ns); t_fre += __builtin_amdgcn_s_memtime() - t; }
+            else if (k >= ns) eng_wait_eq(&cc->fre[s], k - ns);
+            int m, n;
+            int64_t row;
+            wk.packet(e, k, m, row, n);
+            const uint8_t * src = (m == 0 ? p.W[0] : (m == 1 ? p.W[1] : p.W[2])) + row * e.rowb;
+            eng_issue(src, ring + (size_t) s * e.slot, n * e.rowb, pk, lane, lds + e.trash_off);
             if (it >= ll) {
-                eng_vmwait<P>(ll);
+                const unsigned long long t = prof ? __builtin_amdgcn_s_memtime() : 0;
+                eng_vmwait(ll * pk);
+                if (prof) t_vm += __builtin_amdgcn_s_memtime() - t;
                 const int kp = k - ll * NL;
                 if (lane == 0) eng_st(&cc->full[kp % ns], kp);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
-            for (int kk = l + NL * max(0, it - ll); kk < nck; kk += NL) eng_st(&cc->full[kk % ns], kk);
+            for (int kk = l + NL * max(0, it - ll); kk < npk; kk += NL) eng_st(&cc->full[kk % ns], kk);
+        }
+        if (prof) {
+            unsigned long long * pe = p.eprof + 8 * w;
+            atomicAdd(pe + 0, t_fre); atomicAdd(pe + 1, t_vm); atomicAdd(pe + 2, __builtin_amdgcn_s_memtime() - tw0);
+            atomicAdd(pe + 3, (unsigned long long) it);
         }
     } else {
-        // ---- consumers ----
+        // ---- consumers: packets c, c + NC, ... (every row of a packet by one wave) ----
         const int cw = wave - NL;
         eng_act<NC>(p, e, act, cw, lane, cc);
+        // the residual rows go to LDS now: a global load in the packet loop would make the wave
+        // wait vmcnt(0) there, i.e. for its previous outputs' stores as well (gfx9 counts stores
+        // in vmcnt), a memory round trip per packet
+        if (p.rres) {
+            for (int i = cw * 64 + lane; i < wk.nr[0]; i += 64 * NC) cc->rres[i] = p.rres[wk.r0[0] + i];
+        }
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_fetch_add(&cc->rdy, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         eng_wait_eq(&cc->rdy, NC);
         const bool kq = e.qmode == 1;
         const int64_t nd = kq ? e.n / 256 : e.n / 32;
         const gemv_act A = {(const int8_t *) act, (const float *) (act + e.n), (const int16_t *) (act + e.n + 4 * nd)};
-        uint32_t * rr = (uint32_t *) (lds + e.rec_off) + (size_t) cw * BPC * T::RS;
+        // records of up to ENG_GPMAX rows of a chunk; walker lanes: row wr = lane / LPR, class ws
+        uint32_t * rr = (uint32_t *) (lds + e.rec_off) + (size_t) cw * ENG_GPMAX * BPC * T::RS;
         const int nblk = p.ntasks / T::per_block;
-        const int ws = lane % T::LPR;
+        const int wr = lane / T::LPR, ws = lane % T::LPR;
         typename T::act x0;
         if constexpr (ONECH) T::load(A, lane < p.ntasks ? lane : 0, x0);
         double ss = 0.0;
-        for (int i = cw; i < nrows; i += NC) {
-            const int64_t gr = r0 + i;
-            eng_cursor cu;
-            cu.locate(p, gr);
-            const int64_t row = cu.row;
-            const float rc = p.rres ? p.rres[row] : 0.0f;
-            eng_walk<T> wk;
+        const bool prof = p.eprof != nullptr && lane == 0;
+        unsigned long long tc0 = prof ? __builtin_amdgcn_s_memtime() : 0, t_full = 0, nrw = 0;
+        int s = cw % ns;
+        for (int k = cw; k < npk; k += NC) {
+            int m, n;
+            int64_t row0;
+            wk.packet(e, k, m, row0, n);
+            if (prof) { const unsigned long long t = __builtin_amdgcn_s_memtime(); eng_wait_eq(&cc->full[s], k); t_full += __builtin_amdgcn_s_memtime() - t; nrw += n; }
+            else eng_wait_eq(&cc->full[s], k);
+            const uint8_t * pb = ring + (size_t) s * e.slot;
+            const int wrc = wr < n ? wr : n - 1;
+            eng_walk<T> wkr;
             for (int j = 0; j < nch; ++j) {
-                const int k = i * nch + j;
-                const int s = k % ns;
                 const int tg = WAVE * j + lane;            // the task in the row
                 const bool active = tg < p.ntasks;
-                eng_wait_eq(&cc->full[s], k);
-                typename T::raw wraw;
-                T::template fetch<typename lds_loader<T>::type>(ring + (size_t) s * e.slot, active ? lane : 0, wraw);
-                // the slot's bytes are in registers (a wave's LDS accesses complete in order)
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0) eng_st(&cc->fre[s], k);
-                if constexpr (ONECH) {
-                    T::rec(wraw, lane, x0, active, rr);
-                } else {
-                    typename T::act x;
-                    T::load(A, active ? tg : 0, x);
-                    T::rec(wraw, lane, x, active, rr);
+                typename T::act xj;
+                if constexpr (!ONECH) T::load(A, active ? tg : 0, xj);
+                const typename T::act & x = ONECH ? x0 : xj;
+#pragma unroll
+                for (int r = 0; r < ENG_GPMAX; ++r) {
+                    if (r < n) {
+                        typename T::raw wraw;
+                        T::template fetch<typename lds_loader<T>::type>(pb + (size_t) r * e.rowb + (size_t) j * G::SEG, active ? lane : 0, wraw);
+                        T::rec(wraw, lane, x, active, rr + (size_t) r * BPC * T::RS);
+                    }
+                }
+                if (j == nch - 1) {
+                    // every row's bytes have been read (a wave's LDS accesses complete in order)
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane == 0) eng_st(&cc->fre[s], k);
                 }
                 wave_lds_sync();
-                wk.step(rr, min(BPC, nblk - BPC * j), ws);
+                wkr.step(rr + (size_t) wrc * BPC * T::RS, min(BPC, nblk - BPC * j), ws);
                 asm volatile("" ::: "memory");
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
             }
-            const float v = wk.result();
-            if (lane == 0) {
-                if (p.rres) {   // ADD(v, res): the CPU's single f32 add
-                    const float xv = __fadd_rn(v, rc);
+            const float v = wkr.result();
+            if (ws == 0 && wr < n) {
+                const int64_t row = row0 + wr;
+                if (p.rres) {   // ADD(v, res): the CPU's single f32 add (one matrix)
+                    const float xv = __fadd_rn(v, cc->rres[row - wk.r0[0]]);
                     p.rxsum[row] = xv;
                     ss = __dadd_rn(ss, (double) __fmul_rn(xv, xv));
-                } else if (gr >= p.blk0[2]) {
-                    p.dst[2][row] = v;
-                } else if (gr >= p.blk0[1]) {
-                    p.dst[1][row] = v;
                 } else {
-                    p.dst[0][row] = v;
+                    (m == 0 ? p.dst[0] : (m == 1 ? p.dst[1] : p.dst[2]))[row] = v;
                 }
             }
+            s += NC;
+            while (s >= ns) s -= ns;
         }
+        ss = wave_sum(ss);   // the walker lanes' sums (the others hold 0)
         if (p.rres && lane == 0) cc->rpart[cw] = ss;
+        if (prof) {
+            unsigned long long * pe = p.eprof + 8 * w;
+            atomicAdd(pe + 4, t_full); atomicAdd(pe + 5, __builtin_amdgcn_s_memtime() - tc0); atomicAdd(pe + 6, nrw);
+        }
     }
     if (p.rres) {
         __syncthreads();
@@ -1259,13 +1287,15 @@ static int eng_cfg() {
 }
 static int eng_nc() { const int c = eng_cfg(); return c == 214 ? 14 : (c == 88 ? 8 : (c == 610 ? 10 : 12)); }
 static int eng_nl() { const int c = eng_cfg(); return c == 214 ? 2 : (c == 88 ? 8 : (c == 610 ? 6 : 4)); }
+// engine phase counters of the microbenchmark (capi mi355x_bench_gemv2, GGML_MI355X_ENG_PROF):
+// per workgroup 8 counters, s_memtime ticks summed over waves
+unsigned long long * g_eng_prof = nullptr;
 // the SwiGLU prologue's sources for the next engine launch (gemv_group sets them)
 static thread_local const float * g_sw_gate = nullptr;
 static thread_local const float * g_sw_up = nullptr;
 
 template <class T>
-static bool eng_geometry(const gemv_args & a, int nc, eng_geo & e) {
-    using G = os_geo<T>;
+static bool eng_geometry(const gemv_args & a, int nmat, int nc, eng_geo & e) {
     constexpr int BPC = WAVE / T::per_block;
     e.nch = (int) ceil_div(a.ntasks, WAVE);
     const int last_tasks = a.ntasks - WAVE * (e.nch - 1);
@@ -1273,17 +1303,30 @@ static bool eng_geometry(const gemv_args & a, int nc, eng_geo & e) {
     constexpr bool kq = T::per_block == 4;
     e.qmode = kq ? 1 : 2;
     e.n = (int64_t) (a.ntasks / T::per_block) * (kq ? 256 : 32);
-    if (e.n % 256 != 0 || e.n > 16384 || e.last_bytes % 16 != 0) return false;
+    e.rowb = (a.ntasks / T::per_block) * T::blk_bytes;
+    if (e.n % 256 != 0 || e.n > 16384 || e.rowb % 16 != 0 || e.last_bytes % 16 != 0) return false;
+    for (int i = 0; i < nmat; ++i) {
+        if (a.nb01[i] != e.rowb) return false;   // packets are contiguous rows
+    }
+    e.nmat = nmat;
+    // rows per packet: the most (up to 4) whose bytes fill whole KiB within 1/32 (12 KiB at most)
+    e.gp = 1;
+    for (int g = 4; g >= 1; --g) {
+        const int by = g * e.rowb, kib = (by + 1023) / 1024;
+        if (kib <= 12 && (kib * 1024 - by) * 32 <= kib * 1024) { e.gp = g; break; }
+    }
+    e.pk = (e.gp * e.rowb + 1023) / 1024;
+    if (e.pk > 16) return false;
     e.rec_off = (uint32_t) (ENG_CTRL + r16(pro_lds_bytes(e.n, e.qmode)));
-    e.ring_off = (uint32_t) ((e.rec_off + (size_t) nc * BPC * T::RS * 4 + 1023) / 1024 * 1024);
-    e.slot = (uint32_t) G::SEG;   // packed: the loader masks a piece's lanes past the chunk
+    e.ring_off = (uint32_t) ((e.rec_off + (size_t) nc * ENG_GPMAX * BPC * T::RS * 4 + 1023) / 1024 * 1024);
+    e.slot = (uint32_t) (e.pk * 1024);
     e.trash_off = (uint32_t) (ENG_LDS - 1024);
     e.ns = (int) std::min<int64_t>(ENG_NSMAX, (ENG_LDS - 1024 - (int64_t) e.ring_off) / e.slot);
-    // chunks in flight: as many as the ring holds beside the consumers' working set, within
-    // vmcnt's 63 instructions per loader wave
+    // packets in flight per loader: what the ring holds beside the consumers' working set (a
+    // packet per gp consumer rows), within vmcnt's 63 instructions per loader wave
     const int nl = eng_nl();
-    e.ll = std::min(63 / G::NI, (e.ns - nc / 2 - 2) / nl);
-    return e.ll >= 2;
+    e.ll = std::min(63 / e.pk, (e.ns - nc - 1) / nl);
+    return e.ll >= 1 && nc < e.ns;
 }
 
 template <class T, int NL, int NC>
@@ -1303,12 +1346,14 @@ static bool launch_eng_t(hipStream_t st, gemv_args & a, int nmat) {
     if (!eng_enabled() || a.tl.kind || needs_epilogue(a, nmat) || !os_aligned<T>(a, nmat)) return false;
     const int nc = eng_nc();
     eng_geo e = {};
-    if (!eng_geometry<T>(a, nc, e)) return false;
-    e.rows = set_groups(a, nmat, 1);
+    if (!eng_geometry<T>(a, nmat, nc, e)) return false;
+    set_groups(a, nmat, 1);
     e.act_mode = g_sw_gate ? 2 : (a.pro.x ? 1 : 0);
     e.sw_gate = g_sw_gate;
     e.sw_up = g_sw_up;
+    a.eprof = g_eng_prof;
     if (e.act_mode == 1 && a.pro.qmode != e.qmode) return false;
+    if (a.rres && (nmat != 1 || ceil_div(a.M[0], g_num_cu) > ENG_RMAX)) return false;
     switch (eng_cfg()) {
         case 214: launch_eng_v<T, 2, 14>(st, a, e); break;
         case 88:  launch_eng_v<T, 8, 8>(st, a, e); break;
@@ -1330,11 +1375,11 @@ bool gemv_engine_ok(const ggml_tensor * mm) {
     const int64_t nblk = w->ne[0] / ggml_blck_size(w->type);
     eng_geo e = {};
     switch (w->type) {
-        case GGML_TYPE_Q4_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q4_K>(a, 1) && eng_geometry<g_q4_K>(a, eng_nc(), e);
-        case GGML_TYPE_Q5_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q5_K>(a, 1) && eng_geometry<g_q5_K>(a, eng_nc(), e);
-        case GGML_TYPE_Q6_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q6_K>(a, 1) && eng_geometry<g_q6_K>(a, eng_nc(), e);
-        case GGML_TYPE_Q8_0: a.ntasks = (int) nblk;       return os_aligned<g_q8_0>(a, 1) && eng_geometry<g_q8_0>(a, eng_nc(), e);
-        case GGML_TYPE_Q4_0: a.ntasks = (int) nblk;       return os_aligned<g_q4_0>(a, 1) && eng_geometry<g_q4_0>(a, eng_nc(), e);
+        case GGML_TYPE_Q4_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q4_K>(a, 1) && eng_geometry<g_q4_K>(a, 1, eng_nc(), e);
+        case GGML_TYPE_Q5_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q5_K>(a, 1) && eng_geometry<g_q5_K>(a, 1, eng_nc(), e);
+        case GGML_TYPE_Q6_K: a.ntasks = (int) (nblk * 4); return os_aligned<g_q6_K>(a, 1) && eng_geometry<g_q6_K>(a, 1, eng_nc(), e);
+        case GGML_TYPE_Q8_0: a.ntasks = (int) nblk;       return os_aligned<g_q8_0>(a, 1) && eng_geometry<g_q8_0>(a, 1, eng_nc(), e);
+        case GGML_TYPE_Q4_0: a.ntasks = (int) nblk;       return os_aligned<g_q4_0>(a, 1) && eng_geometry<g_q4_0>(a, 1, eng_nc(), e);
         default: return false;
     }
 }

@@ -38,7 +38,8 @@ def main():
     if "--child" in sys.argv:
         return child()
     variants = [("one-shot", {"GGML_MI355X_GEMV_ENG": "0"})] + [
-        (f"eng {c}", {"GGML_MI355X_GEMV_ENG": "1", "GGML_MI355X_ENG_CFG": c}) for c in ("214", "412", "610", "88")]
+        (f"eng {c}", {"GGML_MI355X_GEMV_ENG": "1", "GGML_MI355X_ENG_CFG": c}) for c in ("214", "412")] + [
+        ("eng 412 prof", {"GGML_MI355X_GEMV_ENG": "1", "GGML_MI355X_ENG_CFG": "412", "GGML_MI355X_ENG_PROF": "1"})]
     for label, env in variants:
         print(f"== {label}", flush=True)
         e = dict(os.environ)
@@ -46,6 +47,9 @@ def main():
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=e, capture_output=True, text=True,
                            timeout=240)
         print(r.stdout, end="", flush=True)
+        for line in r.stderr.splitlines():
+            if "[eng-prof]" in line:
+                print("   ", line, flush=True)
         if r.returncode != 0:
             print(f"[rc={r.returncode}] {r.stderr[-600:]}", flush=True)
             return r.returncode
