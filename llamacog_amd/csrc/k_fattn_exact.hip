@@ -75,6 +75,25 @@ __device__ __forceinline__ void lds_dma16(const void * src, const void * lds) {
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory", "m0");
 }
 
+// the same for 4 B per lane (global_load_lds_dword): rows that are not 16-B granular (q8_0 / q4_0
+// cache rows of 136 / 72 B) packed in LDS
+__device__ __forceinline__ void lds_dma4(const void * src, const void * lds) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (lds_ptr_t) lds);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(src) : "memory", "m0");
+}
+
+// s_waitcnt vmcnt(n) for a runtime n (an immediate operand: one case per count, up to 63)
+__device__ __forceinline__ void eng_vm_wait_fa(int n) {
+#define FW(k) case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(k) : "memory"); break;
+#define FW8(k) FW(k) FW(k + 1) FW(k + 2) FW(k + 3) FW(k + 4) FW(k + 5) FW(k + 6) FW(k + 7)
+    switch (n) {
+        FW8(0) FW8(8) FW8(16) FW8(24) FW8(32) FW8(40) FW8(48) FW(56) FW(57) FW(58) FW(59) FW(60) FW(61) FW(62) FW(63)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef FW8
+#undef FW
+}
+
 // one step of the f16 accumulation, y = f16(fma(v, vs, y)) with v and y as f16 bits in the low
 // halves: v_fma_mix_f32 converts both exactly and rounds the fma once to f32, v_cvt_f16_f32
 // rounds that to f16 — the CPU's cvtph_ps / fmadd_ps / cvtps_ph sequence, two dependent
@@ -1340,7 +1359,8 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
 // its chain waves run the recurrence while its stager waves stream the next V chunk into LDS.
 // The arithmetic of every step is k_fattn_exact's (the CPU's ops.cpp:7015-7232), so the bits are.
 constexpr int FAL_PB = 256;       // positions per scores workgroup
-constexpr int FAL_NMAX = 8192;    // positions the chain's coefficient arrays hold
+constexpr int FAL_THREADS = 384;   // chain: waves 0-1 the recurrence, 2-5 stage V (0-3 the coefficients)
+constexpr int FAL_NMAX = 6144;    // positions the chain's coefficient arrays hold
 constexpr int FAL_GMAX = 8;       // query heads per KV head (GQA) the scores kernel takes
 constexpr int FAL_U = 8;          // chain batch
 
@@ -1460,7 +1480,9 @@ __global__ __launch_bounds__(256) void k_fal_scores(const fa_args a, float * __r
 // LDS of the chain kernel
 template <int VT> struct fal_smem {
     static constexpr int D = 128, NB = D / 32;
-    static constexpr int CV = VT ? 256 : 128;   // V positions per stage (32 KiB of f16 / int8 values)
+    static constexpr int CV = 128;                        // V positions per stage
+    static constexpr int RB = VT == 0 ? 2 * D : (VT == 1 ? 34 * NB : 18 * NB);   // bytes per V row (raw)
+    static constexpr int NSTG = 3;                        // stages: chunks c + 1 and c + 2 in flight
     float cm[FAL_NMAX + 2 * FAL_U];             // ms coefficient (1 where dead)
     float sc[FAL_NMAX + 2 * FAL_U];             // vs coefficient (0 where dead)
     uint32_t dead[FAL_NMAX / 32 + 2];           // bit per position: masked (the state is kept)
@@ -1468,16 +1490,14 @@ template <int VT> struct fal_smem {
     float wmax[4];
     int wlast[4];
     float ol[128];
-    __attribute__((aligned(16))) uint16_t vl[2][VT ? 1 : CV * D];
-    __attribute__((aligned(16))) int8_t vq[2][VT ? CV * D : 1];
-    float vd[2][VT ? CV * NB : 1];
+    // V rows exactly as in the cache (f16, or q8_0 / q4_0 blocks), packed, by LDS-DMA
+    __attribute__((aligned(16))) uint8_t vr[NSTG][CV * RB + 64];
 };
 
 template <int VT>   // V type: 0 f16, 1 q8_0, 2 q4_0
-__global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const float * __restrict__ sco) {
+__global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, const float * __restrict__ sco) {
     using SM = fal_smem<VT>;
     constexpr int D = 128, NB = D / 32, CV = SM::CV, U = FAL_U;
-    constexpr int KB = VT == 2 ? 18 : 34;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     kt_enter(a.kt);
     const int64_t h = blockIdx.x, iq3 = blockIdx.y;
@@ -1487,60 +1507,46 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
     const char * mrow = a.mask;
     const float * srow = sco + (iq3 * a.H + h) * a.n_kv;
 
-    // ---- stage V rows [c0, c0 + n) into buffer st: waves 2-3 ----
-    auto stage = [&](int st, int64_t c0, int n) {
-        const int t = tid - 128;
-        if constexpr (VT == 0) {
-            // 4 rows of 256 B per 1 KiB LDS-DMA instruction
+    // ---- stage V rows [c0, c0 + n) into buffer st by LDS-DMA: waves 2-5, every row as it is in
+    // the cache.  Rows back to back in the cache (one KV head) are one contiguous byte range: 1 KiB
+    // per instruction.  Otherwise (the llama view: a position's heads interleaved) f16 rows go 4 to
+    // an instruction and q8_0 / q4_0 rows (136 / 72 B, not 16-B granular) a dword a lane: per wave
+    // and chunk of 128 at most 17 instructions, so two chunks in flight stay within vmcnt's 63.
+    // Returns this wave's instruction count (its vmcnt share of the stage).
+    constexpr int RB = SM::RB, NSTG = SM::NSTG;
+    const bool contig = a.nbv1 == RB && ((uintptr_t) vbase & 15) == 0;
+    auto stage = [&](int st, int64_t c0, int n) -> int {
+        const int t = tid - 128, sw = t >> 6;   // stager wave 0..3
+        uint8_t * dst = sm.vr[st];
+        int cnt = 0;
+        if (contig) {
+            const char * src = vbase + c0 * RB;
+            const int nbytes = n * RB;
+            for (int q = sw; 1024 * q < nbytes; q += 4, ++cnt)
+                lds_dma16(src + min(1024 * q + 16 * (t & 63), nbytes - 16), dst + 1024 * q);
+        } else if constexpr (VT == 0) {
             const int r_in = (t & 63) >> 4, col = t & 15;
-            for (int p = t >> 6; 4 * p < n; p += 2) {
-                const int row = min(4 * p + r_in, n - 1);
-                lds_dma16(vbase + (c0 + row) * a.nbv1 + 16 * col, sm.vl[st] + p * 512);
+            for (int q = sw; 4 * q < n; q += 4, ++cnt) {
+                const int row = min(4 * q + r_in, n - 1);
+                lds_dma16(vbase + (c0 + row) * a.nbv1 + 16 * col, dst + 1024 * q);
             }
         } else {
-            // every load of the chunk in flight before the first LDS store (a loop that stores
-            // each block as it arrives waits one memory round trip per block)
-            constexpr int NPT = CV * NB / 128;   // blocks per stager thread
-            uint4 lo[NPT], hi[NPT];
-            uint32_t dd[NPT];
-#pragma unroll
-            for (int k = 0; k < NPT; ++k) {
-                const int i = t + 128 * k, row = min(i / NB, n - 1), b = i % NB;
-                const uint8_t * src = (const uint8_t *) vbase + (c0 + row) * a.nbv1 + KB * b;
-                if constexpr (VT == 2) {
-                    lo[k] = ld16(src + 2);
-                } else {
-                    lo[k] = ld16(src + 2);
-                    hi[k] = ld16(src + 18);
-                }
-                dd[k] = ld2(src);
-            }
-            int8_t * vq = sm.vq[st];
-#pragma unroll
-            for (int k = 0; k < NPT; ++k) {
-                const int i = t + 128 * k, row = i / NB, b = i % NB;
-                if (row >= n) continue;
-                if constexpr (VT == 2) {
-                    const uint32_t w[4] = {lo[k].x, lo[k].y, lo[k].z, lo[k].w};
-                    uint32_t l4[4], h4[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        l4[u] = ((w[u] & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
-                        h4[u] = (((w[u] >> 4) & 0x0f0f0f0fu) + 0x78787878u) ^ 0x80808080u;
-                    }
-                    *(uint4 *) (vq + row * D + 32 * b) = make_uint4(l4[0], l4[1], l4[2], l4[3]);
-                    *(uint4 *) (vq + row * D + 32 * b + 16) = make_uint4(h4[0], h4[1], h4[2], h4[3]);
-                } else {
-                    *(uint4 *) (vq + row * D + 32 * b) = lo[k];
-                    *(uint4 *) (vq + row * D + 32 * b + 16) = hi[k];
-                }
-                sm.vd[st][row * NB + b] = h2f((uint16_t) dd[k]);
+            constexpr int DW = RB / 4;   // dword i of the stage = row i / DW, dword i % DW
+            const int ndw = n * DW;
+            for (int q = sw; 64 * q < ndw; q += 4, ++cnt) {
+                const int i = min(64 * q + (t & 63), ndw - 1), row = i / DW, w = i % DW;
+                lds_dma4(vbase + (c0 + row) * a.nbv1 + 4 * w, dst + 256 * q);
             }
         }
+        return cnt;
     };
-    // chunk 0's V goes out first (bounded by the cache; the mask bounds it later)
+    // chunks 0 and 1 go out first (bounded by the cache; the mask bounds them later)
     const int64_t n_kv = a.n_kv;
-    if (wave >= 2) stage(0, 0, (int) min<int64_t>(CV, n_kv));
+    int pend = 0;   // this stager wave's instructions of the chunk after the current one
+    if (wave >= 2) {
+        stage(0, 0, (int) min<int64_t>(CV, n_kv));
+        if (n_kv > CV) pend = stage(1, CV, (int) min<int64_t>(CV, n_kv - CV));
+    }
 
     // ---- coefficients of every position (all waves) ----
     // every score and mask value of the thread's positions is loaded first, then the passes
@@ -1548,10 +1554,11 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
     constexpr int NT = FAL_NMAX / 256;
     float sv[NT];
     uint16_t mvb[NT];
+    const bool cw = tid < 256;   // waves 0-3 form the coefficients; 4-5 only join the barriers
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
         const int64_t j = 256 * k + tid;
-        if (256 * k < n_kv) {
+        if (cw && 256 * k < n_kv) {
             const int64_t jc = min(j, n_kv - 1);
             mvb[k] = mrow ? *(const uint16_t *) (mrow + 2 * jc) : (uint16_t) 0;
             sv[k] = srow[jc];
@@ -1564,6 +1571,12 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
         const int64_t t0 = 256 * k;
         if (t0 >= n_kv) break;
         const int64_t j = t0 + tid;
+        if (!cw) {   // the two barriers of the pass, and the live extent (the stagers need it)
+            __syncthreads();
+            nrun = max(nrun, max(max(sm.wlast[0], sm.wlast[1]), max(sm.wlast[2], sm.wlast[3])) + 1);
+            __syncthreads();
+            continue;
+        }
         const float m = j < n_kv ? h2f(mvb[k]) : -INFINITY;
         const bool live = m != -INFINITY;
         const float sj = live ? sv[k] : -INFINITY;
@@ -1616,18 +1629,19 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
     }
     __syncthreads();
 
-    // ---- the recurrence: waves 0-1 one output dim per lane; waves 2-3 stage the next V chunk ----
+    // ---- the recurrence: waves 0-1 one output dim per lane; waves 2-3 keep two chunks in flight ----
     const int d = tid;
     uint32_t yb = 0;     // f16 bits (f16 V)
     float yf = 0.0f;     // f32 accumulator (quantized V)
     float S = 0.0f;
     const int nchunk = (nrun + CV - 1) / CV;
     for (int c = 0; c < nchunk; ++c) {
-        const int st = c & 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();   // stage st is in; every chain lane is done with stage st ^ 1
+        const int st = c % NSTG;
+        // this wave's stage-c instructions have landed (those of c + 1 may still be in flight)
+        if (wave >= 2) eng_vm_wait_fa(pend);
+        __syncthreads();   // stage c is in; every chain lane is done with chunk c - 1's stage
         if (wave >= 2) {
-            if (c + 1 < nchunk) stage(st ^ 1, (int64_t) (c + 1) * CV, min(CV, nrun - (c + 1) * CV));
+            pend = c + 2 < nchunk ? stage((c + 2) % NSTG, (int64_t) (c + 2) * CV, min(CV, nrun - (c + 2) * CV)) : 0;
             continue;
         }
         const int jc = c * CV;                  // first position of the chunk
@@ -1650,7 +1664,7 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
             }
         };
         if constexpr (VT == 0) {
-            const uint16_t * vrow = sm.vl[st] + d;
+            const uint16_t * vrow = (const uint16_t *) sm.vr[st] + d;
             auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) vv[u] = vrow[(j + u) * D];
@@ -1704,17 +1718,29 @@ __global__ __launch_bounds__(256, 1) void k_fal_chain(const fa_args a, const flo
             }
         } else {
             // f32 recurrence on dequantized V: v = (float) q * d (dequantize_row_q8_0 / _q4_0)
-            const int8_t * vq = sm.vq[st] + d;
-            const float * vdp = sm.vd[st] + d / 32;
-            // a batch's raw int8 values and block scales are read one batch ahead; the dequant
-            // (off the chain) happens in run, so a read's wait never precedes the previous batch
-            struct vraw { int q[U]; float dv[U]; };
+            // the lane's byte and its block's f16 scale in a raw row: q8_0 block b = d / 32 at 34 b
+            // (d at +2, qs at +2 + d % 32); q4_0 at 18 b (qs at +2 + d % 16, low nibble for d % 32 < 16)
+            constexpr int KBV = VT == 2 ? 18 : 34;
+            const int bo = KBV * (d / 32);
+            const int qo = bo + 2 + (VT == 2 ? (d % 16) : (d % 32));
+            const int nsh = VT == 2 && (d % 32) >= 16 ? 4 : 0;
+            const uint8_t * vrw = sm.vr[st];
+            // a batch's raw bytes and block scales are read one batch ahead; the dequant (off the
+            // chain) happens in run, so a read's wait never precedes the previous batch
+            struct vraw { uint32_t q[U]; uint32_t dv[U]; };
             auto ldb = [&](int j, vraw & vv, float (&vs)[U]) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) { vv.q[u] = vq[(j + u) * D]; vv.dv[u] = vdp[(j + u) * NB]; }
+                for (int u = 0; u < U; ++u) {
+                    vv.q[u] = vrw[(j + u) * RB + qo];
+                    vv.dv[u] = *(const uint16_t *) (vrw + (j + u) * RB + bo);
+                }
                 ld4(scp + j, vs);
             };
-            auto deq = [&](const vraw & vv, int u) { return __fmul_rn((float) vv.q[u], vv.dv[u]); };
+            // dequantize_row_q8_0 / _q4_0: (float) q * d, q4_0's q = nibble - 8
+            auto deq = [&](const vraw & vv, int u) {
+                const int q = VT == 2 ? (int) ((vv.q[u] >> nsh) & 15u) - 8 : (int) (int8_t) vv.q[u];
+                return __fmul_rn((float) q, h2f((uint16_t) vv.dv[u]));
+            };
             auto run = [&](const vraw & vv, const float (&vs)[U]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -1824,9 +1850,9 @@ void launch_fattn_long(hipStream_t st, const fa_args & a0, float * sco, unsigned
     a.kt = a0.kt;
     const dim3 gc((unsigned) a.H, 1);
     switch (a.v_type) {
-        case GGML_TYPE_F16:  hipLaunchKernelGGL(k_fal_chain<0>, gc, dim3(256), 0, st, a, (const float *) sco); break;
-        case GGML_TYPE_Q8_0: hipLaunchKernelGGL(k_fal_chain<1>, gc, dim3(256), 0, st, a, (const float *) sco); break;
-        default:             hipLaunchKernelGGL(k_fal_chain<2>, gc, dim3(256), 0, st, a, (const float *) sco); break;
+        case GGML_TYPE_F16:  hipLaunchKernelGGL(k_fal_chain<0>, gc, dim3(FAL_THREADS), 0, st, a, (const float *) sco); break;
+        case GGML_TYPE_Q8_0: hipLaunchKernelGGL(k_fal_chain<1>, gc, dim3(FAL_THREADS), 0, st, a, (const float *) sco); break;
+        default:             hipLaunchKernelGGL(k_fal_chain<2>, gc, dim3(FAL_THREADS), 0, st, a, (const float *) sco); break;
     }
 }
 

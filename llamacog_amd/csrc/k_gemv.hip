@@ -1325,8 +1325,9 @@ static bool eng_geometry(const gemv_args & a, int nmat, int nc, eng_geo & e) {
     // packets in flight per loader: what the ring holds beside the consumers' working set (a
     // packet per gp consumer rows), within vmcnt's 63 instructions per loader wave
     const int nl = eng_nl();
-    e.ll = std::min(63 / e.pk, (e.ns - nc - 1) / nl);
-    return e.ll >= 1 && nc < e.ns;
+    // (no deadlock while ns > ll * nl: a loader publishes packet k once it has issued k + ll * nl)
+    e.ll = std::min(63 / e.pk, (e.ns - 1 - nc / 4) / nl);
+    return e.ll >= 1;
 }
 
 template <class T, int NL, int NC>

@@ -804,13 +804,13 @@ void orc_soft_max(const float * x, int64_t nc, int64_t nr, const float * mask, i
  * 99.97% bit-exact on tests/golden/flash_attn.npz, the fused one 98%) */
 #define FA_S_UPDATE(S, ms, vs) ((S) * (ms) + (vs))
 #endif
-/* ggml_compute_forward_flash_attn_ext_f16, ops.cpp:7015-7232, for K/V f16 or q8_0.
+/* ggml_compute_forward_flash_attn_ext_f16, ops.cpp:7015-7232, for K/V f16, q8_0 or q4_0.
  * q: [n_q][H][D] f32, k/v: [n_kv][Hkv][D] in kv_type, mask: [n_q][n_kv] f16 (may be NULL),
  * out: [n_q][H][D].  f16 V accumulates VKQ in f16 exactly like the CPU (ops.cpp:7147-7171). */
 void orc_flash_attn(const float * q, const void * k, const void * v, const uint16_t * mask, int kv_type, int64_t D,
                     int64_t n_q, int64_t H, int64_t n_kv, int64_t Hkv, float scale, float softcap, float * out) {
     const int64_t gqa = H / Hkv;
-    const size_t row = kv_type == T_F16 ? D * 2 : (D / 32) * sizeof(b_q8_0);
+    const size_t row = kv_type == T_F16 ? D * 2 : (D / 32) * (kv_type == T_Q4_0 ? sizeof(b_q4_0) : sizeof(b_q8_0));
     if (softcap != 0) scale /= softcap;
     float * vkq32 = (float *) malloc(sizeof(float) * D);
     uint16_t * vkq16 = (uint16_t *) malloc(sizeof(uint16_t) * D);
@@ -841,7 +841,7 @@ void orc_flash_attn(const float * q, const void * k, const void * v, const uint1
                     for (int64_t d = 0; d < D; ++d) kf[d] = orc_fp16_to_fp32(((const uint16_t *) kd)[d]);
                     s = dot_avx512(kf, qf, D);
                 } else {
-                    s = orc_dot_cpu(T_Q8_0, D, kd, q8, 0);   /* ggml_vec_dot_q8_0_q8_0 order */
+                    s = orc_dot_cpu(kv_type, D, kd, q8, 0);   /* ggml_vec_dot_q8_0_q8_0 / _q4_0_q8_0 order */
                 }
                 s = s * scale;
                 if (softcap != 0.0f) s = softcap * tanhf(s);

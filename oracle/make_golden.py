@@ -7,7 +7,7 @@ produce golden input/output vectors for the hot path:
   * activation quantizers (the CPU backend's from_float for Q8_K and Q8_0),
   * model-file quantized weights (ggml_quantize_chunk) + their dequantization,
   * per-row vec_dot results and CPU mul_mat outputs for Q4_0/Q8_0/Q4_K/Q5_K/Q6_K,
-  * rms_norm, rope (NORM/NEOX, Llama-3 base 500000), soft_max, flash_attn_ext (f16 and q8_0 KV).
+  * rms_norm, rope (NORM/NEOX, Llama-3 base 500000), soft_max, flash_attn_ext (f16, q8_0 and q4_0 KV; a depth-1300 decode case).
 Inputs follow tests/test-quantize-fns.cpp:31-35 (0.1 + 2*cos(i + offset)) plus seeded
 random data and hand-made edge cases.  Run here (where /root/reference exists):
     python oracle/make_golden.py
@@ -210,6 +210,24 @@ def moe_cpu_orders(lib):
     print(f"moe_cpu.npz {os.path.getsize(os.path.join(OUT, 'moe_cpu.npz'))} B")
 
 
+def fa_case(lib, fa, tag, q, kf, vf, m, kvt, kvname, D, H, Hkv, n_kv):
+    """one flash_attn_ext case through the reference CPU backend (gg_flash_attn), stored under tag"""
+    if kvt == F16:
+        kb, vb = kf.astype(np.float16).view(np.uint8), vf.astype(np.float16).view(np.uint8)
+    else:
+        kb = quantize(lib, kvt, kf.reshape(-1, D)).reshape(-1)
+        vb = quantize(lib, kvt, vf.reshape(-1, D)).reshape(-1)
+    n_q = q.shape[0]
+    out = np.zeros((n_q, H, D), dtype=np.float32)
+    lib.gg_flash_attn(fptr(q), fptr(np.ascontiguousarray(kb)), fptr(np.ascontiguousarray(vb)),
+                      fptr(m.view(np.uint16)), kvt, D, n_q, H, n_kv, Hkv, 1.0 / np.sqrt(D), 0.0, fptr(out), 1)
+    fa[f"q_{tag}"] = q
+    fa[f"k_{kvname}_{tag}"] = np.ascontiguousarray(kb)
+    fa[f"v_{kvname}_{tag}"] = np.ascontiguousarray(vb)
+    fa[f"mask_{tag}"] = m.view(np.uint16)
+    fa[f"out_{kvname}_{tag}"] = out
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     lib = load()
@@ -292,21 +310,21 @@ def main():
         for r in range(n_q):
             m[r, valid + r:] = -np.inf
         m[:, 3] = -np.inf
-        for kvt, kvname in ((F16, "f16"), (Q8_0, "q8_0")):
-            if kvt == F16:
-                kb, vb = kf.astype(np.float16).view(np.uint8), vf.astype(np.float16).view(np.uint8)
-            else:
-                kb = quantize(lib, Q8_0, kf.reshape(-1, D)).reshape(-1)
-                vb = quantize(lib, Q8_0, vf.reshape(-1, D)).reshape(-1)
-            out = np.zeros((n_q, H, D), dtype=np.float32)
-            lib.gg_flash_attn(fptr(q), fptr(np.ascontiguousarray(kb)), fptr(np.ascontiguousarray(vb)),
-                              fptr(m.view(np.uint16)), kvt, D, n_q, H, n_kv, Hkv, 1.0 / np.sqrt(D), 0.0, fptr(out), 1)
-            fa[f"q_{n_q}"] = q
-            fa[f"k_{kvname}_{n_q}"] = np.ascontiguousarray(kb)
-            fa[f"v_{kvname}_{n_q}"] = np.ascontiguousarray(vb)
-            fa[f"mask_{n_q}"] = m.view(np.uint16)
-            fa[f"out_{kvname}_{n_q}"] = out
-    np.savez_compressed(os.path.join(OUT, "flash_attn.npz"), D=D, H=H, Hkv=Hkv, n_kv=n_kv, **fa)
+        for kvt, kvname in ((F16, "f16"), (Q8_0, "q8_0"), (Q4_0, "q4_0")):
+            fa_case(lib, fa, f"{n_q}", q, kf, vf, m, kvt, kvname, D, H, Hkv, n_kv)
+    # decode at depth (the long-context pair: scores grid + per-head chain), one KV head (its rows
+    # back to back in the cache) and a mask with holes and a dead tail
+    n_kv_l, H_l, Hkv_l = 1300, 4, 1
+    q = rng.standard_normal((1, H_l, D)).astype(np.float32) * 2
+    kf = rng.standard_normal((n_kv_l, Hkv_l, D)).astype(np.float32)
+    vf = rng.standard_normal((n_kv_l, Hkv_l, D)).astype(np.float32)
+    m = np.zeros((1, n_kv_l), dtype=np.float16)
+    m[0, rng.random(n_kv_l) < 0.25] = -np.inf
+    m[0, 1290:] = -np.inf
+    for kvt, kvname in ((F16, "f16"), (Q8_0, "q8_0"), (Q4_0, "q4_0")):
+        fa_case(lib, fa, "long", q, kf, vf, m, kvt, kvname, D, H_l, Hkv_l, n_kv_l)
+    np.savez_compressed(os.path.join(OUT, "flash_attn.npz"), D=D, H=H, Hkv=Hkv, n_kv=n_kv, H_long=H_l, Hkv_long=Hkv_l,
+                        n_kv_long=n_kv_l, **fa)
     moe(lib)
     cpu_orders(lib)
     moe_cpu_orders(lib)

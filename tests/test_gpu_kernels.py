@@ -151,6 +151,44 @@ def test_flash_attn_q8_0_golden(K, golden_dir, n_q):
     assert_bits(out, g[f"out_q8_0_{n_q}"], f"flash_attn q8_0 n_q={n_q}")
 
 
+@pytest.mark.parametrize("tag", ["1", "7", "long"])
+@pytest.mark.parametrize("kv", ["f16", "q8_0", "q4_0"])
+def test_flash_attn_golden_all_kv(K, golden_dir, tag, kv):
+    """Every KV type against the reference CPU backend's own outputs, including a depth-1300 decode
+    (the long-context pair: scores grid + per-head chain, one KV head so its rows are contiguous)."""
+    g = load(golden_dir, "flash_attn.npz")
+    sfx = "_long" if tag == "long" else ""
+    D, H, Hkv, n_kv = int(g["D"]), int(g["H" + sfx]), int(g["Hkv" + sfx]), int(g["n_kv" + sfx])
+    kvt = {"f16": O.F16, "q8_0": O.Q8_0, "q4_0": O.Q4_0}[kv]
+    out = K.flash_attn(g[f"q_{tag}"], g[f"k_{kv}_{tag}"], g[f"v_{kv}_{tag}"], g[f"mask_{tag}"], kvt, D, H, Hkv, n_kv,
+                       1.0 / np.sqrt(D))
+    assert_bits(out, g[f"out_{kv}_{tag}"], f"flash_attn {kv} {tag}")
+
+
+@pytest.mark.parametrize("kv,n_kv,Hkv,G,pattern", [("q8_0", 2500, 8, 4, "holes"), ("q4_0", 1300, 8, 4, "causal"),
+                                                   ("q4_0", 4100, 2, 8, "sparse"), ("q8_0", 1024, 1, 8, "causal"),
+                                                   ("q8_0", 6144, 8, 4, "causal")])
+def test_flash_attn_quant_long_vs_oracle(K, kv, n_kv, Hkv, G, pattern):
+    """Quantized caches at depth through the long-context pair: interleaved heads (the llama cache
+    view: rows a dword a lane into LDS) and a single KV head (contiguous rows), ragged last chunk,
+    the longest cache the chain takes (6144)."""
+    rng = np.random.default_rng(n_kv + Hkv)
+    D, H = 128, Hkv * G
+    kvt = O.Q8_0 if kv == "q8_0" else O.Q4_0
+    q = (rng.standard_normal((1, H, D)) * 2).astype(np.float32)
+    k = O.quantize_rows(kvt, rng.standard_normal((n_kv * Hkv, D)).astype(np.float32)).reshape(n_kv, -1)
+    v = O.quantize_rows(kvt, rng.standard_normal((n_kv * Hkv, D)).astype(np.float32)).reshape(n_kv, -1)
+    m = np.zeros((1, n_kv), dtype=np.float16)
+    if pattern == "holes":
+        m[0, rng.random(n_kv) < 0.3] = -np.inf
+    elif pattern == "sparse":
+        m[0, rng.random(n_kv) < 0.9] = -np.inf
+        m[0, -1] = 0
+    out = K.flash_attn(q, k, v, m.view(np.uint16), kvt, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    ref = O.flash_attn(q, k, v, m.view(np.uint16), kvt, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    assert_bits(out, ref, f"flash_attn {kv} n_kv={n_kv} Hkv={Hkv} {pattern}")
+
+
 @pytest.mark.parametrize("n_kv,n_q", [(256, 1), (1024, 1), (700, 9), (512, 64)])
 def test_flash_attn_q8_0_llama_shapes_bit_exact(K, n_kv, n_q):
     """q8_0 cache at Llama-3-8B head layout (D 128, 32 / 8 heads), causal mask, vs the oracle."""

@@ -111,16 +111,21 @@ def test_soft_max(golden_dir):
     assert np.allclose(y.sum(axis=1), 1.0, atol=1e-5)
 
 
-@pytest.mark.parametrize("n_q", [1, 7])
-@pytest.mark.parametrize("kv", ["f16", "q8_0"])
-def test_flash_attn(golden_dir, n_q, kv):
+FA_KV = {"f16": O.F16, "q8_0": O.Q8_0, "q4_0": O.Q4_0}
+
+
+@pytest.mark.parametrize("tag", ["1", "7", "long"])
+@pytest.mark.parametrize("kv", sorted(FA_KV))
+def test_flash_attn(golden_dir, tag, kv):
+    """flash_attn_ext as the reference CPU backend computes it (oracle/make_golden.py gg_flash_attn):
+    prefill / decode rows over 256 positions, and a depth-1300 decode with holes and a dead tail."""
     g = load(golden_dir, "flash_attn.npz")
-    D, H, Hkv, n_kv = int(g["D"]), int(g["H"]), int(g["Hkv"]), int(g["n_kv"])
-    kvt = O.F16 if kv == "f16" else O.Q8_0
-    out = O.flash_attn(g[f"q_{n_q}"], g[f"k_{kv}_{n_q}"], g[f"v_{kv}_{n_q}"], g[f"mask_{n_q}"], kvt, D, H, Hkv, n_kv,
+    sfx = "_long" if tag == "long" else ""
+    D, H, Hkv, n_kv = int(g["D"]), int(g["H" + sfx]), int(g["Hkv" + sfx]), int(g["n_kv" + sfx])
+    out = O.flash_attn(g[f"q_{tag}"], g[f"k_{kv}_{tag}"], g[f"v_{kv}_{tag}"], g[f"mask_{tag}"], FA_KV[kv], D, H, Hkv, n_kv,
                        1.0 / np.sqrt(D))
-    ref = g[f"out_{kv}_{n_q}"]
-    # bit-exact: K.Q in the CPU's vec_dot order (AVX-512 f16 / q8_0 class chains), libm expf,
+    ref = g[f"out_{kv}_{tag}"]
+    # bit-exact: K.Q in the CPU's vec_dot order (AVX-512 f16 / q8_0 / q4_0 class chains), libm expf,
     # the FMA of ggml_vec_mad_f16 / _f32, the unfused S*ms + vs
     assert (out.view(np.uint32) == ref.view(np.uint32)).all(), np.abs(out - ref).max() / np.abs(ref).max()
 
