@@ -121,6 +121,7 @@ void exec_ctx::free_scratch() {
     fa_cnt = nullptr;
     if (tail_cnt) (void) hipFree(tail_cnt);
     tail_cnt = nullptr;
+    gemv_ffn_release(*this);
     if (rsum_buf) (void) hipFree(rsum_buf);
     rsum_buf = nullptr;
     if (kt_buf) (void) hipFree(kt_buf);
@@ -1080,6 +1081,7 @@ static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.nsite = 0;
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) i += op_compute(ex, cgraph, i);
+    gemv_ffn_flush(ex);   // a held-back gate/up whose down projection never came
     if (ex.silu_defer) {   // a deferred SILU whose MUL never came
         op_unary(ex, ex.silu_defer);
         ex.silu_defer = ex.silu_mul = nullptr;

@@ -849,6 +849,8 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             return 1;
         }
     }
+    // a held-back gate/up (chained FFN launch) goes out before any other node that computes
+    if (ctx.ffn_down && node != ctx.ffn_down && !is_view_op(node)) gemv_ffn_flush(ctx);
     const int n = ggml_graph_n_nodes(cgraph);
     switch (node->op) {
         case GGML_OP_NONE:

@@ -70,7 +70,11 @@ struct gemv_args {
     unsigned long long * kt;              // in-graph kernel timeline region (nullable)
     uint32_t wl_off;                      // one-shot kernel: LDS byte offset of the weight slices
     unsigned long long * eprof;           // engine phase counters (microbenchmark only; nullable)
+    // one-shot body in a chained launch (k_gemv_ffn): after issuing its weight DMA the workgroup
+    // waits until the FFN_SHARDS counters at dep sum to dep_n (its activation is complete)
+    const int * dep; int dep_n;
 };
+constexpr int FFN_SHARDS = 8, FFN_SHARD_STRIDE = 32;   // ints: one 128-B line per shard
 
 // the producer's partial sums: no-return f64 atomics serialize per 128-B line at the memory
 // side (MI355X_MICROARCH.md dequeue row), so 64 shards, one line each, keep each line's count
@@ -83,6 +87,8 @@ __device__ __forceinline__ float4 ld_wt4(const float * p) { return make_float4(l
 
 // tail 2, one wave per finished Q8_K block: m = silu(gate) * up (ggml_vec_silu_f32's AVX-512
 // ggml_v_silu on the 16-element chunks, libm expf on the tail; vec.cpp:233), quantized
+// (WT: the quantized block write-through, read in the same launch)
+template <bool WT = false>
 __device__ __forceinline__ void tail_swiglu(const gemv_args & p, int blk, int lane) {
     const auto & t = p.tl;
     const int64_t e = 256 * (int64_t) blk + 4 * lane;
@@ -99,7 +105,7 @@ __device__ __forceinline__ void tail_swiglu(const gemv_args & p, int blk, int la
     if (t.silu_out) *(float4 *) (t.silu_out + e) = make_float4(s[0], s[1], s[2], s[3]);
     if (t.mul_out) *(float4 *) (t.mul_out + e) = make_float4(m[0], m[1], m[2], m[3]);
     const int64_t c0 = 256 * (int64_t) blk;
-    if (t.qmode == 1) q8K_wave(m, lane, t.qs + c0, t.qsum + c0 / 16, t.qd + c0 / 256);
+    if (t.qmode == 1) q8K_wave<WT>(m, lane, t.qs + c0, t.qsum + c0 / 16, t.qd + c0 / 256);
     else if (t.qmode == 2) q8_0_wave(m, lane, true, t.qs + c0, t.qd + c0 / 32, t.qsum + c0 / 32);
 }
 
@@ -469,6 +475,25 @@ __global__ __launch_bounds__(256) void k_gemv_pipe2(const gemv_args p1, const in
 // pipelining.  The norm prologue's sources are loaded before the DMAs are issued, so waiting
 // for them leaves the weight stream in flight; a Q8 activation slice is loaded after them.
 // Records, walker and epilogues are the pipelined kernel's (the same bits).
+// a chained launch's consumer: wave 0 spins (lanes 0-7 read one shard each, a few hundred
+// cycles apart: thousands of waiting workgroups polling the same lines would crowd out the
+// producers' own atomics) until the producers' shards sum to n; the other waves wait at the
+// barrier.  The producers wrote their outputs write-through before adding, and nothing in this
+// launch read those bytes before, so plain loads after this see them.
+__device__ __forceinline__ void os_dep_wait(const int * dep, int n) {
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < WAVE) {
+        for (int it = 0;; ++it) {
+            int v = lane < FFN_SHARDS ? __hip_atomic_load(dep + FFN_SHARD_STRIDE * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            v = __builtin_amdgcn_readfirstlane(wave_sum(v));
+            if (v >= n) break;
+            if (it > (1 << 22)) __builtin_trap();   // a producer never reported: fail loudly, not hang
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    __syncthreads();
+}
+
 template <class T> struct os_geo {
     static constexpr int SEG = (WAVE / T::per_block) * T::blk_bytes;   // a wave's row slice
     static constexpr int NI = (SEG + 1023) / 1024;                        // DMA instructions per slice
@@ -516,6 +541,7 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
             }
         }
     }
+    if (p.dep) os_dep_wait(p.dep, p.dep_n);
     // the activation slice after the DMAs: T::load computes on what it loads (bsum pairs, the
     // Q6_K -32 sums), and a wait for a load issued BEFORE the DMAs would hold the DMA issue back
     // by an L2 round trip (the one-shot kernel's rec stage took ~35 % longer that way)
@@ -560,6 +586,8 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
                         const float xv = __fadd_rn(v, rc);
                         p.rxsum[row0 + wr] = xv;
                         rc = xv;
+                    } else if (p.tl.kind) {   // the SwiGLU tail reads it back: write-through
+                        __hip_atomic_store(p.dst[mi] + row0 + wr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } else {
                         p.dst[mi][row0 + wr] = v;
                     }
@@ -570,6 +598,17 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
         }
     }
     if constexpr (MODE == 0) {
+        // the workgroup's row group reports on its Q8_K block's counter (stores drained first, a
+        // no-return add: no round trip before the workgroup retires); the block's tail workgroup
+        // (k_gemv_os past the row groups) runs SILU(gate) * up and its quantization
+        if (p.tl.kind) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int blk = (int) ((g - p.blk0[mi]) * RPG / 256);
+                __hip_atomic_fetch_add(p.tl.cnt + blk * TAIL_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         if (p.rres) {
             // this workgroup's rows' sum of squares (walker lanes hold x) to its shard (no-return atomic)
             __shared__ double rpart[RPG];
@@ -593,13 +632,62 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     }
 }
 
+// a SwiGLU tail workgroup (one per Q8_K block, after every row group in dispatch order, so every
+// producer it waits for is already resident or done): wave 0 waits until the block's gate and up
+// row groups have all reported, re-arms the counter and runs the block's tail
+// done (k_gemv_ffn): the block is quantized write-through and reported on done's shards
+__device__ __forceinline__ void os_tail_block(const gemv_args & p, int blk, int per, int * done = nullptr) {
+    if (threadIdx.x >= WAVE) return;
+    int * c = p.tl.cnt + blk * TAIL_STRIDE;
+    for (int it = 0;; ++it) {
+        const int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (v >= per) break;
+        if (it > (1 << 24)) __builtin_trap();   // a producer never reported: fail loudly, not hang
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done) {
+        tail_swiglu<true>(p, blk, threadIdx.x);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_add(done + FFN_SHARD_STRIDE * (blk % FFN_SHARDS), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        tail_swiglu(p, blk, threadIdx.x);
+    }
+}
+
 template <class T, int R, int WPR, int MODE, bool PRO>
 __global__ __launch_bounds__(256) void k_gemv_os(const gemv_args p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
+    if (MODE == 0 && p.tl.kind && (int64_t) blockIdx.x >= p.blk0[GEMV_MAXMAT]) {
+        constexpr int RPG = (4 / WPR) * R;
+        os_tail_block(p, (int) (blockIdx.x - p.blk0[GEMV_MAXMAT]), 2 * (256 / RPG));
+        return;
+    }
     kt_enter(p.kt);
     // dynamic LDS: [records RPG x nb x RS dwords | prologue activation | weight slices]
     gemv_os_body<T, R, WPR, MODE, PRO>(p, blockIdx.x, (uint8_t *) xr + p.wl_off, xr);
     kt_exit(p.kt);
+}
+
+// ---- chained FFN launch (k_gemv_ffn) ---------------------------------------------------------------
+// The decode FFN of one layer, gate/up -> SILU * MUL -> down, as ONE grid in dispatch order:
+//   [gate/up row groups | one SwiGLU tail workgroup per Q8_K block | down row groups]
+// Each part is the one-shot body (the same records, walkers and bits as separate launches).  A tail
+// workgroup waits for its block's gate and up row groups, quantizes the block write-through and
+// reports on the done shards; a down workgroup issues its weight DMA FIRST and only then waits for
+// all tails, so the down weights stream in while the gate/up stragglers and the tails finish (the
+// separate launches paid the gate/up tail, a product kernel and the down ramp in series).  Every
+// workgroup waits only for workgroups dispatched before it, so the grid cannot deadlock.
+template <class T1, int R1, int WPR1, class T2, int R2, int WPR2>
+__global__ __launch_bounds__(256) void k_gemv_ffn(const gemv_args p1, const gemv_args p2, int * done) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
+    kt_enter(p1.kt);
+    const int64_t ng1 = p1.blk0[GEMV_MAXMAT], nt = p1.tl.n / 256, b = blockIdx.x;
+    if (b < ng1) gemv_os_body<T1, R1, WPR1, 0, false>(p1, b, (uint8_t *) xr + p1.wl_off, xr);
+    else if (b < ng1 + nt) os_tail_block(p1, (int) (b - ng1), 2 * (256 / ((4 / WPR1) * R1)), done);
+    else gemv_os_body<T2, R2, WPR2, 0, false>(p2, b - ng1 - nt, (uint8_t *) xr + p2.wl_off, xr);
+    kt_exit(p1.kt);
 }
 
 template <class T1, class T2, int R2, int WPR, bool PRO, int R1 = 2>
@@ -1207,9 +1295,16 @@ static void launch_os_m(hipStream_t st, gemv_args & a, int nmat) {
     const int64_t ng = set_groups(a, nmat, RPG);
     const size_t lds = os_lds_layout<T, R, WPR>(a);
     a.kt = g_kt_ctx ? g_kt_ctx->kt_take(gemv_kt_name(a, MODE), (unsigned) ng, 256) : nullptr;
+    // SwiGLU tail: one more workgroup per Q8_K block of the product, after the row groups
+    int64_t grid = ng;
+    if (a.tl.kind) {
+        GGML_ASSERT(MODE == 0 && nmat == 2 && a.tl.n % 256 == 0 && 256 % RPG == 0 && a.blk0[GEMV_MAXMAT] == ng);
+        GGML_ASSERT(a.M[0] == a.tl.n && a.M[1] == a.tl.n);
+        grid += a.tl.n / 256;
+    }
 #define OS_LAUNCH(P)                                                                                              \
-    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P>), dim3((unsigned) ng), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a); \
-    else hipLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P>), dim3((unsigned) ng), dim3(256), lds, st, a)
+    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P>), dim3((unsigned) grid), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a); \
+    else hipLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P>), dim3((unsigned) grid), dim3(256), lds, st, a)
     if (a.pro.x) { OS_LAUNCH(true); } else { OS_LAUNCH(false); }
 #undef OS_LAUNCH
 }
@@ -1225,7 +1320,8 @@ static void launch_os(hipStream_t st, gemv_args & a, int nmat) {
 // per workgroup (fewer workgroups form it)
 template <class T>
 static bool launch_os_t(hipStream_t st, gemv_args & a, int nmat) {
-    if (!os_enabled() || a.tl.kind || !os_aligned<T>(a, nmat)) return false;
+    if (!os_enabled() || !os_aligned<T>(a, nmat)) return false;
+    if (a.tl.kind && needs_epilogue(a, nmat)) return false;
     const int wpr = wpr_of(a.ntasks);
     int R = 1;
     if (a.pro.x || (wpr == 4 && !std::is_same<T, g_q6_K>::value)) R = 2;
@@ -1509,11 +1605,119 @@ bool gemv_supported(const ggml_tensor * mm) {
 
 bool gemv_epilogue_ok(const ggml_tensor * mm) { return gemv_supported(mm); }
 
+// ---- chained FFN launch (host) ------------------------------------------------------------------
+// GGML_MI355X_FFN=1: gate/up with a SwiGLU tail is held back until its down projection arrives,
+// then both go out as one k_gemv_ffn grid (any other node in between launches it alone first)
+static bool ffn_enabled() {
+    static const bool on = getenv("GGML_MI355X_FFN") && atoi(getenv("GGML_MI355X_FFN")) != 0;
+    return on;
+}
+
+struct ffn_state {
+    gemv_args a1;
+    int n1 = 0;
+    ggml_type t1 = GGML_TYPE_COUNT;
+};
+
+static ffn_state & ffn_of(exec_ctx & ctx) {
+    if (!ctx.ffn) ctx.ffn = new ffn_state();
+    return *(ffn_state *) ctx.ffn;
+}
+
+void gemv_ffn_release(exec_ctx & ctx) {
+    delete (ffn_state *) ctx.ffn;
+    ctx.ffn = nullptr;
+    ctx.ffn_down = nullptr;
+}
+
+static void launch_by_type(hipStream_t st, ggml_type t, gemv_args & a, int nmat) {
+    switch (t) {
+        case GGML_TYPE_Q4_K: launch_t<g_q4_K>(st, a, nmat); break;
+        case GGML_TYPE_Q5_K: launch_t<g_q5_K>(st, a, nmat); break;
+        case GGML_TYPE_Q6_K: launch_t<g_q6_K>(st, a, nmat); break;
+        case GGML_TYPE_Q8_0: launch_t<g_q8_0>(st, a, nmat); break;
+        case GGML_TYPE_Q4_0: launch_t<g_q4_0>(st, a, nmat); break;
+        default: GGML_ABORT("mi355x: gemv type");
+    }
+}
+
+// the held-back gate/up goes out alone (something other than its down projection comes next)
+void gemv_ffn_flush(exec_ctx & ctx) {
+    if (!ctx.ffn_down) return;
+    ffn_state & f = ffn_of(ctx);
+    ctx.ffn_down = nullptr;
+    g_kt_ctx = ctx.kt_buf && ktrace_enabled() ? &ctx : nullptr;
+    launch_by_type(ctx.stream, f.t1, f.a1, f.n1);
+    g_kt_ctx = nullptr;
+}
+
+// the one-shot geometry rule of launch_os_t (no prologue): rows per wave and waves per row
+template <class T>
+static void os_rule(const gemv_args & a, int & R, int & wpr) {
+    wpr = wpr_of(a.ntasks);
+    R = (wpr == 4 && !std::is_same<T, g_q6_K>::value) ? 2 : 1;
+}
+
+template <class T1, int R1, int WPR1, class T2, int R2, int WPR2>
+static bool launch_ffn_v(exec_ctx & ctx, gemv_args & a1, int n1, gemv_args & a2, int * done) {
+    constexpr int RPG1 = (4 / WPR1) * R1, RPG2 = (4 / WPR2) * R2;
+    const int64_t ng1 = set_groups(a1, n1, RPG1), ng2 = set_groups(a2, 1, RPG2);
+    if (256 % RPG1 != 0 || a1.M[0] != a1.tl.n || a1.M[1] != a1.tl.n) return false;
+    const size_t l1 = os_lds_layout<T1, R1, WPR1>(a1), l2 = os_lds_layout<T2, R2, WPR2>(a2);
+    const size_t lds = std::max(l1, l2);
+    if (lds > 64 * 1024) return false;
+    const int64_t nt = a1.tl.n / 256;
+    a2.dep = done;
+    a2.dep_n = (int) nt;
+    const int64_t grid = ng1 + nt + ng2;
+    a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("ffn", (unsigned) grid, 256) : nullptr;
+    a2.kt = nullptr;
+    if (a1.kt) {
+        // the timeline shows the three parts as their own rows (one region, three ranges)
+        const auto l = g_kt_ctx->kt_list.back();
+        g_kt_ctx->kt_list.pop_back();
+        g_kt_ctx->kt_list.push_back({"ffn:gate_up", l.off, (unsigned) ng1, l.stride});
+        g_kt_ctx->kt_list.push_back({"ffn:tail", l.off + (size_t) ng1 * l.stride, (unsigned) nt, l.stride});
+        g_kt_ctx->kt_list.push_back({"ffn:down", l.off + (size_t) (ng1 + nt) * l.stride, (unsigned) ng2, l.stride});
+    }
+    hipLaunchKernelGGL((k_gemv_ffn<T1, R1, WPR1, T2, R2, WPR2>), dim3((unsigned) grid), dim3(256), lds, ctx.stream, a1, a2, done);
+    return true;
+}
+
+// gate/up (Q4_K, one row per wave) with a Q4_K / Q6_K down projection at K <= 256 tasks
+static bool launch_ffn(exec_ctx & ctx, ffn_state & f, ggml_type t2, gemv_args & a2) {
+    if (f.t1 != GGML_TYPE_Q4_K || f.n1 != 2 || !os_enabled() || a2.tl.kind || a2.pro.x || needs_epilogue(a2, 1) ||
+        needs_epilogue(f.a1, 2) || f.a1.tl.qmode != 1) return false;
+    if (!os_aligned<g_q4_K>(f.a1, 2)) return false;
+    int R1, W1, R2, W2;
+    os_rule<g_q4_K>(f.a1, R1, W1);
+    if (R1 != 1 || W1 != 1) return false;
+    int * done = (int *) gemv_rsum_site(ctx);   // zeroed per graph (run_nodes)
+    if (!done) return false;
+    gemv_args a1 = f.a1;
+    if (t2 == GGML_TYPE_Q4_K) {
+        // one row per workgroup here (not the stand-alone launch's two): the grid's dynamic LDS is
+        // the larger part's, and two-row down groups (31 KB) would cut the gate/up part from
+        // eight resident workgroups per CU to five
+        os_rule<g_q4_K>(a2, R2, W2);
+        if (!os_aligned<g_q4_K>(a2, 1) || W2 != 4) return false;
+        return launch_ffn_v<g_q4_K, 1, 1, g_q4_K, 1, 4>(ctx, a1, 2, a2, done);
+    }
+    if (t2 == GGML_TYPE_Q6_K) {
+        os_rule<g_q6_K>(a2, R2, W2);
+        if (!os_aligned<g_q6_K>(a2, 1) || R2 != 1 || W2 != 4) return false;
+        return launch_ffn_v<g_q4_K, 1, 1, g_q6_K, 1, 4>(ctx, a1, 2, a2, done);
+    }
+    return false;
+}
+
 // one launch for up to three MUL_MATs sharing src1 (all gemv_supported, same K; a second
 // K-quant type joins as the second body of k_gemv_pipe2)
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi) {
     GGML_ASSERT(nmat >= 1 && nmat <= GEMV_MAXMAT);
     gemv_init();
+    const bool ffn_down = ctx.ffn_down && nmat == 1 && mms[0] == ctx.ffn_down;
+    if (ctx.ffn_down && !ffn_down) gemv_ffn_flush(ctx);
     g_kt_ctx = ctx.kt_buf && ktrace_enabled() ? &ctx : nullptr;
     const ggml_tensor * src1 = mms[0]->src[1];
     const ggml_type wt = mms[0]->src[0]->type;
@@ -1642,6 +1846,24 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
             }
             one(wt2, a2, n2);
         }
+    } else if (ffn_down) {
+        // the held-back gate/up and this down projection as one chained grid, else one by one
+        ctx.ffn_down = nullptr;
+        a.ntasks = (int) (nblk * (kq ? 4 : 1));
+        if (!launch_ffn(ctx, ffn_of(ctx), wt, a)) {
+            ffn_state & f = ffn_of(ctx);
+            launch_by_type(ctx.stream, f.t1, f.a1, f.n1);
+            one(wt, a, nmat);
+        }
+    } else if (a.tl.kind && a.tl.qmode == 1 && ffn_enabled() && !ctx.timing && epi->tq_for && wt == GGML_TYPE_Q4_K &&
+               nmat == 2) {
+        // hold back: the down projection (epi->tq_for) may join this launch
+        ffn_state & f = ffn_of(ctx);
+        a.ntasks = (int) (nblk * 4);
+        f.a1 = a;
+        f.n1 = nmat;
+        f.t1 = wt;
+        ctx.ffn_down = epi->tq_for;
     } else {
         one(wt, a, nmat);
     }

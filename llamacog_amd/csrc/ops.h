@@ -59,6 +59,10 @@ struct exec_ctx {
     // SwiGLU prologue pending for the down projection that reads `key` (the MUL of silu(gate)
     // and up): its engine launch forms silu(gate) * up and the quantized activation itself, so
     // the SILU and the MUL never run as nodes (dispatch.cpp, GGML_OP_UNARY)
+    // chained FFN launch (k_gemv.hip k_gemv_ffn): the held-back gate/up's state and the down
+    // projection it waits for (nullptr: nothing held back)
+    void * ffn = nullptr;
+    const ggml_tensor * ffn_down = nullptr;
     struct swiglu_pending { const ggml_tensor * key; const void * data; const float * gate; const float * up; };
     swiglu_pending swiglu = {};
 
@@ -238,6 +242,8 @@ struct gemv_epi {
 };
 bool gemv_supported(const ggml_tensor * mm);
 bool gemv_tail_ready(exec_ctx & ctx);
+void gemv_ffn_flush(exec_ctx & ctx);     // launch a held-back gate/up alone (k_gemv.hip)
+void gemv_ffn_release(exec_ctx & ctx);
 double * gemv_rsum_site(exec_ctx & ctx);   // a zeroed site of rsum_buf, or nullptr
 bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
 bool gemv_engine_ok(const ggml_tensor * mm);     // the persistent engine (k_gemv_eng) takes this mat-vec

@@ -14,16 +14,31 @@ namespace mi355x {
 // The reductions run on DPP / readlane (common.h): max |x| as the unsigned order of the
 // non-negative floats' bits, then the lowest index holding it (== the sequential strict '>'
 // scan), whose value is read from its lane.  All 64 lanes must be active.
+// WT: every store write-through (agent-scope relaxed atomics), for a reader in the same launch
+// that waits on a counter (k_gemv_ffn's down projection); bsums then go two to a dword
+template <bool WT = false>
 __device__ __forceinline__ void q8K_wave(const float (&vv)[4], int lane, int8_t * q, int16_t * bsum, float * d) {
+    auto st32 = [](void * p, uint32_t v) {
+        if constexpr (WT) __hip_atomic_store((uint32_t *) p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else *(uint32_t *) p = v;
+    };
+    auto stbs = [&](int s) {   // bsum[lane / 4] = s for lanes 4k
+        if constexpr (WT) {
+            const int hi = __shfl_down(s, 4, WAVE);
+            if ((lane & 7) == 0) st32(bsum + (lane >> 2), ((uint32_t) (uint16_t) (int16_t) s) | ((uint32_t) (uint16_t) (int16_t) hi << 16));
+        } else {
+            if ((lane & 3) == 0) bsum[lane >> 2] = (int16_t) s;
+        }
+    };
     float la = 0.0f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) la = fmaxf(la, fabsf(vv[k]));
     const uint32_t abits = wave_umax(__float_as_uint(la));
     const float amax = __uint_as_float(abits);
     if (amax == 0.0f) {
-        *(uint32_t *) (q + 4 * lane) = 0;
-        if (lane < 16) bsum[lane] = 0;
-        if (lane == 0) *d = 0.0f;
+        st32(q + 4 * lane, 0);
+        stbs(0);
+        if (lane == 0) st32(d, 0u);
         return;
     }
     uint32_t cand = 0xffffffffu;
@@ -43,10 +58,10 @@ __device__ __forceinline__ void q8K_wave(const float (&vv)[4], int lane, int8_t 
         s += iv;
         packed |= (uint32_t) (iv & 0xff) << (8 * k);
     }
-    *(uint32_t *) (q + 4 * lane) = packed;
+    st32(q + 4 * lane, packed);
     s = quad_sum(s);
-    if ((lane & 3) == 0) bsum[lane >> 2] = (int16_t) s;
-    if (lane == 0) *d = 1.0f / iscale;
+    stbs(s);
+    if (lane == 0) st32(d, __float_as_uint(1.0f / iscale));
 }
 
 // The same Q8_K block over 16 lanes (a DPP row), lane j = lane & 15 holding elements

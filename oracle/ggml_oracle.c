@@ -197,6 +197,28 @@ void orc_quantize_row_q8_0(const float * x, void * vy, int64_t k) {
     }
 }
 
+/* quantize_row_q4_0_ref, ggml-quants.c:25-60 (the CPU's from_float for a q4_0 KV cache): d = the
+ * signed value of largest magnitude / -8, nibbles MIN(15, (int8_t)(x * id + 8.5f)) */
+void orc_quantize_row_q4_0(const float * x, void * vy, int64_t k) {
+    b_q4_0 * y = (b_q4_0 *) vy;
+    for (int64_t i = 0; i < k / 32; i++) {
+        float amax = 0.0f, mx = 0.0f;
+        for (int j = 0; j < 32; j++) {
+            const float v = x[i * 32 + j];
+            if (amax < fabsf(v)) { amax = fabsf(v); mx = v; }
+        }
+        const float d = mx / -8;
+        const float id = d ? 1.0f / d : 0.0f;
+        y[i].d = orc_fp32_to_fp16(d);
+        for (int j = 0; j < 16; ++j) {
+            const float x0 = x[i * 32 + j] * id, x1 = x[i * 32 + 16 + j] * id;
+            const int8_t a0 = (int8_t) (x0 + 8.5f), a1 = (int8_t) (x1 + 8.5f);
+            const uint8_t xi0 = a0 < 15 ? (uint8_t) a0 : 15, xi1 = a1 < 15 ? (uint8_t) a1 : 15;
+            y[i].qs[j] = xi0 | (uint8_t) (xi1 << 4);
+        }
+    }
+}
+
 /* get_scale_min_k4, ggml-quants.c:625-633 */
 static inline void get_scale_min_k4(int j, const uint8_t * q, uint8_t * d, uint8_t * m) {
     if (j < 4) {

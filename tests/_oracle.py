@@ -33,6 +33,7 @@ def lib():
         L.orc_fp32_to_fp16.restype = ctypes.c_uint16
         L.orc_quantize_row_q8_K.argtypes = [P, P, I64]
         L.orc_quantize_row_q8_0.argtypes = [P, P, I64]
+        L.orc_quantize_row_q4_0.argtypes = [P, P, I64]
         L.orc_dequantize_row.argtypes = [ctypes.c_int, P, P, I64]
         L.orc_vec_dot.argtypes = [ctypes.c_int, I64, P, P, P, P]
         L.orc_vec_dot.restype = ctypes.c_float
@@ -58,10 +59,11 @@ def nbytes(t, n):
 
 
 def quantize_rows(t, x):
-    """Q8_K / Q8_0 activation quantization of each row (CPU from_float semantics)."""
+    """Q8_K / Q8_0 / Q4_0 quantization of each row (CPU from_float semantics)."""
+    assert t in (Q8_K, Q8_0, Q4_0), t
     x = np.ascontiguousarray(x, dtype=np.float32)
     out = np.zeros((x.shape[0], nbytes(t, x.shape[1])), dtype=np.uint8)
-    f = lib().orc_quantize_row_q8_K if t == Q8_K else lib().orc_quantize_row_q8_0
+    f = {Q8_K: lib().orc_quantize_row_q8_K, Q8_0: lib().orc_quantize_row_q8_0, Q4_0: lib().orc_quantize_row_q4_0}[t]
     for r in range(x.shape[0]):
         f(ptr(x[r]), ptr(out[r]), x.shape[1])
     return out

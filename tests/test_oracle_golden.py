@@ -43,6 +43,13 @@ def test_q8_0_activation_quantizer_bit_exact(golden_dir):
     assert (got == g["q8_0"]).all(), "Q8_0 blocks differ from the x86 quantize_row_q8_0"
 
 
+def test_q4_0_quantizer_bit_exact(golden_dir):
+    """quantize_row_q4_0_ref (a q4_0 KV cache's from_float) vs the reference's own q4_0 blocks"""
+    g = load(golden_dir, "mul_mat_q4_0.npz")
+    got = O.quantize_rows(O.Q4_0, g["w"])
+    assert (got == g["wq"]).all(), "Q4_0 blocks differ from quantize_row_q4_0_ref"
+
+
 @pytest.mark.parametrize("name", ["q4_0", "q8_0", "q4_K", "q5_K", "q6_K"])
 def test_dequantize_bit_exact(golden_dir, name):
     g = load(golden_dir, f"mul_mat_{name}.npz")
