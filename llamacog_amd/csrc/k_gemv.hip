@@ -568,8 +568,13 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     // ---- this wave's weights are in LDS (the issuing wave's vmcnt covers its own DMAs) ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t * xb = xr;
+#ifndef MI_EXP
+#define MI_EXP 0
+#endif
+    // MI_EXP (time-split experiments only, wrong results): 1 no walk, 2 no records, 3 neither
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+        if (MI_EXP & 2) break;
         typename T::raw w;
         T::template fetch<typename lds_loader<T>::type>(mine + r * G::SLICE - (int64_t) wsub * G::SEG, tt, w);
         T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * nb * T::RS);
@@ -578,7 +583,7 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     else wave_lds_sync();
     __shared__ float res[MODE ? RPG : 1];
     if (wsub == 0) {
-        const float v = T::walk(xb + (size_t) (rowl0 + wrc) * nb * T::RS, nb, ws);
+        const float v = (MI_EXP & 1) ? xb[lane] * 0.5f : T::walk(xb + (size_t) (rowl0 + wrc) * nb * T::RS, nb, ws);
         if (wr < R && ws == 0) {
             if constexpr (MODE == 0) {
                 if (row0 + wr < M) {
@@ -654,6 +659,124 @@ __device__ __forceinline__ void os_tail_block(const gemv_args & p, int blk, int 
     } else {
         tail_swiglu(p, blk, threadIdx.x);
     }
+}
+
+// ---- looping one-shot body: several row groups per workgroup, weights double-buffered ----------
+// The one-shot body's per-group work (DMA -> records -> walk -> store; the same records, walker
+// and bits), but a workgroup runs groups g, g + grid, ... and issues group g + grid's weight DMA
+// into its second slice set BEFORE computing group g, so its own compute overlaps its next
+// stream and the activation is loaded once per workgroup instead of once per group (the
+// one-shot kernel moves ~9 KB per workgroup and then computes with no bytes of its own in
+// flight).  No prologue, epilogue or tail (MODE 0); the residual producer accumulates its sum
+// of squares over the workgroup's groups and adds it once.
+template <class T, int R, int WPR>
+__device__ __forceinline__ void os_issue(const gemv_args & p, int64_t g, uint8_t * mine, int wave, int lane) {
+    using G = os_geo<T>;
+    constexpr int RPG = (4 / WPR) * R;
+    const int wsub = wave % WPR;
+    const int rowl0 = (wave / WPR) * R;
+    const int mi = gemv_mat(p, g);
+    const int64_t row0 = (g - p.blk0[mi]) * RPG + rowl0;
+    const int64_t M = p.M[mi];
+    const int nt_w = min(WAVE, p.ntasks - WAVE * wsub);
+    const int seg = (nt_w / T::per_block) * T::blk_bytes;
+    const uint8_t * Wm = p.W[mi];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint8_t * src = Wm + min(row0 + r, M - 1) * p.nb01[mi] + (int64_t) wsub * G::SEG;
+#pragma unroll
+        for (int i = 0; i < G::NI; ++i) {
+            const int off = min(i * 1024 + 16 * lane, seg - 16);
+            __builtin_amdgcn_global_load_lds((const void *) (src + off), (gemv_lds_t) (mine + r * G::SLICE + i * 1024), 16, 0,
+                                             MI_WNT ? 2 : 0);
+        }
+    }
+}
+
+template <class T, int R, int WPR>
+__global__ __launch_bounds__(256) void k_gemv_osl(const gemv_args p) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
+    kt_enter(p.kt);
+    constexpr int RPG = (4 / WPR) * R;
+    using G = os_geo<T>;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wsub = wave % WPR;
+    const int t = wsub * WAVE + lane;
+    const bool active = t < p.ntasks;
+    const int tt = active ? t : 0;
+    const int nb = p.ntasks / T::per_block;
+    const int rowl0 = (wave / WPR) * R;
+    const int wr = lane / T::LPR, ws = lane % T::LPR;
+    const int wrc = wr < R ? wr : 0;
+    const int64_t ng = p.blk0[GEMV_MAXMAT], grid = gridDim.x;
+    uint8_t * wl = (uint8_t *) xr + p.wl_off;
+    uint8_t * buf[2] = {wl + (size_t) wave * 2 * R * G::SLICE, wl + (size_t) wave * 2 * R * G::SLICE + (size_t) R * G::SLICE};
+    int64_t g = blockIdx.x;
+    os_issue<T, R, WPR>(p, g, buf[0], wave, lane);
+    typename T::act x;
+    T::load(p.A, tt, x);
+    double ss = 0.0;
+    int cur = 0;
+    for (; g < ng; g += grid) {
+        const int64_t gn = g + grid;
+        const bool more = gn < ng;   // uniform
+        if (more) os_issue<T, R, WPR>(p, gn, buf[cur ^ 1], wave, lane);
+        const int mi = gemv_mat(p, g);
+        const int64_t row0 = (g - p.blk0[mi]) * RPG + rowl0;
+        const int64_t M = p.M[mi];
+        float rc = 0.0f;
+        if (p.rres) rc = p.rres[min(row0 + wrc, p.M[0] - 1)];
+        // this group's weights have landed (the next group's DMA may still be in flight)
+        if (more) {
+            if constexpr (G::NI * R == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+            else if constexpr (G::NI * R == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else if constexpr (G::NI * R == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            else if constexpr (G::NI * R == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if constexpr (G::NI * R == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if constexpr (G::NI * R == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        uint32_t * xb = xr;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            typename T::raw w;
+            T::template fetch<typename lds_loader<T>::type>(buf[cur] + r * G::SLICE - (int64_t) wsub * G::SEG, tt, w);
+            T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * nb * T::RS);
+        }
+        if constexpr (WPR > 1) __syncthreads();
+        else wave_lds_sync();
+        if (wsub == 0) {
+            const float v = T::walk(xb + (size_t) (rowl0 + wrc) * nb * T::RS, nb, ws);
+            if (wr < R && ws == 0 && row0 + wr < M) {
+                if (p.rres) {   // ADD(v, res): the CPU's single f32 add
+                    const float xv = __fadd_rn(v, rc);
+                    p.rxsum[row0 + wr] = xv;
+                    ss = __dadd_rn(ss, (double) __fmul_rn(xv, xv));
+                } else {
+                    p.dst[mi][row0 + wr] = v;
+                }
+            }
+        }
+        // the records are rewritten by the next group: every wave's walk is done with them
+        if constexpr (WPR > 1) __syncthreads();
+        else wave_lds_sync();
+        cur ^= 1;
+    }
+    if (p.rres) {
+        // this workgroup's rows' sum of squares (walker lanes hold partials) to its shard
+        __shared__ double rpart[RPG];
+        if (wsub == 0 && wr < R && ws == 0) rpart[rowl0 + wr] = ss;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double tot = 0.0;
+#pragma unroll
+            for (int k = 0; k < RPG; ++k) tot = __dadd_rn(tot, rpart[k]);
+            __hip_atomic_fetch_add(p.rsum + RSUM_STRIDE * (blockIdx.x % RSUM_SHARDS), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    kt_exit(p.kt);
 }
 
 template <class T, int R, int WPR, int MODE, bool PRO>
@@ -1309,8 +1432,30 @@ static void launch_os_m(hipStream_t st, gemv_args & a, int nmat) {
 #undef OS_LAUNCH
 }
 
+// GGML_MI355X_OSL = workgroups per CU of the looping one-shot kernel (0: off, the default)
+static int osl_per_cu() {
+    static const int v = getenv("GGML_MI355X_OSL") ? atoi(getenv("GGML_MI355X_OSL")) : 0;
+    return v;
+}
+
+template <class T, int R, int WPR>
+static bool launch_osl(hipStream_t st, gemv_args & a, int nmat) {
+    constexpr int RPG = (4 / WPR) * R;
+    const int64_t ng = set_groups(a, nmat, RPG);
+    const size_t rec = r16((size_t) RPG * (a.ntasks / T::per_block) * T::RS * 4);
+    a.wl_off = (uint32_t) rec;
+    const size_t lds = rec + (size_t) 4 * 2 * R * os_geo<T>::SLICE;
+    if (lds > 64 * 1024) return false;
+    const int64_t grid = std::min<int64_t>(ng, (int64_t) osl_per_cu() * g_num_cu);
+    a.kt = g_kt_ctx ? g_kt_ctx->kt_take(a.rres ? "gemvl+resid" : "gemvl", (unsigned) grid, 256) : nullptr;
+    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_osl<T, R, WPR>), dim3((unsigned) grid), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a);
+    else hipLaunchKernelGGL((k_gemv_osl<T, R, WPR>), dim3((unsigned) grid), dim3(256), lds, st, a);
+    return true;
+}
+
 template <class T, int R, int WPR>
 static void launch_os(hipStream_t st, gemv_args & a, int nmat) {
+    if (osl_per_cu() > 0 && !needs_epilogue(a, nmat) && !a.pro.x && !a.tl.kind && launch_osl<T, R, WPR>(st, a, nmat)) return;
     if (needs_epilogue(a, nmat)) launch_os_m<T, R, WPR, 1>(st, a, nmat);
     else launch_os_m<T, R, WPR, 0>(st, a, nmat);
 }

@@ -48,9 +48,20 @@ __device__ __forceinline__ float hsum8_lanes(float v) {
 
 // class chains: lane s of the group walks acc = fma(f, cls[s], acc) over nb records of RS
 // dwords (classes at dwords 0..7, the scale product at dword fo)
+// (records are read eight blocks at a time ahead of their FMAs: the chain then waits on one LDS
+// round trip per eight blocks, not per block)
 __device__ __forceinline__ float class_chain(const uint32_t * rr, int nb, int RS, int fo, int s) {
     float acc = 0.0f;
-    for (int b = 0; b < nb; ++b) acc = fmaf(asf(rr[b * RS + fo]), (float) (int) rr[b * RS + s], acc);
+    int b = 0;
+    for (; b + 8 <= nb; b += 8) {
+        float f[8];
+        int c[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { f[k] = asf(rr[(b + k) * RS + fo]); c[k] = (int) rr[(b + k) * RS + s]; }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = fmaf(f[k], (float) c[k], acc);
+    }
+    for (; b < nb; ++b) acc = fmaf(asf(rr[b * RS + fo]), (float) (int) rr[b * RS + s], acc);
     return acc;
 }
 
@@ -198,7 +209,18 @@ struct g_q4_K {
     }
     __device__ static float walk(const uint32_t * rr, int nb, int) {
         float A = 0.0f, B = 0.0f;
-        for (int b = 0; b < nb; ++b) {
+        int b = 0;
+        for (; b + 8 <= nb; b += 8) {   // eight records in flight ahead of their FMAs
+            uint4 r[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r[k] = *(const uint4 *) (rr + (b + k) * RS);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                A = fmaf((float) (int) r[k].x, asf(r[k].z), A);
+                B = fmaf((float) (int) r[k].y, asf(r[k].w), B);
+            }
+        }
+        for (; b < nb; ++b) {
             const uint4 r = *(const uint4 *) (rr + b * RS);
             A = fmaf((float) (int) r.x, asf(r.z), A);
             B = fmaf((float) (int) r.y, asf(r.w), B);
