@@ -1359,7 +1359,6 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
 // its chain waves run the recurrence while its stager waves stream the next V chunk into LDS.
 // The arithmetic of every step is k_fattn_exact's (the CPU's ops.cpp:7015-7232), so the bits are.
 constexpr int FAL_PB = 256;       // positions per scores workgroup
-constexpr int FAL_THREADS = 384;   // chain: waves 0-1 the recurrence, 2-5 stage V (0-3 the coefficients)
 constexpr int FAL_NMAX = 6144;    // positions the chain's coefficient arrays hold
 constexpr int FAL_GMAX = 8;       // query heads per KV head (GQA) the scores kernel takes
 constexpr int FAL_U = 8;          // chain batch
@@ -1479,9 +1478,9 @@ __global__ __launch_bounds__(256) void k_fal_scores(const fa_args a, float * __r
 
 // LDS of the chain kernel
 template <int VT> struct fal_smem {
-    static constexpr int D = 128, NB = D / 32;
+    static constexpr int D = 128, DH = D / FAL_DSPLIT, NBH = DH / 32;   // a workgroup's dims
     static constexpr int CV = 128;                        // V positions per stage
-    static constexpr int RB = VT == 0 ? 2 * D : (VT == 1 ? 34 * NB : 18 * NB);   // bytes per V row (raw)
+    static constexpr int RB = VT == 0 ? 2 * DH : (VT == 1 ? 34 * NBH : 18 * NBH);   // bytes of a row's half (raw)
     static constexpr int NSTG = 3;                        // stages: chunks c + 1 and c + 2 in flight
     float cm[FAL_NMAX + 2 * FAL_U];             // ms coefficient (1 where dead)
     float sc[FAL_NMAX + 2 * FAL_U];             // vs coefficient (0 where dead)
@@ -1489,8 +1488,9 @@ template <int VT> struct fal_smem {
     uint8_t gb[FAL_NMAX / 64 + 4];              // per 64 positions: its 8 batches taking the general step
     float wmax[4];
     int wlast[4];
-    float ol[128];
-    // V rows exactly as in the cache (f16, or q8_0 / q4_0 blocks), packed, by LDS-DMA
+    float ol[64];
+    // the workgroup's half of each V row exactly as in the cache (f16, or q8_0 / q4_0 blocks),
+    // packed, by LDS-DMA
     __attribute__((aligned(16))) uint8_t vr[NSTG][CV * RB + 64];
 };
 
@@ -1500,40 +1500,37 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     constexpr int D = 128, NB = D / 32, CV = SM::CV, U = FAL_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     kt_enter(a.kt);
-    const int64_t h = blockIdx.x, iq3 = blockIdx.y;
+    // FAL_DSPLIT workgroups per head, each the recurrence of DH of its dims: V is staged through
+    // the CU's LDS-DMA at ~25 GB/s per CU (MI355X_MICROARCH.md ldsdma-fill), so one CU per head
+    // spent most of the chain waiting for its V stages; the split halves every CU's bytes while
+    // each keeps a whole chain of its own (the dims' recurrences are independent; the
+    // coefficients are formed by every workgroup of the head alike)
+    const int64_t h = blockIdx.x / FAL_DSPLIT, dh = blockIdx.x % FAL_DSPLIT, iq3 = blockIdx.y;
     const int64_t hk = h / (a.H / a.Hkv);
     __shared__ __attribute__((aligned(16))) SM sm;
-    const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
+    constexpr int RB = SM::RB, NSTG = SM::NSTG, DH = SM::DH;
+    const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3 + dh * RB;
     const char * mrow = a.mask;
     const float * srow = sco + (iq3 * a.H + h) * a.n_kv;
 
-    // ---- stage V rows [c0, c0 + n) into buffer st by LDS-DMA: waves 2-5, every row as it is in
-    // the cache.  Rows back to back in the cache (one KV head) are one contiguous byte range: 1 KiB
-    // per instruction.  Otherwise (the llama view: a position's heads interleaved) f16 rows go 4 to
-    // an instruction and q8_0 / q4_0 rows (136 / 72 B, not 16-B granular) a dword a lane: per wave
-    // and chunk of 128 at most 17 instructions, so two chunks in flight stay within vmcnt's 63.
-    // Returns this wave's instruction count (its vmcnt share of the stage).
-    constexpr int RB = SM::RB, NSTG = SM::NSTG;
-    const bool contig = a.nbv1 == RB && ((uintptr_t) vbase & 15) == 0;
+    // ---- stage this half of V rows [c0, c0 + n) into buffer st by LDS-DMA: waves 1-3.  f16
+    // halves (128 B) go 8 to an instruction; q8_0 / q4_0 halves (68 / 36 B, not 16-B granular) a
+    // dword a lane: per wave and chunk of 128 at most 12 instructions, so two chunks in flight
+    // stay within vmcnt's 63.  Returns this wave's instruction count (its vmcnt share).
     auto stage = [&](int st, int64_t c0, int n) -> int {
-        const int t = tid - 128, sw = t >> 6;   // stager wave 0..3
+        const int t = tid - 64, sw = t >> 6;   // stager wave 0..2
         uint8_t * dst = sm.vr[st];
         int cnt = 0;
-        if (contig) {
-            const char * src = vbase + c0 * RB;
-            const int nbytes = n * RB;
-            for (int q = sw; 1024 * q < nbytes; q += 4, ++cnt)
-                lds_dma16(src + min(1024 * q + 16 * (t & 63), nbytes - 16), dst + 1024 * q);
-        } else if constexpr (VT == 0) {
-            const int r_in = (t & 63) >> 4, col = t & 15;
-            for (int q = sw; 4 * q < n; q += 4, ++cnt) {
-                const int row = min(4 * q + r_in, n - 1);
+        if constexpr (VT == 0) {
+            const int r_in = (t & 63) >> 3, col = t & 7;
+            for (int q = sw; 8 * q < n; q += 3, ++cnt) {
+                const int row = min(8 * q + r_in, n - 1);
                 lds_dma16(vbase + (c0 + row) * a.nbv1 + 16 * col, dst + 1024 * q);
             }
         } else {
             constexpr int DW = RB / 4;   // dword i of the stage = row i / DW, dword i % DW
             const int ndw = n * DW;
-            for (int q = sw; 64 * q < ndw; q += 4, ++cnt) {
+            for (int q = sw; 64 * q < ndw; q += 3, ++cnt) {
                 const int i = min(64 * q + (t & 63), ndw - 1), row = i / DW, w = i % DW;
                 lds_dma4(vbase + (c0 + row) * a.nbv1 + 4 * w, dst + 256 * q);
             }
@@ -1543,7 +1540,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     // chunks 0 and 1 go out first (bounded by the cache; the mask bounds them later)
     const int64_t n_kv = a.n_kv;
     int pend = 0;   // this stager wave's instructions of the chunk after the current one
-    if (wave >= 2) {
+    if (wave >= 1) {
         stage(0, 0, (int) min<int64_t>(CV, n_kv));
         if (n_kv > CV) pend = stage(1, CV, (int) min<int64_t>(CV, n_kv - CV));
     }
@@ -1554,7 +1551,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     constexpr int NT = FAL_NMAX / 256;
     float sv[NT];
     uint16_t mvb[NT];
-    const bool cw = tid < 256;   // waves 0-3 form the coefficients; 4-5 only join the barriers
+    const bool cw = tid < 256;   // waves 0-3 form the coefficients (any further waves only join the barriers)
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
         const int64_t j = 256 * k + tid;
@@ -1629,8 +1626,9 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     }
     __syncthreads();
 
-    // ---- the recurrence: waves 0-1 one output dim per lane; waves 2-3 keep two chunks in flight ----
-    const int d = tid;
+    // ---- the recurrence: wave 0, one of the workgroup's dims per lane; waves 1-3 keep two chunks
+    // in flight ----
+    const int d = lane;
     uint32_t yb = 0;     // f16 bits (f16 V)
     float yf = 0.0f;     // f32 accumulator (quantized V)
     float S = 0.0f;
@@ -1638,12 +1636,17 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     for (int c = 0; c < nchunk; ++c) {
         const int st = c % NSTG;
         // this wave's stage-c instructions have landed (those of c + 1 may still be in flight)
-        if (wave >= 2) eng_vm_wait_fa(pend);
+#ifndef FAL_EXP
+#define FAL_EXP 0
+#endif
+        // FAL_EXP (time-split experiments only, wrong results): 1 no recurrence, 2 no staging wait
+        if (wave >= 1 && !(FAL_EXP & 2)) eng_vm_wait_fa(pend);
         __syncthreads();   // stage c is in; every chain lane is done with chunk c - 1's stage
-        if (wave >= 2) {
+        if (wave >= 1) {
             pend = c + 2 < nchunk ? stage((c + 2) % NSTG, (int64_t) (c + 2) * CV, min(CV, nrun - (c + 2) * CV)) : 0;
             continue;
         }
+        if (FAL_EXP & 1) continue;
         const int jc = c * CV;                  // first position of the chunk
         const int nr = min(CV, nrun - jc);      // positions to run
         const int nb = (nr + U - 1) / U;
@@ -1667,7 +1670,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             const uint16_t * vrow = (const uint16_t *) sm.vr[st] + d;
             auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) vv[u] = vrow[(j + u) * D];
+                for (int u = 0; u < U; ++u) vv[u] = vrow[(j + u) * DH];
                 ld4(scp + j, vs);
             };
             auto run = [&](const uint32_t (&vv)[U], const float (&vs)[U]) {
@@ -1718,8 +1721,9 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             }
         } else {
             // f32 recurrence on dequantized V: v = (float) q * d (dequantize_row_q8_0 / _q4_0)
-            // the lane's byte and its block's f16 scale in a raw row: q8_0 block b = d / 32 at 34 b
-            // (d at +2, qs at +2 + d % 32); q4_0 at 18 b (qs at +2 + d % 16, low nibble for d % 32 < 16)
+            // the lane's byte and its block's f16 scale in a raw half row: q8_0 block b = d / 32 at
+            // 34 b (d at +2, qs at +2 + d % 32); q4_0 at 18 b (qs at +2 + d % 16, low nibble for
+            // d % 32 < 16)
             constexpr int KBV = VT == 2 ? 18 : 34;
             const int bo = KBV * (d / 32);
             const int qo = bo + 2 + (VT == 2 ? (d % 16) : (d % 32));
@@ -1787,33 +1791,34 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     }
 
     // ---- output and its optional quantization (k_fattn_exact's epilogue) ----
-    float * drow = (float *) ((char *) a.dst + h * a.nb1_dst + iq3 * a.nb2_dst);
-    const float o = d < D ? __fmul_rn(VT ? yf : h2f((uint16_t) yb), 1.0f / S) : 0.0f;
-    if (d < D) {
+    // (wave 0 holds the workgroup's DH outputs, dims DH·dh ..)
+    float * drow = (float *) ((char *) a.dst + h * a.nb1_dst + iq3 * a.nb2_dst) + DH * dh;
+    const float o = wave == 0 ? __fmul_rn(VT ? yf : h2f((uint16_t) yb), 1.0f / S) : 0.0f;
+    if (wave == 0) {
         if (a.qmode == 1) __hip_atomic_store(drow + d, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else drow[d] = o;
     }
     if (a.qmode == 2) {
-        __syncthreads();
-        if (d < D) sm.ol[d] = o;
+        // Q8_0 blocks of 32: the workgroup's DH outputs are whole blocks
+        if (wave == 0) sm.ol[d] = o;
         __syncthreads();
         if (wave == 0) {
-            const bool valid = 4 * lane < D;
+            const bool valid = 4 * lane < DH;
             float q[4] = {0.f, 0.f, 0.f, 0.f};
             if (valid) { const float4 v4 = *(const float4 *) (sm.ol + 4 * lane); q[0] = v4.x; q[1] = v4.y; q[2] = v4.z; q[3] = v4.w; }
-            const int64_t c0 = h * D;
+            const int64_t c0 = h * D + DH * dh;
             q8_0_wave(q, lane, valid, a.qs + c0, a.qd + c0 / 32, a.qsum + c0 / 32);
         }
     } else if (a.qmode == 1) {
-        // Q8_K: a block of 256 = two heads; the second of their workgroups to finish quantizes it
-        // (write-through outputs drained before the counter add, read back with sc1 loads)
+        // Q8_K: a block of 256 = two heads = 2·FAL_DSPLIT workgroups; the last of them to finish
+        // quantizes it (write-through outputs drained before the counter add, read back with sc1 loads)
         const int64_t blk = (h * D) / 256;
         __shared__ int is_last;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
             const int prev = __hip_atomic_fetch_add(a.cnt + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            is_last = prev == 1;
+            is_last = prev == 2 * FAL_DSPLIT - 1;
             if (is_last) __hip_atomic_store(a.cnt + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
@@ -1838,6 +1843,11 @@ bool fattn_long_ok(const fa_args & a, int64_t nq3) {
            (a.k_type == GGML_TYPE_F16 || a.k_type == GGML_TYPE_Q8_0 || a.k_type == GGML_TYPE_Q4_0);
 }
 
+static size_t fal_pad(size_t static_lds) {
+    const size_t half = 80 * 1024 + 1024;
+    return static_lds >= half ? 0 : half - static_lds;
+}
+
 void launch_fattn_long(hipStream_t st, const fa_args & a0, float * sco, unsigned long long * kt_scores) {
     fa_args a = a0;
     a.kt = kt_scores;
@@ -1848,11 +1858,13 @@ void launch_fattn_long(hipStream_t st, const fa_args & a0, float * sco, unsigned
         default:             hipLaunchKernelGGL(k_fal_scores<2>, gs, dim3(256), 0, st, a, sco); break;
     }
     a.kt = a0.kt;
-    const dim3 gc((unsigned) a.H, 1);
+    const dim3 gc((unsigned) (a.H * FAL_DSPLIT), 1);
     switch (a.v_type) {
-        case GGML_TYPE_F16:  hipLaunchKernelGGL(k_fal_chain<0>, gc, dim3(FAL_THREADS), 0, st, a, (const float *) sco); break;
-        case GGML_TYPE_Q8_0: hipLaunchKernelGGL(k_fal_chain<1>, gc, dim3(FAL_THREADS), 0, st, a, (const float *) sco); break;
-        default:             hipLaunchKernelGGL(k_fal_chain<2>, gc, dim3(FAL_THREADS), 0, st, a, (const float *) sco); break;
+        // (dynamic LDS pads a workgroup past half the CU's 160 KiB: one per CU, so no two chains
+        // share a CU's LDS-DMA stream)
+        case GGML_TYPE_F16:  hipLaunchKernelGGL(k_fal_chain<0>, gc, dim3(FAL_THREADS), fal_pad(sizeof(fal_smem<0>)), st, a, (const float *) sco); break;
+        case GGML_TYPE_Q8_0: hipLaunchKernelGGL(k_fal_chain<1>, gc, dim3(FAL_THREADS), fal_pad(sizeof(fal_smem<1>)), st, a, (const float *) sco); break;
+        default:             hipLaunchKernelGGL(k_fal_chain<2>, gc, dim3(FAL_THREADS), fal_pad(sizeof(fal_smem<2>)), st, a, (const float *) sco); break;
     }
 }
 

@@ -4,7 +4,7 @@ per wave at exit INSIDE the replayed hipGraph; this script decodes N tokens with
 on and prints, per launch label, the mean duration, dispatch ramp and the gap that precedes it,
 plus the per-token span split into instrumented kernel time and gaps.
 
-usage: python scripts/ktrace.py [--config llama3-8b-q4km] [--tokens 16] [--depth 0] [--csv out.csv]
+usage: python scripts/ktrace.py [--config llama3-8b-q4km] [--tokens 16] [--depth 0] [--kv f16] [--csv out.csv]
 """
 import argparse
 import collections
@@ -24,9 +24,10 @@ def main():
     ap.add_argument("--tokens", type=int, default=16)
     ap.add_argument("--depth", type=int, default=0)
     ap.add_argument("--csv", default="gpurun_out/ktrace.csv")
+    ap.add_argument("--kv", default="f16", help="KV cache type (f16, q8_0, q4_0)")
     a = ap.parse_args()
     path = gguf_synth.ensure(a.config)
-    m = la.Model(path, gpu=True, n_ctx=max(512, a.depth + a.tokens + 64))
+    m = la.Model(path, gpu=True, n_ctx=max(512, a.depth + a.tokens + 64), kv_type=a.kv)
     plugin = la.plugin_lib()
     plugin.ggml_backend_mi355x_ktrace_dump.argtypes = [ctypes.c_char_p]
     if a.depth:
