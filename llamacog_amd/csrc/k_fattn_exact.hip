@@ -107,6 +107,15 @@ __device__ __forceinline__ uint32_t f16_mad(uint32_t vbits, float vs, uint32_t y
     return r;
 }
 
+// the same with v held as a half (a ds_read_u16 result used as it is: no zero-extension mask)
+__device__ __forceinline__ uint32_t f16_mad_h(_Float16 v, float vs, uint32_t ybits) {
+    float t;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(v), "v"(vs), "v"(ybits));
+    uint32_t r;
+    asm("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
+
 // y = f16(f32(y) * ms): v_fma_mix_f32 with a -0 addend is the product rounded once to f32 (as
 // the CPU's _mm512_mul_ps of the converted halves), then the f16 rounding (vec_scale_f16)
 // (the -0 addend comes in a register: -0.0 is not an inline constant, and a +0 addend would turn
@@ -1494,6 +1503,19 @@ template <int VT> struct fal_smem {
     __attribute__((aligned(16))) uint8_t vr[NSTG][CV * RB + 64];
 };
 
+#ifndef FAL_EXP
+#define FAL_EXP 0
+#endif
+#ifndef FAL_H16
+#define FAL_H16 0   // V values held as halves in the chain (1; measured 7 % slower at 4096) or as 32-bit words (0)
+#endif
+#if FAL_H16
+typedef _Float16 fal_v16;
+#define FAL_MAD f16_mad_h
+#else
+typedef uint32_t fal_v16;
+#define FAL_MAD f16_mad
+#endif
 template <int VT>   // V type: 0 f16, 1 q8_0, 2 q4_0
 __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, const float * __restrict__ sco) {
     using SM = fal_smem<VT>;
@@ -1632,16 +1654,27 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     uint32_t yb = 0;     // f16 bits (f16 V)
     float yf = 0.0f;     // f32 accumulator (quantized V)
     float S = 0.0f;
+    nrun = __builtin_amdgcn_readfirstlane(nrun);   // uniform (from LDS): scalar loop control below
     const int nchunk = (nrun + CV - 1) / CV;
+#if FAL_EXP & 4
+    // phase clocks of workgroup 0's chain wave (time-split experiments only): start of the
+    // recurrence, summed barrier waits, end
+    const unsigned long long e_t1 = __builtin_amdgcn_s_memtime();
+    unsigned long long e_wait = 0;
+#endif
     for (int c = 0; c < nchunk; ++c) {
         const int st = c % NSTG;
         // this wave's stage-c instructions have landed (those of c + 1 may still be in flight)
-#ifndef FAL_EXP
-#define FAL_EXP 0
-#endif
-        // FAL_EXP (time-split experiments only, wrong results): 1 no recurrence, 2 no staging wait
+        // FAL_EXP (time-split experiments only, wrong results): 1 no recurrence, 2 no staging wait,
+        // 4 phase clocks
         if (wave >= 1 && !(FAL_EXP & 2)) eng_vm_wait_fa(pend);
+#if FAL_EXP & 4
+        const unsigned long long e_b0 = __builtin_amdgcn_s_memtime();
+#endif
         __syncthreads();   // stage c is in; every chain lane is done with chunk c - 1's stage
+#if FAL_EXP & 4
+        e_wait += __builtin_amdgcn_s_memtime() - e_b0;
+#endif
         if (wave >= 1) {
             pend = c + 2 < nchunk ? stage((c + 2) % NSTG, (int64_t) (c + 2) * CV, min(CV, nrun - (c + 2) * CV)) : 0;
             continue;
@@ -1667,21 +1700,21 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             }
         };
         if constexpr (VT == 0) {
-            const uint16_t * vrow = (const uint16_t *) sm.vr[st] + d;
-            auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
+            const auto * vrow = (const std::conditional_t<FAL_H16, _Float16, uint16_t> *) sm.vr[st] + d;
+            auto ldb = [&](int j, fal_v16 (&vv)[U], float (&vs)[U]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) vv[u] = vrow[(j + u) * DH];
                 ld4(scp + j, vs);
             };
-            auto run = [&](const uint32_t (&vv)[U], const float (&vs)[U]) {
+            auto run = [&](const fal_v16 (&vv)[U], const float (&vs)[U]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    yb = f16_mad(vv[u], vs[u], yb);
+                    yb = FAL_MAD(vv[u], vs[u], yb);
                     S = __fadd_rn(S, vs[u]);   // not contracted on the CPU
                 }
             };
             auto fast_run = [&](int j0, int nf) {
-                uint32_t va[U], vb[U];
+                fal_v16 va[U], vb[U];
                 float sa[U], sb[U];
                 ldb(j0, va, sa);
                 for (int k = 0; k < nf; k += 2) {
@@ -1693,7 +1726,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
                 }
             };
             auto general = [&](int j) {
-                uint32_t vv[U];
+                fal_v16 vv[U];
                 float vs[U], ms[U];
                 ldb(j, vv, vs);
                 ld4(cmp + j, ms);
@@ -1706,7 +1739,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
                     asm("" : "+v"(t));   // two roundings, as f16r
                     const uint32_t ys = upd ? (uint32_t) f2h(t) : yb;
                     const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
-                    const uint32_t yn = f16_mad(vv[u], vs[u], ys);
+                    const uint32_t yn = FAL_MAD(vv[u], vs[u], ys);
                     const float Sn = __fadd_rn(Ss, vs[u]);
                     yb = live ? yn : yb;
                     S = live ? Sn : S;
@@ -1790,6 +1823,10 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
         }
     }
 
+#if FAL_EXP & 4
+    if (blockIdx.x == 0 && tid == 0)
+        printf("[fal] n %d chunks %d: loop %llu ticks (barrier waits %llu)\n", nrun, nchunk, __builtin_amdgcn_s_memtime() - e_t1, e_wait);
+#endif
     // ---- output and its optional quantization (k_fattn_exact's epilogue) ----
     // (wave 0 holds the workgroup's DH outputs, dims DH·dh ..)
     float * drow = (float *) ((char *) a.dst + h * a.nb1_dst + iq3 * a.nb2_dst) + DH * dh;

@@ -522,8 +522,13 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     if constexpr (PRO) gemv_pro_load(p, pr);
     const int wr = lane / T::LPR, ws = lane % T::LPR;
     const int wrc = wr < R ? wr : 0;
+    // one walking wave (W1): after every wave's records, wave 0 walks all RPG rows of the group
+    // (its lanes in parallel: one walk where four waves each ran one, the other waves retire)
+    constexpr bool W1 = WPR == 1 && MODE == 0 && RPG * T::LPR <= WAVE;
+    const int64_t grow0 = (g - p.blk0[mi]) * RPG;
+    const int wr1 = lane / T::LPR, ws1 = lane % T::LPR, wrc1 = wr1 < RPG ? wr1 : 0;
     float rc = 0.0f;
-    if (MODE == 0 && p.rres) rc = p.rres[min(row0 + wrc, p.M[0] - 1)];
+    if (MODE == 0 && p.rres) rc = p.rres[min((W1 ? grow0 + wrc1 : row0 + wrc), p.M[0] - 1)];
     // ---- weight DMA: this wave's R row slices -> its LDS region (nt: read once per token) ----
     uint8_t * mine = wl + (size_t) wave * R * G::SLICE;
     {
@@ -578,6 +583,44 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
         typename T::raw w;
         T::template fetch<typename lds_loader<T>::type>(mine + r * G::SLICE - (int64_t) wsub * G::SEG, tt, w);
         T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * nb * T::RS);
+    }
+    if constexpr (W1) {
+        __syncthreads();   // every wave's records are in
+        if (wave != 0) return;
+        const float v = T::walk(xb + (size_t) wrc1 * nb * T::RS, nb, ws1);
+        const int64_t row = grow0 + wr1;
+        const bool mine_row = wr1 < RPG && ws1 == 0 && row < M;
+        double sq = 0.0;
+        if (mine_row) {
+            if (p.rres) {   // ADD(v, res): the CPU's single f32 add
+                const float xv = __fadd_rn(v, rc);
+                p.rxsum[row] = xv;
+                sq = (double) __fmul_rn(xv, xv);
+            } else if (p.tl.kind) {   // the SwiGLU tail reads it back: write-through
+                __hip_atomic_store(p.dst[mi] + row, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                p.dst[mi][row] = v;
+            }
+        }
+        if (p.tl.kind) {   // only this wave stored: drain, then one lane reports the group
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                const int blk = (int) (grow0 / 256);
+                __hip_atomic_fetch_add(p.tl.cnt + blk * TAIL_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (p.rres) {   // the group's rows' sum of squares, in row order, to the workgroup's shard
+            __shared__ double rpart1[RPG];
+            if (wr1 < RPG && ws1 == 0) rpart1[wr1] = sq;
+            wave_lds_sync();
+            if (lane == 0) {
+                double tot = 0.0;
+#pragma unroll
+                for (int k = 0; k < RPG; ++k) tot = __dadd_rn(tot, rpart1[k]);
+                __hip_atomic_fetch_add(p.rsum + RSUM_STRIDE * (g % RSUM_SHARDS), tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        return;
     }
     if constexpr (WPR > 1 || MODE != 0) __syncthreads();
     else wave_lds_sync();
