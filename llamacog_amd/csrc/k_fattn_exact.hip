@@ -1503,6 +1503,13 @@ template <int VT> struct fal_smem {
     __attribute__((aligned(16))) uint8_t vr[NSTG][CV * RB + 64];
 };
 
+// one step of a wave's inclusive max-scan: lanes without a DPP source keep -inf as the operand
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float fal_dmax(float v) {
+    const int t = __builtin_amdgcn_update_dpp(__float_as_int(-INFINITY), __float_as_int(v), CTRL, ROW_MASK, 0xf, false);
+    return fmaxf(v, __int_as_float(t));
+}
+
 #ifndef FAL_EXP
 #define FAL_EXP 0
 #endif
@@ -1522,6 +1529,9 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     constexpr int D = 128, NB = D / 32, CV = SM::CV, U = FAL_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     kt_enter(a.kt);
+#if FAL_EXP & 4
+    const unsigned long long e_t0 = __builtin_amdgcn_s_memtime();
+#endif
     // FAL_DSPLIT workgroups per head, each the recurrence of DH of its dims: V is staged through
     // the CU's LDS-DMA at ~25 GB/s per CU (MI355X_MICROARCH.md ldsdma-fill), so one CU per head
     // spent most of the chain waiting for its V stages; the split halves every CU's bytes while
@@ -1550,11 +1560,14 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
                 lds_dma16(vbase + (c0 + row) * a.nbv1 + 16 * col, dst + 1024 * q);
             }
         } else {
-            constexpr int DW = RB / 4;   // dword i of the stage = row i / DW, dword i % DW
-            const int ndw = n * DW;
-            for (int q = sw; 64 * q < ndw; q += 3, ++cnt) {
-                const int i = min(64 * q + (t & 63), ndw - 1), row = i / DW, w = i % DW;
-                lds_dma4(vbase + (c0 + row) * a.nbv1 + 4 * w, dst + 256 * q);
+            // each stager wave moves a contiguous third of the rows
+            constexpr int DW = RB / 4;   // dword i of the wave's rows = row r0 + i / DW, dword i % DW
+            const int per = (n + 2) / 3, r0 = min(n, sw * per), r1 = min(n, r0 + per);
+            const int ndw = (r1 - r0) * DW;
+            for (int q = 0; 64 * q < ndw; ++q, ++cnt) {
+                // lanes past the wave's rows stay off: their LDS slots are the next wave's rows
+                const int i = 64 * q + (t & 63), row = r0 + i / DW, w = i % DW;
+                if (i < ndw) lds_dma4(vbase + (c0 + row) * a.nbv1 + 4 * w, dst + r0 * RB + 256 * q);
             }
         }
         return cnt;
@@ -1568,81 +1581,127 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     }
 
     // ---- coefficients of every position (all waves) ----
-    // every score and mask value of the thread's positions is loaded first, then the passes
-    // scan them (a load per pass would put one memory round trip in each of up to 32 passes)
+    // Wave w owns a contiguous segment of positions (64·nq of them, lane l at 64 i + l of group i),
+    // so the running maximum is a scan inside the wave (DPP row shifts and row broadcasts, no LDS
+    // round trips) plus ONE exchange of the four segment maxima: the CPU's M before position j is
+    // the maximum over every earlier live position, which is the same set either way (max is
+    // order-free).  Every score and mask value is loaded first (one memory round trip).
     constexpr int NT = FAL_NMAX / 256;
+    const int nq = (int) ((n_kv + 255) / 256);   // 64-position groups per wave (uniform)
+    // expf's 32-entry 2^(i/32) table in LDS: a global-table gather per position put one memory
+    // round trip into every group of the coefficient pass
+    __shared__ uint64_t exptab[32];
+    if (tid < 32) exptab[tid] = lx_exp2f_tab[tid];
+    const int seg0 = wave * 64 * nq;   // (positions < FAL_NMAX: 32-bit arithmetic)
+    const int nkv = (int) n_kv;
     float sv[NT];
     uint16_t mvb[NT];
-    const bool cw = tid < 256;   // waves 0-3 form the coefficients (any further waves only join the barriers)
 #pragma unroll
-    for (int k = 0; k < NT; ++k) {
-        const int64_t j = 256 * k + tid;
-        if (cw && 256 * k < n_kv) {
-            const int64_t jc = min(j, n_kv - 1);
-            mvb[k] = mrow ? *(const uint16_t *) (mrow + 2 * jc) : (uint16_t) 0;
-            sv[k] = srow[jc];
+    for (int i = 0; i < NT; ++i) {
+        if (i < nq) {
+            const int jc = min(seg0 + 64 * i + lane, nkv - 1);
+            mvb[i] = mrow ? *(const uint16_t *) (mrow + 2 * jc) : (uint16_t) 0;
+            sv[i] = srow[jc];
         }
     }
-    float carry = -INFINITY;
-    int nrun = 0;
+
+    // phase A: each group's own inclusive max-scan and total (the groups are independent, so their
+    // latency chains interleave: one wave per SIMD has nothing else to hide them behind), then the
+    // carry into every group from the totals before it; the live extent
+    float pm[NT], tot[NT];
+    int wlast = -1;
 #pragma unroll
-    for (int k = 0; k < NT; ++k) {
-        const int64_t t0 = 256 * k;
-        if (t0 >= n_kv) break;
-        const int64_t j = t0 + tid;
-        if (!cw) {   // the two barriers of the pass, and the live extent (the stagers need it)
-            __syncthreads();
-            nrun = max(nrun, max(max(sm.wlast[0], sm.wlast[1]), max(sm.wlast[2], sm.wlast[3])) + 1);
-            __syncthreads();
-            continue;
+    for (int i = 0; i < NT; ++i) {
+        if (i < nq) {   // (a guard, not a break: the loop stays unrolled and the arrays in registers)
+            const int j = seg0 + 64 * i + lane;
+            const bool live = j < nkv && h2f(mvb[i]) != -INFINITY;
+            const float sj = live ? sv[i] : -INFINITY;
+            sv[i] = sj;
+            float v = sj;
+            v = fal_dmax<0x111, 0xf>(v);   // row_shr:1
+            v = fal_dmax<0x112, 0xf>(v);   // row_shr:2
+            v = fal_dmax<0x114, 0xf>(v);   // row_shr:4
+            v = fal_dmax<0x118, 0xf>(v);   // row_shr:8
+            v = fal_dmax<0x142, 0xa>(v);   // row_bcast:15
+            v = fal_dmax<0x143, 0xc>(v);   // row_bcast:31
+            pm[i] = v;
+            tot[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+            const unsigned long long lb = __ballot(live);
+            if (lb) wlast = (int) (seg0 + 64 * i + 63 - __clzll(lb));
         }
-        const float m = j < n_kv ? h2f(mvb[k]) : -INFINITY;
-        const bool live = m != -INFINITY;
-        const float sj = live ? sv[k] : -INFINITY;
-        float smx = sj;   // inclusive max-scan over the wave
+    }
+    float carry[NT];   // the maximum of the segment's groups before group i
+    float run = -INFINITY;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const float tt = __shfl_up(smx, o, WAVE);
-            if (lane >= o) smx = fmaxf(smx, tt);
+    for (int i = 0; i < NT; ++i) {
+        if (i < nq) {   // (a guard, not a break: the loop stays unrolled and the arrays in registers)
+            carry[i] = run;
+            pm[i] = fmaxf(pm[i], run);
+            run = fmaxf(run, tot[i]);
         }
-        const unsigned long long lb = __ballot(live);
-        if (lane == 63) sm.wmax[wave] = smx;
-        if (lane == 0) sm.wlast[wave] = lb ? (int) (t0 + 64 * wave + 63 - __clzll(lb)) : -1;
-        __syncthreads();
-        float M = carry;
-        for (int w2 = 0; w2 < wave; ++w2) M = fmaxf(M, sm.wmax[w2]);
-        const float ex = __shfl_up(smx, 1, WAVE);
-        if (lane > 0) M = fmaxf(M, ex);
-        float cmv = 1.0f, scv = 0.0f;
+    }
+#if FAL_EXP & 4
+    const unsigned long long e_ta = __builtin_amdgcn_s_memtime();
+#endif
+    if (lane == 0) { sm.wmax[wave] = run; sm.wlast[wave] = wlast; }
+    __syncthreads();   // (also publishes exptab)
+#if FAL_EXP & 4
+    const unsigned long long e_tb = __builtin_amdgcn_s_memtime();
+#endif
+    float Mprev = -INFINITY;
+    for (int w2 = 0; w2 < wave; ++w2) Mprev = fmaxf(Mprev, sm.wmax[w2]);
+    int nrun = max(max(sm.wlast[0], sm.wlast[1]), max(sm.wlast[2], sm.wlast[3])) + 1;
+    // phase B: per position the exclusive maximum M and the score go to cm / sc (the expf pass
+    // below turns them into (ms, vs) chunk by chunk, ahead of the chain), dead bits, batch flags
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+        if (i < nq) {   // (a guard, not a break: the loop stays unrolled and the arrays in registers)
+            const int j = seg0 + 64 * i + lane;
+            const float sj = sv[i];
+            const bool live = j < nkv && h2f(mvb[i]) != -INFINITY;
+            const float ex = __shfl_up(pm[i], 1, WAVE);
+            const float M = fmaxf(Mprev, lane > 0 ? ex : carry[i]);
+            const bool upd = live && sj > M;
+            if (j < FAL_NMAX) { sm.cm[j] = M; sm.sc[j] = sj; }
+            const unsigned long long gw = __ballot(!live || upd);
+            const unsigned long long dw = __ballot(!live);
+            if (lane == 0) {
+                const int p0 = seg0 + 64 * i;
+                sm.dead[p0 / 32] = (uint32_t) dw;
+                sm.dead[p0 / 32 + 1] = (uint32_t) (dw >> 32);
+                // bit b: any of batch b's U = 8 positions flagged (each byte's OR, then gathered)
+                static_assert(U == 8, "byte-wise batch flags");
+                uint64_t x = gw;
+                x |= x >> 4; x |= x >> 2; x |= x >> 1;
+                sm.gb[p0 / 64] = (uint8_t) (((x & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+            }
+        }
+    }
+    // the expf pass of 64 positions from p0 (one per lane), in place: the CPU's ms = expf(Mold - M)
+    // and vs = 1 on a max update, ms = 1 and vs = expf(s - M) otherwise, (1, 0) where dead
+    auto coef64 = [&](int p0) {
+        const int j = p0 + lane;
+        const float M = sm.cm[j], sj = sm.sc[j];
+        const bool live = ((sm.dead[j / 32] >> (j % 32)) & 1u) == 0;
         const bool upd = live && sj > M;
+        float cmv = 1.0f, scv = 0.0f;
         if (live) {
-            if (upd) { cmv = M == -INFINITY ? 0.0f : expf_cr(M - sj); scv = 1.0f; }
-            else scv = expf_cr(sj - M);
+            const float e = lx_expf_t(upd ? M - sj : sj - M, exptab);
+            if (upd) { cmv = M == -INFINITY ? 0.0f : e; scv = 1.0f; }
+            else scv = e;
         }
-        if (j < FAL_NMAX) { sm.cm[j] = cmv; sm.sc[j] = scv; }
-        const unsigned long long gw = __ballot(!live || upd);
-        const unsigned long long dw = __ballot(!live);
-        if (lane == 0) {
-            sm.dead[(t0 + 64 * wave) / 32] = (uint32_t) dw;
-            sm.dead[(t0 + 64 * wave) / 32 + 1] = (uint32_t) (dw >> 32);
-            uint32_t f = 0;
-#pragma unroll
-            for (int b = 0; b < 64 / U; ++b) f |= ((gw >> (U * b)) & ((1ull << U) - 1)) ? 1u << b : 0u;
-            sm.gb[(t0 + 64 * wave) / 64] = (uint8_t) f;
-        }
-        const int lastw = max(max(sm.wlast[0], sm.wlast[1]), max(sm.wlast[2], sm.wlast[3]));
-        nrun = max(nrun, lastw + 1);
-        carry = fmaxf(fmaxf(carry, fmaxf(sm.wmax[0], sm.wmax[1])), fmaxf(sm.wmax[2], sm.wmax[3]));
-        __syncthreads();
-    }
-    // the batch past the last live position reads dead padding
-    __syncthreads();
-    if (tid < 2 * U) {
-        const int j = nrun + tid;
-        sm.cm[j] = 1.0f; sm.sc[j] = 0.0f;
-    }
-    if (tid == 0) {
-        // positions past the last live one are dead (the last batch reads up to U - 1 of them)
+        sm.cm[j] = cmv;
+        sm.sc[j] = scv;
+    };
+#if FAL_EXP & 4
+    const unsigned long long e_tc = __builtin_amdgcn_s_memtime();
+#endif
+    __syncthreads();   // M / s and the dead bits of every position are in
+    nrun = __builtin_amdgcn_readfirstlane(nrun);   // uniform (from LDS): scalar loop control below
+    const int nchunk = (nrun + CV - 1) / CV;
+    if (nchunk > 0 && wave < CV / 64) coef64(64 * wave);   // chunk 0's coefficients before the loop
+    if (tid == 0 && nrun > 0) {
+        // the positions past the last live one are dead (the last batch reads up to U - 1 of them)
         for (int j = nrun; j < ((nrun + U - 1) / U) * U + U; ++j) sm.dead[j / 32] |= 1u << (j % 32);
         sm.gb[nrun / 64] |= (uint8_t) (1u << ((nrun % 64) / U));   // the partial batch (if any)
     }
@@ -1654,8 +1713,6 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     uint32_t yb = 0;     // f16 bits (f16 V)
     float yf = 0.0f;     // f32 accumulator (quantized V)
     float S = 0.0f;
-    nrun = __builtin_amdgcn_readfirstlane(nrun);   // uniform (from LDS): scalar loop control below
-    const int nchunk = (nrun + CV - 1) / CV;
 #if FAL_EXP & 4
     // phase clocks of workgroup 0's chain wave (time-split experiments only): start of the
     // recurrence, summed barrier waits, end
@@ -1677,6 +1734,11 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
 #endif
         if (wave >= 1) {
             pend = c + 2 < nchunk ? stage((c + 2) % NSTG, (int64_t) (c + 2) * CV, min(CV, nrun - (c + 2) * CV)) : 0;
+            // the next chunk's coefficients, by one stager wave in turn, while the chain runs this one
+            if (c + 1 < nchunk && (c + 1) % 3 == wave - 1) {
+#pragma unroll
+                for (int g2 = 0; g2 < CV / 64; ++g2) coef64((c + 1) * CV + 64 * g2);
+            }
             continue;
         }
         if (FAL_EXP & 1) continue;
@@ -1764,6 +1826,8 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             const uint8_t * vrw = sm.vr[st];
             // a batch's raw bytes and block scales are read one batch ahead; the dequant (off the
             // chain) happens in run, so a read's wait never precedes the previous batch
+            // (dequantizing whole chunks into an f32 buffer in the stager waves measured slower:
+            // the stagers, not the chain, became the bound)
             struct vraw { uint32_t q[U]; uint32_t dv[U]; };
             auto ldb = [&](int j, vraw & vv, float (&vs)[U]) {
 #pragma unroll
@@ -1825,7 +1889,8 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
 
 #if FAL_EXP & 4
     if (blockIdx.x == 0 && tid == 0)
-        printf("[fal] n %d chunks %d: loop %llu ticks (barrier waits %llu)\n", nrun, nchunk, __builtin_amdgcn_s_memtime() - e_t1, e_wait);
+        printf("[fal] n %d chunks %d: scan %llu exchange %llu M-pass %llu rest %llu, loop %llu ticks (barrier waits %llu)\n", nrun,
+               nchunk, e_ta - e_t0, e_tb - e_ta, e_tc - e_tb, e_t1 - e_tc, __builtin_amdgcn_s_memtime() - e_t1, e_wait);
 #endif
     // ---- output and its optional quantization (k_fattn_exact's epilogue) ----
     // (wave 0 holds the workgroup's DH outputs, dims DH·dh ..)
