@@ -625,7 +625,15 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     if constexpr (WPR > 1 || MODE != 0) __syncthreads();
     else wave_lds_sync();
     __shared__ float res[MODE ? RPG : 1];
-    if (wsub == 0) {
+    // epilogue launches: wave 0 walks every row of the group into res (one walk where four waves
+    // each ran one); the stores below are the whole workgroup's as before
+    constexpr bool W1E = WPR == 1 && MODE != 0 && RPG * T::LPR <= WAVE;
+    if constexpr (W1E) {
+        if (wave == 0) {
+            const float v = T::walk(xb + (size_t) wrc1 * nb * T::RS, nb, ws1);
+            if (wr1 < RPG && ws1 == 0) res[wr1] = v;
+        }
+    } else if (wsub == 0) {
         const float v = (MI_EXP & 1) ? xb[lane] * 0.5f : T::walk(xb + (size_t) (rowl0 + wrc) * nb * T::RS, nb, ws);
         if (wr < R && ws == 0) {
             if constexpr (MODE == 0) {
