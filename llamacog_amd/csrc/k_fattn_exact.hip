@@ -1368,7 +1368,7 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
 // its chain waves run the recurrence while its stager waves stream the next V chunk into LDS.
 // The arithmetic of every step is k_fattn_exact's (the CPU's ops.cpp:7015-7232), so the bits are.
 constexpr int FAL_PB = 256;       // positions per scores workgroup
-constexpr int FAL_NMAX = 6144;    // positions the chain's coefficient arrays hold
+constexpr int FAL_NMAX = 8192;    // positions the chain's coefficient arrays hold
 constexpr int FAL_GMAX = 8;       // query heads per KV head (GQA) the scores kernel takes
 constexpr int FAL_U = 8;          // chain batch
 
@@ -1486,15 +1486,17 @@ __global__ __launch_bounds__(256) void k_fal_scores(const fa_args a, float * __r
 }
 
 // LDS of the chain kernel
-template <int VT> struct fal_smem {
+// NM: positions the coefficient arrays hold (6144 or FAL_NMAX: the smaller instance keeps the
+// per-thread score registers and the unrolled passes of shorter caches small)
+template <int VT, int NM = FAL_NMAX> struct fal_smem {
     static constexpr int D = 128, DH = D / FAL_DSPLIT, NBH = DH / 32;   // a workgroup's dims
     static constexpr int CV = 128;                        // V positions per stage
     static constexpr int RB = VT == 0 ? 2 * DH : (VT == 1 ? 34 * NBH : 18 * NBH);   // bytes of a row's half (raw)
     static constexpr int NSTG = 3;                        // stages: chunks c + 1 and c + 2 in flight
-    float cm[FAL_NMAX + 2 * FAL_U];             // ms coefficient (1 where dead)
-    float sc[FAL_NMAX + 2 * FAL_U];             // vs coefficient (0 where dead)
-    uint32_t dead[FAL_NMAX / 32 + 2];           // bit per position: masked (the state is kept)
-    uint8_t gb[FAL_NMAX / 64 + 4];              // per 64 positions: its 8 batches taking the general step
+    float cm[NM + 2 * FAL_U];                   // ms coefficient (1 where dead)
+    float sc[NM + 2 * FAL_U];                   // vs coefficient (0 where dead)
+    uint32_t dead[NM / 32 + 2];                 // bit per position: masked (the state is kept)
+    uint8_t gb[NM / 64 + 4];                    // per 64 positions: its 8 batches taking the general step
     float wmax[4];
     int wlast[4];
     float ol[64];
@@ -1523,9 +1525,9 @@ typedef _Float16 fal_v16;
 typedef uint32_t fal_v16;
 #define FAL_MAD f16_mad
 #endif
-template <int VT>   // V type: 0 f16, 1 q8_0, 2 q4_0
+template <int VT, int NM>   // V type: 0 f16, 1 q8_0, 2 q4_0; NM: positions held (n_kv <= NM)
 __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, const float * __restrict__ sco) {
-    using SM = fal_smem<VT>;
+    using SM = fal_smem<VT, NM>;
     constexpr int D = 128, NB = D / 32, CV = SM::CV, U = FAL_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     kt_enter(a.kt);
@@ -1586,13 +1588,13 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     // round trips) plus ONE exchange of the four segment maxima: the CPU's M before position j is
     // the maximum over every earlier live position, which is the same set either way (max is
     // order-free).  Every score and mask value is loaded first (one memory round trip).
-    constexpr int NT = FAL_NMAX / 256;
+    constexpr int NT = NM / 256;
     const int nq = (int) ((n_kv + 255) / 256);   // 64-position groups per wave (uniform)
     // expf's 32-entry 2^(i/32) table in LDS: a global-table gather per position put one memory
     // round trip into every group of the coefficient pass
     __shared__ uint64_t exptab[32];
     if (tid < 32) exptab[tid] = lx_exp2f_tab[tid];
-    const int seg0 = wave * 64 * nq;   // (positions < FAL_NMAX: 32-bit arithmetic)
+    const int seg0 = wave * 64 * nq;   // (positions < NM: 32-bit arithmetic)
     const int nkv = (int) n_kv;
     float sv[NT];
     uint16_t mvb[NT];
@@ -1662,7 +1664,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             const float ex = __shfl_up(pm[i], 1, WAVE);
             const float M = fmaxf(Mprev, lane > 0 ? ex : carry[i]);
             const bool upd = live && sj > M;
-            if (j < FAL_NMAX) { sm.cm[j] = M; sm.sc[j] = sj; }
+            if (j < NM) { sm.cm[j] = M; sm.sc[j] = sj; }
             const unsigned long long gw = __ballot(!live || upd);
             const unsigned long long dw = __ballot(!live);
             if (lane == 0) {
@@ -1939,7 +1941,10 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
 // the long-context pair applies: one query row, D = 128, a cache longer than FA_LONG_MIN (and
 // within the chain's coefficient arrays), a GQA group the scores kernel takes, one batch
 bool fattn_long_ok(const fa_args & a, int64_t nq3) {
-    static const int lmin = getenv("GGML_MI355X_FA_LONG") ? atoi(getenv("GGML_MI355X_FA_LONG")) : FA_LONG_MIN;
+    // from where the pair beats the per-head kernels (scripts/probe_fal.py, round 4): f16 ≈ 700
+    // positions, q8_0 below 512 (its per-head kernel is slower); GGML_MI355X_FA_LONG sets both
+    static const int lenv = getenv("GGML_MI355X_FA_LONG") ? atoi(getenv("GGML_MI355X_FA_LONG")) : -1;
+    const int lmin = lenv >= 0 ? lenv : (a.k_type == GGML_TYPE_F16 ? FA_LONG_MIN : FA_LONG_MIN_Q);
     return lmin > 0 && a.n_q == 1 && a.D == 128 && nq3 == 1 && a.n_kv >= lmin && a.n_kv <= FAL_NMAX &&
            a.H % a.Hkv == 0 && a.H / a.Hkv <= FAL_GMAX && (a.qmode != 1 || a.H % 2 == 0) &&
            (a.k_type == GGML_TYPE_F16 || a.k_type == GGML_TYPE_Q8_0 || a.k_type == GGML_TYPE_Q4_0);
@@ -1961,12 +1966,15 @@ void launch_fattn_long(hipStream_t st, const fa_args & a0, float * sco, unsigned
     }
     a.kt = a0.kt;
     const dim3 gc((unsigned) (a.H * FAL_DSPLIT), 1);
+    const bool small = a.n_kv <= 6144;
     switch (a.v_type) {
         // (dynamic LDS pads a workgroup past half the CU's 160 KiB: one per CU, so no two chains
         // share a CU's LDS-DMA stream)
-        case GGML_TYPE_F16:  hipLaunchKernelGGL(k_fal_chain<0>, gc, dim3(FAL_THREADS), fal_pad(sizeof(fal_smem<0>)), st, a, (const float *) sco); break;
-        case GGML_TYPE_Q8_0: hipLaunchKernelGGL(k_fal_chain<1>, gc, dim3(FAL_THREADS), fal_pad(sizeof(fal_smem<1>)), st, a, (const float *) sco); break;
-        default:             hipLaunchKernelGGL(k_fal_chain<2>, gc, dim3(FAL_THREADS), fal_pad(sizeof(fal_smem<2>)), st, a, (const float *) sco); break;
+#define FAL_CHAIN(VT, NM) hipLaunchKernelGGL((k_fal_chain<VT, NM>), gc, dim3(FAL_THREADS), fal_pad(sizeof(fal_smem<VT, NM>)), st, a, (const float *) sco)
+        case GGML_TYPE_F16:  if (small) FAL_CHAIN(0, 6144); else FAL_CHAIN(0, FAL_NMAX); break;
+        case GGML_TYPE_Q8_0: if (small) FAL_CHAIN(1, 6144); else FAL_CHAIN(1, FAL_NMAX); break;
+        default:             if (small) FAL_CHAIN(2, 6144); else FAL_CHAIN(2, FAL_NMAX); break;
+#undef FAL_CHAIN
     }
 }
 

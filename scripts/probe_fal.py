@@ -15,7 +15,7 @@ def child(which):
     op = la.plugin_lib().mi355x_bench_op
     op.restype = ctypes.c_double
     op.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
-    for n, v in ((256, 136), (1024, 1024), (2048, 2048), (4352, 4096), (8192, 8192)):
+    for n, v in ((256, 136), (512, 512), (768, 700), (1024, 1024), (2048, 2048), (4352, 4096), (8192, 8192)):
         print(f"  n_kv={n:5d} valid={v:5d}: {op(which, n, v, 30):8.2f} us", flush=True)
 
 
@@ -23,7 +23,7 @@ def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--child":
         return child(int(sys.argv[2]))
     for kv, which in (("f16", 0), ("q8_0", 3)):
-        for label, env in (("per-head kernels", {"GGML_MI355X_FA_LONG": "0"}), ("long pair", {"GGML_MI355X_FA_LONG": "512"})):
+        for label, env in (("per-head kernels", {"GGML_MI355X_FA_LONG": "0"}), ("long pair", {"GGML_MI355X_FA_LONG": "256"})):
             print(f"== {kv} cache, {label}", flush=True)
             e = dict(os.environ)
             e.update(env)

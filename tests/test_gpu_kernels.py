@@ -167,11 +167,11 @@ def test_flash_attn_golden_all_kv(K, golden_dir, tag, kv):
 
 @pytest.mark.parametrize("kv,n_kv,Hkv,G,pattern", [("q8_0", 2500, 8, 4, "holes"), ("q4_0", 1300, 8, 4, "causal"),
                                                    ("q4_0", 4100, 2, 8, "sparse"), ("q8_0", 1024, 1, 8, "causal"),
-                                                   ("q8_0", 6144, 8, 4, "causal")])
+                                                   ("q8_0", 8192, 8, 4, "causal"), ("q4_0", 600, 8, 4, "holes")])
 def test_flash_attn_quant_long_vs_oracle(K, kv, n_kv, Hkv, G, pattern):
     """Quantized caches at depth through the long-context pair: interleaved heads (the llama cache
     view: rows a dword a lane into LDS) and a single KV head (contiguous rows), ragged last chunk,
-    the longest cache the chain takes (6144)."""
+    the longest cache the chain takes (8192), and a short one past the quantized threshold (384)."""
     rng = np.random.default_rng(n_kv + Hkv)
     D, H = 128, Hkv * G
     kvt = O.Q8_0 if kv == "q8_0" else O.Q4_0
@@ -246,7 +246,7 @@ def test_buffer_from_host_ptr_matvec_bit_exact():
 @pytest.mark.parametrize("n_kv,Hkv,G,pattern", [(300, 4, 1, "holes"), (1000, 8, 2, "first_chunk_dead"),
                                                   (256, 8, 4, "single"), (129, 2, 4, "holes"), (4352, 8, 4, "sparse"),
                                                   (2000, 8, 2, "first_chunk_dead"), (1300, 2, 4, "single"),
-                                                  (5000, 8, 4, "holes")])
+                                                  (5000, 8, 4, "holes"), (8192, 8, 4, "sparse"), (800, 8, 4, "holes")])
 def test_flash_attn_f16_decode_masks_vs_oracle(K, n_kv, Hkv, G, pattern):
     """Decode (one query row) over masks the causal tail does not exercise: dead positions inside
     a batch, a whole dead chunk, a single live position, one position past a chunk boundary, and
