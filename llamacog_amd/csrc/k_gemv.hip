@@ -1511,9 +1511,9 @@ static void launch_os(hipStream_t st, gemv_args & a, int nmat) {
     else launch_os_m<T, R, WPR, 0>(st, a, nmat);
 }
 
-// rows per wave of the one-shot kernel (tools/gemv_lab.hip, round 3): one row, except two for
-// the 4-bit K-quants at K = 14336, and two (four at K <= 4096) wherever a norm prologue is formed
-// per workgroup (fewer workgroups form it)
+// rows per wave of the one-shot kernel (tools/gemv_lab.hip, round 3; round 4 below): two for the
+// 4-bit K-quants at K = 14336, two (four at K <= 4096) wherever a norm prologue is formed per
+// workgroup (fewer workgroups form it), and two for the plain one-wave-per-row launches
 template <class T>
 static bool launch_os_t(hipStream_t st, gemv_args & a, int nmat) {
     if (!os_enabled() || !os_aligned<T>(a, nmat)) return false;
@@ -1522,6 +1522,12 @@ static bool launch_os_t(hipStream_t st, gemv_args & a, int nmat) {
     int R = 1;
     if (a.pro.x || (wpr == 4 && !std::is_same<T, g_q6_K>::value)) R = 2;
     if (a.pro.x && wpr == 1) R = 4;   // a norm prologue per workgroup: half as many of them (9.9 -> 9.3 us)
+    // with one walking wave per workgroup, two rows per wave for the plain (no prologue / epilogue)
+    // launches: gate/up 16.5 -> 14.9 us (scripts/probe_mall_gemv.py, round 4); the 6-bit output
+    // head keeps one (71 vs 77 us). GGML_MI355X_OS_R overrides it (A/B only)
+    if (!a.pro.x && wpr == 1 && !needs_epilogue(a, nmat) && !std::is_same<T, g_q6_K>::value) R = 2;
+    static const int r_env = getenv("GGML_MI355X_OS_R") ? atoi(getenv("GGML_MI355X_OS_R")) : 0;
+    if (r_env > 0 && !a.pro.x && wpr == 1 && !needs_epilogue(a, nmat)) R = r_env;
     if (wpr == 4 && needs_epilogue(a, nmat)) return false;   // rope pairs need an even group
     gemv_args b = a;
     const size_t lds = R == 4 ? os_lds_layout<T, 4, 1>(b)

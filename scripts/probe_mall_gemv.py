@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 Q4_K, Q6_K = 12, 14
 BB = {Q4_K: (144, 256), Q6_K: (210, 256)}
 SHAPES = [("O-proj q4K", Q4_K, 4096, 4096, 1), ("QK q4K", Q4_K, 4096, 5120, 1), ("gate+up q4K", Q4_K, 4096, 14336, 2),
-          ("down q4K", Q4_K, 14336, 4096, 1), ("down q6K", Q6_K, 14336, 4096, 1)]
+          ("down q4K", Q4_K, 14336, 4096, 1), ("down q6K", Q6_K, 14336, 4096, 1), ("head q6K", Q6_K, 4096, 128256, 1)]
 
 
 def main():
