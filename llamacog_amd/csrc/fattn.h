@@ -47,8 +47,9 @@ void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int6
 // grid into sco [H][n_kv], then one chain workgroup per head (coefficients of all positions in
 // LDS, V streamed by stager waves); from FA_LONG_MIN cached positions (GGML_MI355X_FA_LONG)
 constexpr int FAL_THREADS = 256;   // the long-context chain kernel: wave 0 the recurrence, 1-3 stage V
+constexpr int FAL_PB = 128;        // positions per scores workgroup (k_fal_scores)
 constexpr int FAL_DSPLIT = 2;      // chain workgroups per head (each DH = 128 / FAL_DSPLIT of its dims)
-constexpr int FA_LONG_MIN = 768;     // f16 cache
+constexpr int FA_LONG_MIN = 512;     // f16 cache
 constexpr int FA_LONG_MIN_Q = 384;   // q8_0 / q4_0 cache
 bool fattn_long_ok(const fa_args & a, int64_t nq3);
 void launch_fattn_long(hipStream_t stream, const fa_args & a, float * sco, unsigned long long * kt_scores);

@@ -102,7 +102,7 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     if (fattn_long_ok(a, nq3)) {
         // long cache: scores by a wide grid, then the exact recurrence (k_fattn_exact.hip)
         float * sco = (float *) ctx.scratch(1, (size_t) a.H * a.n_kv * sizeof(float));
-        unsigned long long * kts = ctx.kt_take("fa_scores", (unsigned) (ceil_div(a.n_kv, (int64_t) 256) * a.Hkv), 256);
+        unsigned long long * kts = ctx.kt_take("fa_scores", (unsigned) (ceil_div(a.n_kv, (int64_t) FAL_PB) * a.Hkv), 256);
         a.kt = ctx.kt_take("fa_chain", (unsigned) (a.H * FAL_DSPLIT), FAL_THREADS);
         launch_fattn_long(ctx.stream, a, sco, kts);
     } else if (fattn_dec2_ok(a, nq3)) {

@@ -1367,7 +1367,6 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
 // (ms, vs) coefficients of ALL positions in LDS (a scan, then expf per position: parallel), and
 // its chain waves run the recurrence while its stager waves stream the next V chunk into LDS.
 // The arithmetic of every step is k_fattn_exact's (the CPU's ops.cpp:7015-7232), so the bits are.
-constexpr int FAL_PB = 256;       // positions per scores workgroup
 constexpr int FAL_NMAX = 8192;    // positions the chain's coefficient arrays hold
 constexpr int FAL_GMAX = 8;       // query heads per KV head (GQA) the scores kernel takes
 constexpr int FAL_U = 8;          // chain batch

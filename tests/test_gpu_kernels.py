@@ -246,7 +246,8 @@ def test_buffer_from_host_ptr_matvec_bit_exact():
 @pytest.mark.parametrize("n_kv,Hkv,G,pattern", [(300, 4, 1, "holes"), (1000, 8, 2, "first_chunk_dead"),
                                                   (256, 8, 4, "single"), (129, 2, 4, "holes"), (4352, 8, 4, "sparse"),
                                                   (2000, 8, 2, "first_chunk_dead"), (1300, 2, 4, "single"),
-                                                  (5000, 8, 4, "holes"), (8192, 8, 4, "sparse"), (800, 8, 4, "holes")])
+                                                  (5000, 8, 4, "holes"), (8192, 8, 4, "sparse"), (800, 8, 4, "holes"),
+                                                  (520, 8, 4, "holes")])
 def test_flash_attn_f16_decode_masks_vs_oracle(K, n_kv, Hkv, G, pattern):
     """Decode (one query row) over masks the causal tail does not exercise: dead positions inside
     a batch, a whole dead chunk, a single live position, one position past a chunk boundary, and
