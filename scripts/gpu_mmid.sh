@@ -1,0 +1,15 @@
+# MUL_MAT_ID decode on the one-shot kernel: MoE parity tests, Mixtral tg A/B against k_mmx, trace
+set -o pipefail
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$PWD}
+cd $R
+OUT=gpurun_out/${OUT:-r04mm}
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -rA --timeout 300 --timeout-method thread -k "mul_mat_id or moe or mixtral or bit_identical" > $OUT/pytest_moe.log 2>&1 || { echo "pytest rc=$?"; grep -E "FAILED|Error|assert" $OUT/pytest_moe.log | head -20; tail -5 $OUT/pytest_moe.log; exit 1; }
+grep -E "passed|failed" $OUT/pytest_moe.log | tail -1
+B="python bench.py --config mixtral-8x7b-q5km --steps 64 --warmup 4 --no-cpu-baseline --no-split-series --roofline-steps 8"
+timeout -k 10 600 $B > $OUT/bench_mixtral.json 2> $OUT/bench_mixtral.err || { echo "bench rc=$?"; tail -20 $OUT/bench_mixtral.err; exit 1; }
+GGML_MI355X_MMID_OS=0 timeout -k 10 600 $B --pp 0 > $OUT/bench_mixtral_mmx.json 2> $OUT/bench_mixtral_mmx.err || { echo "bench mmx rc=$?"; tail -20 $OUT/bench_mixtral_mmx.err; exit 1; }
+timeout -k 10 600 $B --pp 0 > $OUT/bench_mixtral_os2.json 2> $OUT/bench_mixtral_os2.err || { echo "bench os2 rc=$?"; exit 1; }
+for f in bench_mixtral bench_mixtral_mmx bench_mixtral_os2; do python3 -c "import json;d=json.load(open('$OUT/$f.json'));print('$f', d['value'], 'pp', d.get('pp_tok_s'), 'frac', d.get('model_bw_frac_of_8TBs'))"; done
+OUT=${OUT#gpurun_out/} bash scripts/gpu_mixtral_trace.sh > /dev/null && head -12 $OUT/mixtral_kernel_stats_summary.txt
