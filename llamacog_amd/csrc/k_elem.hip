@@ -837,6 +837,106 @@ __global__ __launch_bounds__(64) void k_moe_route(const moe_route_args a) {
     float * p = (float *) (a.probs + t * a.nb_p);
     int32_t * o = (int32_t *) (a.order + t * a.nb_o);
     const int n = a.n_exp;
+    if ((a.stage & 1) && n <= 16) {
+        // up to 16 experts (Mixtral: 8): the same arithmetic in registers. The global
+        // probabilities / order are written once at the end instead of being re-read through every
+        // pass (the exchange sort's p[o[j]] was a chain of dependent global loads: 7.3 us a launch)
+        float pv[16];
+        int32_t ov[16];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            pv[i] = i < n ? __fmul_rn(x[i], a.scale) : 0.0f;
+            if (i < n) mx = fmaxf(mx, pv[i]);
+        }
+        double s = 0.0;
+        if (n == 16) {
+            float e[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) e[k] = pv[k] = v_expf_avx512(__fsub_rn(pv[k], mx));
+            s += (double) reduce16_avx512(e);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if (i < n) {
+                    pv[i] = expf_cr(__fsub_rn(pv[i], mx));
+                    s += (double) pv[i];
+                }
+            }
+        }
+        const float inv = (float) (1.0 / s);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            pv[i] = __fmul_rn(pv[i], inv);
+            ov[i] = i;
+            if (i < n) p[i] = pv[i];
+        }
+        // the exchange sort on (value, index) pairs: sv[j] is always p[o[j]]
+        float sv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sv[i] = pv[i];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+#pragma unroll
+            for (int k = j + 1; k < 16; ++k) {
+                if (k < n && sv[j] < sv[k]) {   // GGML_SORT_ORDER_DESC
+                    const float tv = sv[j]; sv[j] = sv[k]; sv[k] = tv;
+                    const int32_t ti = ov[j]; ov[j] = ov[k]; ov[k] = ti;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) if (i < n) o[i] = ov[i];
+        if (a.stage & 2) {
+            float * wr = (float *) (a.w + t * a.nb_w);
+            double ws = 0.0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (k < a.n_used) {
+                    wr[k] = sv[k];
+                    ws += (double) sv[k];
+                }
+            }
+            if (a.wsum) {
+                const float sf = (float) ws;
+                *(float *) (a.wsum + t * a.nb_s) = sf;
+                if (a.wn) {
+                    float * nr = (float *) (a.wn + t * a.nb_n);
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) if (k < a.n_used) nr[k] = sv[k] / sf;
+                }
+            }
+        }
+        return;
+    }
+    if ((a.stage & 2) && !(a.stage & 1) && a.n_used <= 8) {
+        // stage 2 alone: the routed ids, then their probabilities, each as one batch of loads
+        int32_t oi[8];
+        float wv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) oi[k] = k < a.n_used ? o[k] : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) wv[k] = k < a.n_used ? p[oi[k]] : 0.0f;
+        float * wr = (float *) (a.w + t * a.nb_w);
+        double ws = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k < a.n_used) {
+                wr[k] = wv[k];
+                ws += (double) wv[k];
+            }
+        }
+        if (a.wsum) {
+            const float sf = (float) ws;
+            *(float *) (a.wsum + t * a.nb_s) = sf;
+            if (a.wn) {
+                float * nr = (float *) (a.wn + t * a.nb_n);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) if (k < a.n_used) nr[k] = wv[k] / sf;
+            }
+        }
+        return;
+    }
     if (a.stage & 1) {
     float mx = -INFINITY;
     for (int i = 0; i < n; ++i) {

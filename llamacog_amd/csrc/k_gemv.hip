@@ -1539,6 +1539,8 @@ static bool launch_os_t(hipStream_t st, gemv_args & a, int nmat) {
     if (!a.pro.x && wpr == 1 && !needs_epilogue(a, nmat) && !std::is_same<T, g_q6_K>::value) R = 2;
     static const int r_env = getenv("GGML_MI355X_OS_R") ? atoi(getenv("GGML_MI355X_OS_R")) : 0;
     if (r_env > 0 && !a.pro.x && wpr == 1 && !needs_epilogue(a, nmat)) R = r_env;
+    static const int r4_env = getenv("GGML_MI355X_OS_R4") ? atoi(getenv("GGML_MI355X_OS_R4")) : 0;   // A/B: K = 14336
+    if ((r4_env == 1 || r4_env == 2) && !a.pro.x && wpr == 4 && !needs_epilogue(a, nmat)) R = r4_env;
     if (wpr == 4 && needs_epilogue(a, nmat)) return false;   // rope pairs need an even group
     gemv_args b = a;
     const size_t lds = R == 4 ? os_lds_layout<T, 4, 1>(b)
