@@ -73,11 +73,6 @@ struct gemv_args {
     // one-shot body in a chained launch (k_gemv_ffn): after issuing its weight DMA the workgroup
     // waits until the FFN_SHARDS counters at dep sum to dep_n (its activation is complete)
     const int * dep; int dep_n;
-    // MUL_MAT_ID of one token (gemv_mmid, one-shot kernel only): matrix i is expert
-    // *(xids + i * xids_nb0) of the stack at W[i] (xnb02 bytes apart), read on the device; its
-    // activation column is A + i * (xqs_st, xd_st, xs_st) (0: one column shared by the slots)
-    const char * xids; int64_t xids_nb0, xnb02; int xn_as;
-    int64_t xqs_st, xd_st, xs_st;
 };
 constexpr int FFN_SHARDS = 8, FFN_SHARD_STRIDE = 32;   // ints: one 128-B line per shard
 
@@ -540,11 +535,6 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
         const int nt_w = min(WAVE, p.ntasks - WAVE * wsub);
         const int seg = (nt_w / T::per_block) * T::blk_bytes;
         const uint8_t * Wm = p.W[mi];
-        if (p.xids) {   // routed expert (uniform over the workgroup, before any barrier)
-            const int ex = *(const int32_t *) (p.xids + mi * p.xids_nb0);
-            if (ex < 0 || ex >= p.xn_as) return;
-            Wm += (int64_t) ex * p.xnb02;
-        }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint8_t * src = Wm + min(row0 + r, M - 1) * p.nb01[mi] + (int64_t) wsub * G::SEG;
@@ -564,10 +554,6 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     if constexpr (PRO) {
         gemv_act A = p.A;
         gemv_pro_finish(p, pr, (uint8_t *) xr + p.pro.lds_off, A);
-        T::load(A, tt, x);
-    } else if (p.xqs_st) {   // MUL_MAT_ID: this slot's column (a uniform branch: the plain
-        // launches keep their kernel-argument addressing, which measured ~8 % faster)
-        const gemv_act A = {p.A.qs + mi * p.xqs_st, p.A.d + mi * p.xd_st, p.A.s + mi * p.xs_st};
         T::load(A, tt, x);
     } else {
         T::load(p.A, tt, x);
@@ -1520,7 +1506,7 @@ static bool launch_osl(hipStream_t st, gemv_args & a, int nmat) {
 
 template <class T, int R, int WPR>
 static void launch_os(hipStream_t st, gemv_args & a, int nmat) {
-    if (osl_per_cu() > 0 && !needs_epilogue(a, nmat) && !a.pro.x && !a.tl.kind && !a.xids && launch_osl<T, R, WPR>(st, a, nmat)) return;
+    if (osl_per_cu() > 0 && !needs_epilogue(a, nmat) && !a.pro.x && !a.tl.kind && launch_osl<T, R, WPR>(st, a, nmat)) return;
     if (needs_epilogue(a, nmat)) launch_os_m<T, R, WPR, 1>(st, a, nmat);
     else launch_os_m<T, R, WPR, 0>(st, a, nmat);
 }
@@ -1542,8 +1528,6 @@ static bool launch_os_t(hipStream_t st, gemv_args & a, int nmat) {
     if (!a.pro.x && wpr == 1 && !needs_epilogue(a, nmat) && !std::is_same<T, g_q6_K>::value) R = 2;
     static const int r_env = getenv("GGML_MI355X_OS_R") ? atoi(getenv("GGML_MI355X_OS_R")) : 0;
     if (r_env > 0 && !a.pro.x && wpr == 1 && !needs_epilogue(a, nmat)) R = r_env;
-    static const int r4_env = getenv("GGML_MI355X_OS_R4") ? atoi(getenv("GGML_MI355X_OS_R4")) : 0;   // A/B: K = 14336
-    if ((r4_env == 1 || r4_env == 2) && !a.pro.x && wpr == 4 && !needs_epilogue(a, nmat)) R = r4_env;
     if (wpr == 4 && needs_epilogue(a, nmat)) return false;   // rope pairs need an even group
     gemv_args b = a;
     const size_t lds = R == 4 ? os_lds_layout<T, 4, 1>(b)
@@ -2092,57 +2076,6 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
     if (a.tl.qmode) ctx.qcache_put(epi->tq_key, tkq, tact);
     g_sw_gate = g_sw_up = nullptr;
     g_kt_ctx = nullptr;
-}
-
-// ---- MUL_MAT_ID of one token on the one-shot kernel ----------------------------------------------
-// The n_used routed experts of a decode step as the matrices of one launch: each workgroup reads
-// its expert id from ids on the device and streams that expert's rows (k_mmx KIND 1 does the
-// same one row per wave with register loads). Same records and walk (qtypes.h), so the same bits
-// as ggml_compute_forward_mul_mat_id (ggml-cpu.c:1466). GGML_MI355X_MMID_OS=0 keeps k_mmx.
-bool gemv_mmid(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act) {
-    static const bool on = !getenv("GGML_MI355X_MMID_OS") || atoi(getenv("GGML_MI355X_MMID_OS")) != 0;
-    const ggml_tensor * as = dst->src[0];
-    const ggml_tensor * b = dst->src[1];
-    const ggml_tensor * ids = dst->src[2];
-    const int64_t n_used = ids->ne[0];
-    if (!on || !os_enabled() || ids->ne[1] != 1 || n_used < 1 || n_used > GEMV_MAXMAT) return false;
-    if (b->ne[1] != 1 && b->ne[1] != n_used) return false;   // slot e reads column e % ne11
-    int per = 0;
-    switch (as->type) {
-        case GGML_TYPE_Q4_K: case GGML_TYPE_Q4_0:
-            if (as->ne[1] % 8 != 0) return false;   // k_mmx's vec_dot order (not repacked)
-            per = as->type == GGML_TYPE_Q4_K ? 4 : 1;
-            break;
-        case GGML_TYPE_Q5_K: case GGML_TYPE_Q6_K: per = 4; break;
-        case GGML_TYPE_Q8_0: per = 1; break;
-        default: return false;
-    }
-    const int64_t nblk = as->ne[0] / ggml_blck_size(as->type);
-    if (nblk * per > 4 * WAVE || as->nb[2] % 16 != 0) return false;
-    gemv_init();
-    g_kt_ctx = ctx.kt_buf && ktrace_enabled() ? &ctx : nullptr;
-    gemv_args a = {};
-    for (int i = 0; i < (int) n_used; ++i) {
-        a.W[i] = (const uint8_t *) as->data;
-        a.nb01[i] = as->nb[1];
-        a.M[i] = as->ne[1];
-        a.dst[i] = (float *) ((char *) dst->data + i * dst->nb[1]);
-    }
-    a.A = {act.qs, act.d, act.s};
-    a.xids = (const char *) ids->data; a.xids_nb0 = ids->nb[0]; a.xnb02 = as->nb[2]; a.xn_as = (int) as->ne[2];
-    if (b->ne[1] > 1) { a.xqs_st = act.qs_stride(); a.xd_st = act.d_stride(); a.xs_st = act.s_stride(); }
-    a.ntasks = (int) (nblk * per);
-    bool ok = false;
-    switch (as->type) {
-        case GGML_TYPE_Q4_K: ok = launch_os_t<g_q4_K>(ctx.stream, a, (int) n_used); break;
-        case GGML_TYPE_Q5_K: ok = launch_os_t<g_q5_K>(ctx.stream, a, (int) n_used); break;
-        case GGML_TYPE_Q6_K: ok = launch_os_t<g_q6_K>(ctx.stream, a, (int) n_used); break;
-        case GGML_TYPE_Q8_0: ok = launch_os_t<g_q8_0>(ctx.stream, a, (int) n_used); break;
-        case GGML_TYPE_Q4_0: ok = launch_os_t<g_q4_0>(ctx.stream, a, (int) n_used); break;
-        default: break;
-    }
-    g_kt_ctx = nullptr;
-    return ok;
 }
 
 // the SwiGLU tails' arrival counters exist (allocated outside any capture, zeroed once)
