@@ -119,11 +119,6 @@ void exec_ctx::free_scratch() {
     }
     if (fa_cnt) (void) hipFree(fa_cnt);
     fa_cnt = nullptr;
-    if (tail_cnt) (void) hipFree(tail_cnt);
-    tail_cnt = nullptr;
-    gemv_ffn_release(*this);
-    if (rsum_buf) (void) hipFree(rsum_buf);
-    rsum_buf = nullptr;
     if (kt_buf) (void) hipFree(kt_buf);
     kt_buf = nullptr;
     kt_cap = kt_off = 0;
@@ -888,7 +883,9 @@ static std::atomic<int> g_no_fuse{env_flag("GGML_MI355X_NO_FUSE")};
 static std::atomic<int> g_no_graph{env_flag("GGML_MI355X_NO_GRAPH") | env_flag("ROCPROF_KERNEL_TRACE")};
 // in-graph kernel timeline (profiling; GGML_MI355X_KTRACE=1 or ggml_backend_mi355x_set_ktrace)
 static std::atomic<int> g_ktrace{env_flag("GGML_MI355X_KTRACE")};
-struct kt_sample { long graph; int idx; const char * name; unsigned nwg; double t0, t_last_start, t1; };
+// per launch: first start, last start, last end; workgroup 0's end (a prologue launch's lead)
+// and the mean workgroup lifetime (start to its last wave's exit)
+struct kt_sample { long graph; int idx; const char * name; unsigned nwg; double t0, t_last_start, t1, t_wg0_end, wg_mean; };
 static std::mutex g_kt_mtx;
 static std::vector<kt_sample> g_kt_samples;
 static long g_kt_graphs = 0;
@@ -1051,14 +1048,24 @@ static void kt_collect(mi_backend_ctx * ctx) {
     }
     for (size_t i = 0; i < ex.kt_list.size(); ++i) {
         const auto & l = ex.kt_list[i];
-        unsigned long long s0 = ~0ull, sl = 0, e1 = 0;
+        unsigned long long s0 = ~0ull, sl = 0, e1 = 0, w0e = 0;
+        double life = 0.0;
+        unsigned nl = 0;
         for (unsigned w = 0; w < l.nwg; ++w) {
             const unsigned long long * r = h.data() + l.off + (size_t) w * l.stride;
-            if (r[0]) { s0 = std::min(s0, r[0]); sl = std::max(sl, r[0]); }
-            for (unsigned k = 1; k < l.stride; ++k) e1 = std::max(e1, r[k]);
+            unsigned long long we = 0;
+            for (unsigned k = 1; k < l.stride; ++k) we = std::max(we, r[k]);
+            if (r[0]) {
+                s0 = std::min(s0, r[0]);
+                sl = std::max(sl, r[0]);
+                if (we >= r[0]) { life += (double) (we - r[0]); ++nl; }
+            }
+            e1 = std::max(e1, we);
+            if (w == 0) w0e = we;
         }
         if (s0 == ~0ull) continue;
-        g_kt_samples.push_back({gs, (int) i, l.name, l.nwg, (s0 - base) * tick_ns, (sl - base) * tick_ns, (e1 - base) * tick_ns});
+        g_kt_samples.push_back({gs, (int) i, l.name, l.nwg, (s0 - base) * tick_ns, (sl - base) * tick_ns, (e1 - base) * tick_ns,
+                                w0e ? (w0e - base) * tick_ns : 0.0, nl ? life / nl * tick_ns : 0.0});
     }
 }
 
@@ -1077,19 +1084,13 @@ static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.done.clear();
     ex.silu_defer = ex.silu_mul = nullptr;
     ex.pro = {};
-    ex.swiglu = {};
-    ex.nsite = 0;
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) i += op_compute(ex, cgraph, i);
-    gemv_ffn_flush(ex);   // a held-back gate/up whose down projection never came
     if (ex.silu_defer) {   // a deferred SILU whose MUL never came
         op_unary(ex, ex.silu_defer);
         ex.silu_defer = ex.silu_mul = nullptr;
     }
-    // the residual sums of this graph, read by now: zero for the next graph
-    if (ex.nsite) MI_CHECK(hipMemsetAsync(ex.rsum_buf, 0, (size_t) ex.nsite * exec_ctx::SITE_DOUBLES * sizeof(double), ex.stream));
     ex.pro = {};
-    ex.swiglu = {};
 }
 
 // returns true when the graph was launched as (or captured into) a hipGraph
@@ -1525,9 +1526,10 @@ GGML_BACKEND_API int ggml_backend_mi355x_ktrace_dump(const char * path) {
     std::lock_guard<std::mutex> lk(g_kt_mtx);
     FILE * f = fopen(path, "w");
     if (!f) return -1;
-    fprintf(f, "graph,idx,kernel,nwg,start_ns,last_start_ns,end_ns\n");
+    fprintf(f, "graph,idx,kernel,nwg,start_ns,last_start_ns,end_ns,wg0_end_ns,wg_mean_ns\n");
     for (const auto & k : g_kt_samples) {
-        fprintf(f, "%ld,%d,%s,%u,%.0f,%.0f,%.0f\n", k.graph, k.idx, k.name, k.nwg, k.t0, k.t_last_start, k.t1);
+        fprintf(f, "%ld,%d,%s,%u,%.0f,%.0f,%.0f,%.0f,%.0f\n", k.graph, k.idx, k.name, k.nwg, k.t0, k.t_last_start, k.t1, k.t_wg0_end,
+                k.wg_mean);
     }
     fclose(f);
     const int n = (int) g_kt_samples.size();

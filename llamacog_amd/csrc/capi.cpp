@@ -290,18 +290,8 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv(int wtype, int64_t K, int64
 // epi_kind: 0 plain; 1 SiLU of matrix 0; 2 f16 (KV-cache) store of every matrix through a
 // dynamic-pointer slot; 3 NORM rope (Llama-3 parameters, head dim 128) of matrix 0 with its
 // f16 store
-namespace mi355x { extern unsigned long long * g_eng_prof; }
 extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int64_t M, int nmat, int copies, int iters, int epi_kind) {
     const ggml_type t = (ggml_type) wtype;
-    // GGML_MI355X_ENG_PROF=1: the engine's per-workgroup phase counters, averaged over the timed
-    // launches, go to stderr (loader waits for free slots / for landed packets; consumer waits)
-    static const bool eprof = getenv("GGML_MI355X_ENG_PROF") && atoi(getenv("GGML_MI355X_ENG_PROF")) != 0;
-    unsigned long long * ep = nullptr;
-    if (eprof) {
-        MI_CHECK(hipMalloc(&ep, 8 * 4096 * sizeof(unsigned long long)));
-        MI_CHECK(hipMemset(ep, 0, 8 * 4096 * sizeof(unsigned long long)));
-        g_eng_prof = ep;
-    }
     const size_t row = ggml_row_size(t, K);
     const size_t mat = row * (size_t) M;
     std::vector<char *> pool((size_t) copies * nmat);
@@ -430,37 +420,12 @@ extern "C" GGML_BACKEND_API double mi355x_bench_gemv2(int wtype, int64_t K, int6
     };
     run(0);   // quantizes X into the cache; later launches reuse it
     for (int i = 1; i < 4; ++i) run(i);
-    if (ep) {
-        MI_CHECK(hipStreamSynchronize(sc.ex.stream));
-        MI_CHECK(hipMemset(ep, 0, 8 * 4096 * sizeof(unsigned long long)));
-    }
     MI_CHECK(hipEventRecord(e0, sc.ex.stream));
     for (int i = 0; i < iters; ++i) run(i);
     MI_CHECK(hipEventRecord(e1, sc.ex.stream));
     MI_CHECK(hipEventSynchronize(e1));
     float ms = 0;
     MI_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    if (ep) {
-        // per launch, averaged over workgroups: loader (per loader wave) fre-wait / vmcnt-wait / total
-        // ticks and packets; consumer (per consumer wave) full-wait / total ticks and rows
-        std::vector<unsigned long long> h(8 * 4096);
-        MI_CHECK(hipMemcpy(h.data(), ep, h.size() * 8, hipMemcpyDeviceToHost));
-        double acc[8] = {0};
-        int nw = 0;
-        for (int w = 0; w < 4096; ++w) {
-            if (h[8 * w + 2] == 0 && h[8 * w + 5] == 0) continue;
-            ++nw;
-            for (int k = 0; k < 8; ++k) acc[k] += (double) h[8 * w + k];
-        }
-        if (nw) {
-            const double f = 1.0 / ((double) nw * iters);
-            fprintf(stderr, "[eng-prof] wg %d: loader waves: fre-wait %.0f vm-wait %.0f total %.0f ticks, %.1f packets | "
-                            "consumer waves: full-wait %.0f total %.0f ticks, %.1f rows (sums over the workgroup's waves)\n",
-                    nw, acc[0] * f, acc[1] * f, acc[2] * f, acc[3] * f, acc[4] * f, acc[5] * f, acc[6] * f);
-        }
-        g_eng_prof = nullptr;
-        MI_CHECK(hipFree(ep));
-    }
     MI_CHECK(hipEventDestroy(e0));
     MI_CHECK(hipEventDestroy(e1));
     for (auto p : pool) MI_CHECK(hipFree(p));

@@ -425,12 +425,19 @@ static int next_compute(ggml_cgraph * g, int p, int n) {
 static void norm_stores(ggml_cgraph * g, int n, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm,
                         bool & store_norm, bool & store_mul);
 
+// GGML_MI355X_PROLOGUE=0: the norm chains run as their own launches (k_fused.hip)
+static bool prologues_enabled() {
+    static const bool on = !getenv("GGML_MI355X_PROLOGUE") || atoi(getenv("GGML_MI355X_PROLOGUE")) != 0;
+    return on;
+}
+
 // Residual producer (k_gemv.hip): the single projection mm0 at node i is followed by
 // ADD(mm0, res) -> RMS_NORM -> [MUL w] (the residual and the next norm, build_norm in
 // src/llama-graph.cpp:464-497) whose only readers are decode mat-vecs.  The producer stores
-// x = mm0 + res (mm0 itself is dead) and the sum of squares; the consumers form the norm in
-// their prologue, so neither the RMS_NORM nor the MUL runs as a node.  Same-lane in-place
-// aliases of mm0 / res by the ADD output are safe (each row is read before it is written).
+// x = mm0 + res (mm0 itself is dead); every workgroup of the consumers' launch forms the norm
+// from x in its prologue (k_gemv.hip), so neither the RMS_NORM nor the MUL runs as a node.
+// Same-lane in-place aliases of mm0 / res by the ADD output are safe (each row is read before it
+// is written).
 static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tensor * mm0, gemv_epi & epi,
                        std::vector<const ggml_tensor *> & absorbed) {
     const int pa = next_compute(g, i, n);
@@ -462,86 +469,50 @@ static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tenso
             rows += c->ne[0];
         }
     }
-    // the one-shot GEMV forms the prologue in every workgroup: for wide consumers (the FFN
-    // gate/up, 28672 rows; the output head) that is thousands of redundant norms, and the
-    // stand-alone norm kernel plus a prologue-free launch measured faster (round 3 kernel
-    // timeline: gate/up 27.0 us with the prologue vs 15 + 4 without); Q/K/V keep it.  A persistent
-    // LDS-ring kernel that forms it once per resident workgroup measured slower still (round 3:
-    // gate/up + prologue 22.0 us, tg 393-415 vs 420-430 tok/s over five ring geometries)
-    // ... unless every reader runs on the persistent engine, which forms it once per CU
-    bool all_engine = !readers.empty();
-    for (const ggml_tensor * c : readers) all_engine = all_engine && gemv_engine_ok(c);
-    if (rows > 16384 && !all_engine) return;
+    // every consumer workgroup forms the norm: for wide consumers (the FFN gate/up, 28672 rows; the
+    // output head) that is thousands of redundant norms, and the stand-alone norm kernel plus a
+    // prologue-free launch measured faster (round 3 kernel timeline: gate/up 27.0 us with the
+    // prologue vs 15 + 4 without); Q/K/V keep it
+    if (rows > 16384) return;
     if (!dead_after(g, n, pl + 1, last, readers)) return;
     if (mul && !dead_after(g, n, pn + 1, nm, {mul})) return;
-    double * site = gemv_rsum_site(ctx);
-    if (!site) return;
     epi.rres = (const float *) res->data;
     epi.rxsum = (float *) ad->data;
-    epi.rsum = site;
     float eps;
     memcpy(&eps, nm->op_params, sizeof(float));
-    ctx.pro = {last, last->data, (const float *) ad->data, mul ? (const float *) mul->src[1]->data : nullptr, site, eps, nm->ne[0]};
+    ctx.pro = {last, last->data, 1, (const float *) ad->data, mul ? (const float *) mul->src[1]->data : nullptr, eps, nm->ne[0]};
     absorbed.push_back(ad);
     absorbed.push_back(nm);
     if (mul) absorbed.push_back(mul);
 }
 
-// GEMV tail 2: the gate/up pair of this launch is followed by SILU(gate) and MUL(silu, up)
-// (build_ffn LLM_FFN_SILU + PAR, src/llama-graph.cpp:555-616), optionally feeding the down
-// mat-vec.  Both are hoisted to this launch: checked like every hoisted node; their outputs may
-// alias the gate / up outputs only exactly (the same lane reads, then writes, each element).
-static void plan_tail_swiglu(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tensor * const * mms, gemv_epi & epi,
-                             std::vector<const ggml_tensor *> & absorbed) {
-    // FFN widths up to 16384 (Llama-3-8B 14336); the 28672-wide 70B FFN runs faster with the
-    // stand-alone product kernel (71.2 vs 69.9 tok/s, scripts/gpu_bigmodels.sh variants)
-    if (mms[0]->src[0]->type != mms[1]->src[0]->type || mms[0]->ne[0] != mms[1]->ne[0] || mms[0]->ne[0] % 256 != 0 ||
-        mms[0]->ne[0] > 16384 || mms[0]->ne[0] / 256 > exec_ctx::TAIL_CNT) return;
-    auto skipped = [&](const ggml_tensor * c) {
-        return is_view_op(c) || std::find(absorbed.begin(), absorbed.end(), c) != absorbed.end() ||
-               std::find(ctx.done.begin(), ctx.done.end(), c) != ctx.done.end();
-    };
-    int ps = -1;
-    for (int k = i + 1; k < n && k <= i + 6; ++k) {
-        ggml_tensor * c = ggml_graph_node(g, k);
-        if (skipped(c)) continue;
-        if (c->op == GGML_OP_UNARY && ggml_get_unary_op(c) == GGML_UNARY_OP_SILU && (c->src[0] == mms[0] || c->src[0] == mms[1])) ps = k;
-        break;
+// RMS_NORM (node i) of an x computed before -> [MUL w] whose only readers are decode mat-vecs
+// and whose outputs nothing else reads (the first layer's attention norm of the embedding): the
+// readers' launch forms it in its activation prologue (k_gemv.hip), no norm launch
+static bool plan_norm_prologue(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * nm = ggml_graph_node(g, i);
+    const ggml_tensor * x = nm->src[0];
+    if (!f32c(nm) || !f32c(x) || !ggml_are_same_shape(nm, x) || nm->ne[0] % 256 != 0 || nm->ne[0] > 16384 || ggml_nrows(nm) != 1)
+        return false;
+    ggml_tensor * mul = norm_weight_mul(g, i, n);
+    if (mul && (!f32c(mul) || !ggml_is_contiguous(mul->src[1]))) return false;
+    ggml_tensor * last = mul ? mul : nm;
+    const int pl = node_index(g, last);
+    ggml_tensor * mm = at(g, next_compute(g, pl, n), n);
+    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != last || !gemv_supported(mm)) return false;
+    std::vector<const ggml_tensor *> readers;
+    for (int k = pl + 1; k < n && k <= pl + 16; ++k) {
+        const ggml_tensor * c = ggml_graph_node(g, k);
+        if (c->op == GGML_OP_MUL_MAT && c->src[1] == last && gemv_supported(c)) readers.push_back(c);
     }
-    if (ps < 0) return;
-    ggml_tensor * sl = ggml_graph_node(g, ps);
-    const int tg = sl->src[0] == mms[0] ? 0 : 1, tu = 1 - tg;
-    int pm = -1;
-    for (int k = ps + 1; k < n && k <= ps + 4; ++k) {
-        ggml_tensor * c = ggml_graph_node(g, k);
-        if (skipped(c)) continue;
-        if (c->op == GGML_OP_MUL && ((c->src[0] == sl && c->src[1] == mms[tu]) || (c->src[1] == sl && c->src[0] == mms[tu]))) pm = k;
-        break;
-    }
-    if (pm < 0) return;
-    ggml_tensor * mul = ggml_graph_node(g, pm);
-    if (!f32c(sl) || !f32c(mul) || !ggml_are_same_shape(sl, mms[tg]) || !ggml_are_same_shape(mul, mms[tg])) return;
-    auto clash = [](const ggml_tensor * t, const ggml_tensor * o) {
-        return overlaps(t, o) && !(t->data == o->data && ggml_nbytes(t) == ggml_nbytes(o));
-    };
-    if (clash(sl, mms[0]) || clash(sl, mms[1]) || clash(mul, mms[0]) || clash(mul, mms[1]) || clash(mul, sl)) return;
-    const ggml_tensor * o1[1] = {sl};
-    if (!can_hoist(g, i, ps, o1, 1, absorbed)) return;
-    std::vector<const ggml_tensor *> ab2 = absorbed;
-    ab2.push_back(sl);
-    const ggml_tensor * o2[1] = {mul};
-    if (!can_hoist(g, i, pm, o2, 1, ab2)) return;
-    ggml_tensor * down = at(g, next_compute(g, pm, n), n);
-    if (down && !(down->op == GGML_OP_MUL_MAT && down->src[1] == mul && gemv_supported(down))) down = nullptr;
-    epi.tail = true;
-    epi.t_gate = tg; epi.t_up = tu;
-    epi.t_silu = sl; epi.t_mul = mul;
-    epi.t_store_silu = !dead_after(g, n, ps + 1, sl, {mul});
-    epi.t_store_mul = !(down && dead_after(g, n, pm + 1, mul, {down}));
-    epi.tq_for = down;
-    epi.tq_key = mul;
-    absorbed.push_back(sl);
-    absorbed.push_back(mul);
+    if (!dead_after(g, n, pl + 1, last, readers)) return false;
+    if (mul && !dead_after(g, n, i + 1, nm, {mul})) return false;
+    // x stays live past the readers (the residual ADD reads it), so no reader output overlaps it
+    if (dead_after(g, n, pl + 1, x, {})) return false;
+    float eps;
+    memcpy(&eps, nm->op_params, sizeof(float));
+    ctx.pro = {last, last->data, 1, (const float *) x->data, mul ? (const float *) mul->src[1]->data : nullptr, eps, nm->ne[0]};
+    return true;
 }
 
 // decode mat-vec: launch node i together with up to two later MUL_MATs on the same src1
@@ -554,15 +525,10 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     ggml_tensor * mms[3] = {mm0, nullptr, nullptr};
     gemv_epi epi;
     int nm = 1;
-    // the activation of a pending norm prologue (plan_resid at the producer)
+    // the activation of a pending prologue (planned at its producer chain)
     if (ctx.pro.last && ctx.pro.last == mm0->src[1] && ctx.pro.data == mm0->src[1]->data) {
-        epi.px = ctx.pro.x; epi.pw = ctx.pro.w; epi.psum = ctx.pro.sum; epi.peps = ctx.pro.eps; epi.pn = ctx.pro.n;
-    }
-    // the SwiGLU product this launch forms in its prologue (planned at the SILU node)
-    if (ctx.swiglu.key && ctx.swiglu.key == mm0->src[1] && ctx.swiglu.data == mm0->src[1]->data) {
-        epi.sw_gate = ctx.swiglu.gate;
-        epi.sw_up = ctx.swiglu.up;
-        ctx.swiglu = {};
+        epi.pkind = ctx.pro.kind;
+        epi.px = ctx.pro.x; epi.pw = ctx.pro.w; epi.peps = ctx.pro.eps; epi.pn = ctx.pro.n;
     }
     std::vector<const ggml_tensor *> absorbed;   // nodes this launch computes (besides node i)
     std::vector<const ggml_tensor *> outs = {mm0};
@@ -617,7 +583,7 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     add_epilogues(0, i);
     settle(0, i);
 
-    for (int j = i + 1; j < n && j <= i + 12 && nm < 3 && !epi.sw_gate; ++j) {
+    for (int j = i + 1; j < n && j <= i + 12 && nm < 3; ++j) {
         ggml_tensor * c = ggml_graph_node(g, j);
         if (c->op != GGML_OP_MUL_MAT || c->src[1] != mm0->src[1] || !gemv_supported(c)) continue;
         if (std::find(ctx.done.begin(), ctx.done.end(), c) != ctx.done.end()) continue;
@@ -668,22 +634,14 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
         fprintf(stderr, "\n");
     }
     // the next norm chain moves into this launch (residual producer) and its consumers
-    // (prologue); silu(gate) * up into the gate/up launch (SwiGLU tail).  GGML_MI355X_TAILS=0 /
-    // GGML_MI355X_RESID=0 run those chains as their own launches (k_fused.hip)
-    // the SwiGLU tail measured slower than the stand-alone product kernel in the replayed graph
-    // (in-graph kernel timeline, round 3: 2725 vs 2673 us per Llama-3-8B token): opt-in
-    static const bool tails = getenv("GGML_MI355X_TAILS") && atoi(getenv("GGML_MI355X_TAILS")) != 0;
+    // (prologue).  GGML_MI355X_RESID=0 runs the chain as its own launch (k_fused.hip)
     static const bool resid = !getenv("GGML_MI355X_RESID") || atoi(getenv("GGML_MI355X_RESID")) != 0;
     bool plain = true;
     for (int m = 0; m < nm; ++m) {
         plain = plain && !epi.silu[m] && !epi.rope[m] && !epi.f16out[m] && !epi.rope_f16[m] && !epi.elide_dst[m];
     }
-    if (resid && plain && nm == 1) plan_resid(ctx, g, i, n, mm0, epi, absorbed);
-    if (tails && plain && nm == 2 && gemv_tail_ready(ctx)) plan_tail_swiglu(ctx, g, i, n, mms, epi, absorbed);
-    if (dbg && (epi.tail || epi.rres || epi.px)) {
-        fprintf(stderr, "[mi355x]   tail=%d -> %s resid=%d prologue=%d\n", epi.tail, epi.tq_for ? epi.tq_for->name : "(none)",
-                epi.rres != nullptr, epi.px != nullptr);
-    }
+    if (resid && prologues_enabled() && plain && nm == 1) plan_resid(ctx, g, i, n, mm0, epi, absorbed);
+    if (dbg && (epi.rres || epi.px)) fprintf(stderr, "[mi355x]   resid=%d prologue=%d\n", epi.rres != nullptr, epi.px != nullptr);
     gemv_group(ctx, mms, nm, &epi);
     // node i+1 when it is node i's SiLU is consumed here; everything else is skipped later
     const bool next_absorbed = epi.silu[0] && epi.silu[0] == at(g, i + 1, n);
@@ -849,8 +807,6 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             return 1;
         }
     }
-    // a held-back gate/up (chained FFN launch) goes out before any other node that computes
-    if (ctx.ffn_down && node != ctx.ffn_down && !is_view_op(node)) gemv_ffn_flush(ctx);
     const int n = ggml_graph_n_nodes(cgraph);
     switch (node->op) {
         case GGML_OP_NONE:
@@ -878,6 +834,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             // src/llama-graph.cpp:464-497); the norm output is still written, so other
             // readers of it stay correct.
             ggml_tensor * mul = norm_weight_mul(cgraph, i, n);
+            if (fusion_enabled() && prologues_enabled() && plan_norm_prologue(ctx, cgraph, i, n)) return mul ? 2 : 1;
             if (fusion_enabled()) {
                 ggml_tensor * mm = at(cgraph, i + (mul ? 2 : 1), n);
                 bool sn, sm;
@@ -972,15 +929,6 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                         ggml_tensor * mm = at(cgraph, j + 1, n);
                         const bool ssilu = !dead_after(cgraph, n, i + 1, node, {c});
                         const bool smul = !(mm && mm->op == GGML_OP_MUL_MAT && dead_after(cgraph, n, j + 1, c, {mm}));
-                        // the down projection right behind, on the engine, and nothing else reading the
-                        // SILU or the product: the engine forms silu(gate) * up in its prologue
-                        const ggml_tensor * gate = node->src[0], * up = c->src[1];
-                        if (j == i + 1 && !ssilu && !smul && mm->src[1] == c && f32c(gate) && f32c(up) && f32c(c) &&
-                            ggml_are_same_shape(gate, up) && ggml_are_same_shape(c, gate) && ggml_nrows(c) == 1 &&
-                            c->ne[0] % 256 == 0 && c->ne[0] <= 16384 && gemv_engine_ok(mm)) {
-                            ctx.swiglu = {c, c->data, (const float *) gate->data, (const float *) up->data};
-                            return 2;
-                        }
                         if (fused_silu_mul_quant(ctx, node, c, mm, ssilu, smul)) {
                             if (j == i + 1) return 2;
                             ctx.done.push_back(c);

@@ -107,15 +107,6 @@ __device__ __forceinline__ uint32_t f16_mad(uint32_t vbits, float vs, uint32_t y
     return r;
 }
 
-// the same with v held as a half (a ds_read_u16 result used as it is: no zero-extension mask)
-__device__ __forceinline__ uint32_t f16_mad_h(_Float16 v, float vs, uint32_t ybits) {
-    float t;
-    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(v), "v"(vs), "v"(ybits));
-    uint32_t r;
-    asm("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(t));
-    return r;
-}
-
 // y = f16(f32(y) * ms): v_fma_mix_f32 with a -0 addend is the product rounded once to f32 (as
 // the CPU's _mm512_mul_ps of the converted halves), then the f16 rounding (vec_scale_f16)
 // (the -0 addend comes in a register: -0.0 is not an inline constant, and a +0 addend would turn
@@ -1511,28 +1502,15 @@ __device__ __forceinline__ float fal_dmax(float v) {
     return fmaxf(v, __int_as_float(t));
 }
 
-#ifndef FAL_EXP
-#define FAL_EXP 0
-#endif
-#ifndef FAL_H16
-#define FAL_H16 0   // V values held as halves in the chain (1; measured 7 % slower at 4096) or as 32-bit words (0)
-#endif
-#if FAL_H16
-typedef _Float16 fal_v16;
-#define FAL_MAD f16_mad_h
-#else
+// the chain holds the f16 V values as 32-bit words (as halves it measured 7 % slower at 4096)
 typedef uint32_t fal_v16;
 #define FAL_MAD f16_mad
-#endif
 template <int VT, int NM>   // V type: 0 f16, 1 q8_0, 2 q4_0; NM: positions held (n_kv <= NM)
 __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, const float * __restrict__ sco) {
     using SM = fal_smem<VT, NM>;
     constexpr int D = 128, NB = D / 32, CV = SM::CV, U = FAL_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     kt_enter(a.kt);
-#if FAL_EXP & 4
-    const unsigned long long e_t0 = __builtin_amdgcn_s_memtime();
-#endif
     // FAL_DSPLIT workgroups per head, each the recurrence of DH of its dims: V is staged through
     // the CU's LDS-DMA at ~25 GB/s per CU (MI355X_MICROARCH.md ldsdma-fill), so one CU per head
     // spent most of the chain waiting for its V stages; the split halves every CU's bytes while
@@ -1641,14 +1619,8 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             run = fmaxf(run, tot[i]);
         }
     }
-#if FAL_EXP & 4
-    const unsigned long long e_ta = __builtin_amdgcn_s_memtime();
-#endif
     if (lane == 0) { sm.wmax[wave] = run; sm.wlast[wave] = wlast; }
     __syncthreads();   // (also publishes exptab)
-#if FAL_EXP & 4
-    const unsigned long long e_tb = __builtin_amdgcn_s_memtime();
-#endif
     float Mprev = -INFINITY;
     for (int w2 = 0; w2 < wave; ++w2) Mprev = fmaxf(Mprev, sm.wmax[w2]);
     int nrun = max(max(sm.wlast[0], sm.wlast[1]), max(sm.wlast[2], sm.wlast[3])) + 1;
@@ -1694,9 +1666,6 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
         sm.cm[j] = cmv;
         sm.sc[j] = scv;
     };
-#if FAL_EXP & 4
-    const unsigned long long e_tc = __builtin_amdgcn_s_memtime();
-#endif
     __syncthreads();   // M / s and the dead bits of every position are in
     nrun = __builtin_amdgcn_readfirstlane(nrun);   // uniform (from LDS): scalar loop control below
     const int nchunk = (nrun + CV - 1) / CV;
@@ -1714,25 +1683,11 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     uint32_t yb = 0;     // f16 bits (f16 V)
     float yf = 0.0f;     // f32 accumulator (quantized V)
     float S = 0.0f;
-#if FAL_EXP & 4
-    // phase clocks of workgroup 0's chain wave (time-split experiments only): start of the
-    // recurrence, summed barrier waits, end
-    const unsigned long long e_t1 = __builtin_amdgcn_s_memtime();
-    unsigned long long e_wait = 0;
-#endif
     for (int c = 0; c < nchunk; ++c) {
         const int st = c % NSTG;
         // this wave's stage-c instructions have landed (those of c + 1 may still be in flight)
-        // FAL_EXP (time-split experiments only, wrong results): 1 no recurrence, 2 no staging wait,
-        // 4 phase clocks
-        if (wave >= 1 && !(FAL_EXP & 2)) eng_vm_wait_fa(pend);
-#if FAL_EXP & 4
-        const unsigned long long e_b0 = __builtin_amdgcn_s_memtime();
-#endif
+        if (wave >= 1) eng_vm_wait_fa(pend);
         __syncthreads();   // stage c is in; every chain lane is done with chunk c - 1's stage
-#if FAL_EXP & 4
-        e_wait += __builtin_amdgcn_s_memtime() - e_b0;
-#endif
         if (wave >= 1) {
             pend = c + 2 < nchunk ? stage((c + 2) % NSTG, (int64_t) (c + 2) * CV, min(CV, nrun - (c + 2) * CV)) : 0;
             // the next chunk's coefficients, by one stager wave in turn, while the chain runs this one
@@ -1742,7 +1697,6 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             }
             continue;
         }
-        if (FAL_EXP & 1) continue;
         const int jc = c * CV;                  // first position of the chunk
         const int nr = min(CV, nrun - jc);      // positions to run
         const int nb = (nr + U - 1) / U;
@@ -1763,7 +1717,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             }
         };
         if constexpr (VT == 0) {
-            const auto * vrow = (const std::conditional_t<FAL_H16, _Float16, uint16_t> *) sm.vr[st] + d;
+            const auto * vrow = (const uint16_t *) sm.vr[st] + d;
             auto ldb = [&](int j, fal_v16 (&vv)[U], float (&vs)[U]) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) vv[u] = vrow[(j + u) * DH];
@@ -1888,11 +1842,6 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
         }
     }
 
-#if FAL_EXP & 4
-    if (blockIdx.x == 0 && tid == 0)
-        printf("[fal] n %d chunks %d: scan %llu exchange %llu M-pass %llu rest %llu, loop %llu ticks (barrier waits %llu)\n", nrun,
-               nchunk, e_ta - e_t0, e_tb - e_ta, e_tc - e_tb, e_t1 - e_tc, __builtin_amdgcn_s_memtime() - e_t1, e_wait);
-#endif
     // ---- output and its optional quantization (k_fattn_exact's epilogue) ----
     // (wave 0 holds the workgroup's DH outputs, dims DH·dh ..)
     float * drow = (float *) ((char *) a.dst + h * a.nb1_dst + iq3 * a.nb2_dst) + DH * dh;

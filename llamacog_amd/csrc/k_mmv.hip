@@ -492,6 +492,7 @@ bool mul_mat_id_supported(const ggml_tensor * op) {
 bool mmq_id_supported(const ggml_tensor * dst);
 void mul_mat_q_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, const int32_t * cnt, const int32_t * off,
                   const int32_t * list, int64_t n_pairs);
+bool gemv_mmid(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act);
 
 void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst) {
     const ggml_tensor * as = dst->src[0];
@@ -525,6 +526,11 @@ void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst) {
         if (!ctx.qcache_get(b, kq, act)) {
             quantize_act(ctx, b, kq, act, exec_ctx::QSLOT);
             ctx.qcache_put(b, kq, act);
+        }
+        // one token: the routed experts as one one-shot launch (k_gemv.hip, its ID instance)
+        if (T == 1 && gemv_mmid(ctx, dst, act)) {
+            if (ctx.timing) ctx.time_end(TK_MMV, bytes, ev_beg);
+            return;
         }
     } else {
         auto al = [](size_t v) { return (v + 255) & ~size_t(255); };

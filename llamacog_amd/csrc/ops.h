@@ -41,30 +41,12 @@ struct exec_ctx {
     // arrival counters of the flash-attention output quantization (k_fattn_exact.hip)
     static constexpr int FA_CNT = 1024;
     int *   fa_cnt = nullptr;
-    // arrival counters of the GEMV tails (k_gemv.hip: the last workgroup runs the next node's
-    // producer chain), TAIL_CNT words each on its own 4-KiB line; zeroed once, self-resetting
-    static constexpr int TAIL_CNT = 256;
-    int *   tail_cnt = nullptr;
-    // residual producer -> norm prologue hand-off (k_gemv.hip): per site 64 double sums (128 B
-    // apart) that the producer's workgroups add to and the consumer's read; zeroed at the end of
-    // every graph (run_nodes), so each graph starts from zero
-    static constexpr int MAX_SITES = 256, SITE_DOUBLES = 1024;
-    double * rsum_buf = nullptr;
-    int      nsite = 0;
-    // the pending prologue: RMS_NORM chain `last` (and its data pointer) whose consumers form
-    // their activation from x, w and sum
-    struct pro_pending { const ggml_tensor * last; const void * data; const float * x; const float * w; const double * sum;
+    // the pending prologue: the chain whose output `last` (and its data pointer) the next decode
+    // mat-vecs read; they form it from x and w in their launch (kind 1: RMS_NORM(x) [* w])
+    // instead of a launch of its own (dispatch.cpp)
+    struct pro_pending { const ggml_tensor * last; const void * data; int kind; const float * x; const float * w;
                          float eps; int64_t n; };
     pro_pending pro = {};
-    // SwiGLU prologue pending for the down projection that reads `key` (the MUL of silu(gate)
-    // and up): its engine launch forms silu(gate) * up and the quantized activation itself, so
-    // the SILU and the MUL never run as nodes (dispatch.cpp, GGML_OP_UNARY)
-    // chained FFN launch (k_gemv.hip k_gemv_ffn): the held-back gate/up's state and the down
-    // projection it waits for (nullptr: nothing held back)
-    void * ffn = nullptr;
-    const ggml_tensor * ffn_down = nullptr;
-    struct swiglu_pending { const ggml_tensor * key; const void * data; const float * gate; const float * up; };
-    swiglu_pending swiglu = {};
 
     void * scratch(int slot, size_t bytes);
     void   free_scratch();
@@ -75,13 +57,6 @@ struct exec_ctx {
     // ggml node (and its data pointer) and cleared at the start of every graph_compute,
     // because libllama re-uses node objects across graphs.
     static constexpr int QSLOT = 0;
-    // a GEMV tail quantizes its result for the NEXT launch while other workgroups of its own
-    // launch may still read the launch's input: it writes the other of the two slots
-    static constexpr int QSLOT2 = 4;
-    int qslot_of(const void * p) const {
-        return slot_ptr[QSLOT2] && (const char *) p >= (const char *) slot_ptr[QSLOT2] &&
-               (const char *) p < (const char *) slot_ptr[QSLOT2] + slot_size[QSLOT2] ? QSLOT2 : QSLOT;
-    }
     const ggml_tensor * qc_tensor = nullptr;
     const void *        qc_data   = nullptr;
     bool                qc_kquant = false;
@@ -224,29 +199,16 @@ struct gemv_epi {
     // overwritten): not stored
     bool elide_dst[3]  = {false, false, false};   // the projection itself
     bool elide_rope[3] = {false, false, false};   // its rope (kept only as the f16 cache row)
-    // SwiGLU tail (k_gemv.hip gemv_tail): SILU(matrix t_gate) * matrix t_up, quantized for the
-    // consumer tq_for (nullptr: not quantized) under the cache key tq_key
-    bool tail = false;
-    ggml_tensor * t_silu = nullptr; ggml_tensor * t_mul = nullptr;
-    int t_gate = 0, t_up = 1;
-    bool t_store_mul = true, t_store_silu = true;
-    const ggml_tensor * tq_for = nullptr;
-    const ggml_tensor * tq_key = nullptr;
-    // residual producer (one matrix): x = out + rres stored to rxsum, sum of squares to rsum
-    const float * rres = nullptr; float * rxsum = nullptr; double * rsum = nullptr;
-    // norm prologue: the activation is quant(RMS_NORM(px) [* pw]) with the producer's sums psum
-    const float * px = nullptr; const float * pw = nullptr; const double * psum = nullptr;
+    // residual producer (one matrix): x = out + rres stored to rxsum
+    const float * rres = nullptr; float * rxsum = nullptr;
+    // norm prologue: the activation is quant(RMS_NORM(px) [* pw]) (pkind 1), formed by every
+    // workgroup of the launch (k_gemv.hip)
+    int pkind = 0;
+    const float * px = nullptr; const float * pw = nullptr;
     float peps = 0.0f; int64_t pn = 0;
-    // SwiGLU prologue (engine only): the activation is quant(silu(sw_gate) * sw_up)
-    const float * sw_gate = nullptr; const float * sw_up = nullptr;
 };
 bool gemv_supported(const ggml_tensor * mm);
-bool gemv_tail_ready(exec_ctx & ctx);
-void gemv_ffn_flush(exec_ctx & ctx);     // launch a held-back gate/up alone (k_gemv.hip)
-void gemv_ffn_release(exec_ctx & ctx);
-double * gemv_rsum_site(exec_ctx & ctx);   // a zeroed site of rsum_buf, or nullptr
 bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
-bool gemv_engine_ok(const ggml_tensor * mm);     // the persistent engine (k_gemv_eng) takes this mat-vec
 void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi);
 bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c);   // c may join mm0's launch as a second weight type
 

@@ -15,7 +15,7 @@ namespace mi355x {
 // non-negative floats' bits, then the lowest index holding it (== the sequential strict '>'
 // scan), whose value is read from its lane.  All 64 lanes must be active.
 // WT: every store write-through (agent-scope relaxed atomics), for a reader in the same launch
-// that waits on a counter (k_gemv_ffn's down projection); bsums then go two to a dword
+// that waits on a counter; bsums then go two to a dword
 template <bool WT = false>
 __device__ __forceinline__ void q8K_wave(const float (&vv)[4], int lane, int8_t * q, int16_t * bsum, float * d) {
     auto st32 = [](void * p, uint32_t v) {

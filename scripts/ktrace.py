@@ -44,7 +44,7 @@ def main():
     graphs = collections.defaultdict(list)
     for r in rows:
         graphs[int(r["graph"])].append(r)
-    stats = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0])   # n, dur, ramp, gap_before, nwg
+    stats = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0, 0, 0.0, 0.0])   # n, dur, ramp, gap_before, nwg, wg0 end, wg life
     spans, busy = [], []
     for g, rs in graphs.items():
         rs.sort(key=lambda r: int(r["idx"]))
@@ -58,15 +58,18 @@ def main():
             s[2] += tl - t0
             s[3] += (t0 - prev_end) if prev_end is not None else 0.0
             s[4] = int(r["nwg"])
+            s[5] += float(r.get("wg0_end_ns", 0) or 0) - t0
+            s[6] += float(r.get("wg_mean_ns", 0) or 0)
             b += t1 - t0
             prev_end = t1
         spans.append(float(rs[-1]["end_ns"]) - float(rs[0]["start_ns"]))
         busy.append(b)
     ng = len(graphs)
     print(f"{a.config}: {ng} graphs ({n} launch records), depth {a.depth}")
-    print(f"{'launch':24s} {'per tok':>7s} {'nwg':>5s} {'mean us':>8s} {'ramp us':>8s} {'gap before us':>14s}")
-    for k, (cnt, d, rp, gp, nwg) in sorted(stats.items(), key=lambda kv: -kv[1][1]):
-        print(f"{k:24s} {cnt / ng:7.1f} {nwg:5d} {d / cnt / 1e3:8.2f} {rp / cnt / 1e3:8.2f} {gp / cnt / 1e3:14.2f}")
+    print(f"{'launch':24s} {'per tok':>7s} {'nwg':>5s} {'mean us':>8s} {'ramp us':>8s} {'gap before us':>14s} {'wg0 end us':>10s} {'wg life us':>10s}")
+    for k, (cnt, d, rp, gp, nwg, w0, wl) in sorted(stats.items(), key=lambda kv: -kv[1][1]):
+        print(f"{k:24s} {cnt / ng:7.1f} {nwg:5d} {d / cnt / 1e3:8.2f} {rp / cnt / 1e3:8.2f} {gp / cnt / 1e3:14.2f} "
+              f"{w0 / cnt / 1e3:10.2f} {wl / cnt / 1e3:10.2f}")
     sp, bu = sum(spans) / ng / 1e3, sum(busy) / ng / 1e3
     print(f"per token: span {sp:.1f} us (first instrumented start -> last end), instrumented kernels {bu:.1f} us, "
           f"gaps + other kernels {sp - bu:.1f} us")

@@ -94,6 +94,30 @@ def test_greedy_llama3_8b_2layer_prompt512():
     _check(_greedy("llama3-8b-2l-q4km", 512, 8, True))
 
 
+def test_greedy_llama3_8b_full_depth_q4km():
+    """The model bench.py times (BASELINE.json configs[1] / [2]): all 32 layers of Llama-3-8B
+    Q4_K_M, where the use_more_bits alternation of Q4_K / Q6_K attn_v and ffn_down over the layers
+    (src/llama-quant.cpp:185-187: 16 Q6_K layers) and the Q6_K output head appear together.  A
+    32-token prompt (MFMA prefill tiles) then 16 greedy tokens (the replayed decode graph): ids and
+    every logit bit-identical to the CPU backend (tools/main/main.cpp --temp 0's selection)."""
+    _check(_greedy("llama3-8b-q4km", 32, 16, True))
+
+
+def test_greedy_mixtral_full_depth_q5km():
+    """All 32 layers of Mixtral-8x7B Q5_K_M (BASELINE.json configs[4]): 8 experts per layer with
+    top-2 routing, Q5_K experts, the use_more_bits Q6_K ffn_down layers and Q8_0 attn_k / attn_v
+    (src/llama-quant.cpp:300-311); prompt 16 (expert-sorted batch MUL_MAT_ID) then 4 decode steps,
+    bit-identical to the CPU backend."""
+    _check(_greedy("mixtral-8x7b-q5km", 16, 4, True))
+
+
+def test_greedy_llama3_70b_full_depth_q4km():
+    """All 80 layers of Llama-3-70B Q4_K_M (BASELINE.json configs[3], here on one GPU: 41.9 GB of
+    weights in one 288 GB HBM): attn_v Q5_K / Q6_K by the 70B rule, the Q4_K / Q6_K ffn_down
+    alternation at K = 28672; prompt 8 then 2 decode steps, bit-identical to the CPU backend."""
+    _check(_greedy("llama3-70b-q4km", 8, 2, True))
+
+
 def test_greedy_llama3_70b_2layer_q4km():
     """Llama-3-70B layer shapes (BASELINE.json configs[3]): n_embd 8192, FFN 28672, 64 / 8 heads,
     attn_v Q5_K (layer 0, the 70B rule) and Q6_K (layer 1), ffn_down Q4_K and Q6_K at K = 28672
