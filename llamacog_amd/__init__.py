@@ -35,6 +35,9 @@ def _require(path: str, what: str) -> str:
 
 def plugin_lib() -> ctypes.CDLL:
     """The MI355X plugin as a ctypes library (same dlopen handle libllama uses)."""
+    base = os.path.join(REFHOST, "libggml-base.so")
+    if os.path.exists(base):   # an A/B build outside the tree has no rpath to it
+        ctypes.CDLL(base, mode=ctypes.RTLD_GLOBAL)
     lib = ctypes.CDLL(_require(PLUGIN, "MI355X backend plugin"), mode=ctypes.RTLD_GLOBAL)
     lib.ggml_backend_mi355x_get_timing.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]

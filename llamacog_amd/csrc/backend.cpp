@@ -907,6 +907,8 @@ unsigned long long * exec_ctx::kt_take(const char * name, unsigned nwg, unsigned
 
 bool fusion_enabled() { return g_no_fuse.load(std::memory_order_relaxed) == 0; }
 bool graphs_enabled() { return g_no_graph.load(std::memory_order_relaxed) == 0; }
+// GGML_MI355X_DEBUG_OPS=1: every dispatched node and stand-alone activation quantize on stderr
+bool debug_ops() { static const bool on = env_flag("GGML_MI355X_DEBUG_OPS"); return on; }
 }
 
 static void graph_signature(ggml_cgraph * cgraph, std::vector<int64_t> & sig) {
@@ -1084,8 +1086,10 @@ static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.done.clear();
     ex.silu_defer = ex.silu_mul = nullptr;
     ex.pro = {};
+    ex.moe = {};
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) i += op_compute(ex, cgraph, i);
+    GGML_ASSERT(!ex.moe.comb);   // a deferred combine always meets its residual ADD
     if (ex.silu_defer) {   // a deferred SILU whose MUL never came
         op_unary(ex, ex.silu_defer);
         ex.silu_defer = ex.silu_mul = nullptr;

@@ -689,7 +689,13 @@ static int op_rope_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
 // quantize launch of its own
 static ggml_tensor * moe_quant_consumer(ggml_cgraph * g, int n, const ggml_tensor * out, const ggml_tensor * mm,
                                         const ggml_tensor ** qkey) {
-    if (!mm || mm->op != GGML_OP_MUL_MAT || mmv_q_supported_type(mm->src[0]->type)) return nullptr;
+    // the router may follow the norm behind views (build_moe_ffn reshapes cur for the experts
+    // first, src/llama-graph.cpp:682)
+    if (mm && is_view_op(mm)) {
+        const int lim = node_index(g, mm) + 4;
+        for (int k = node_index(g, mm); mm && is_view_op(mm) && k < lim;) mm = at(g, ++k, n);
+    }
+    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != out || mmv_q_supported_type(mm->src[0]->type)) return nullptr;
     const int p = node_index(g, mm);
     for (int k = p + 1; k < n && k <= p + 16; ++k) {
         ggml_tensor * c = ggml_graph_node(g, k);
@@ -700,6 +706,18 @@ static ggml_tensor * moe_quant_consumer(ggml_cgraph * g, int n, const ggml_tenso
             return c;
         }
         return nullptr;
+    }
+    return nullptr;
+}
+
+// a later MUL_MAT reading the same output `out` with another weight type than the first reader
+// mm (Mixtral: Q8_0 attn_k / attn_v after the Q5_K attn_q), or nullptr
+static const ggml_tensor * other_type_reader(ggml_cgraph * g, int n, const ggml_tensor * out, const ggml_tensor * mm) {
+    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != out) return nullptr;
+    const int p = node_index(g, mm);
+    for (int k = p + 1; k < n && k <= p + 12; ++k) {
+        const ggml_tensor * c = ggml_graph_node(g, k);
+        if (c->op == GGML_OP_MUL_MAT && c->src[1] == out && c->src[0]->type != mm->src[0]->type) return c;
     }
     return nullptr;
 }
@@ -748,27 +766,125 @@ static bool try_moe_sort(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
 }
 
 // The expert outputs weighted and summed (build_moe_ffn :761-777, n_used = 2): MUL(experts,
-// weights) followed, after views only, by the ADD of its two slot views.  One launch; the MUL
-// output is not stored when only that ADD reads it.
-static bool try_moe_combine(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+// weights) followed, after views only, by the ADD of its two slot views: that ADD, or nullptr.
+// The MUL output is never stored, so only that ADD may read it.
+static ggml_tensor * moe_combine_sum(ggml_cgraph * g, int i, int n) {
     ggml_tensor * mul = ggml_graph_node(g, i);
     const ggml_tensor * e = mul->src[0], * w = mul->src[1];
-    if (!f32c(mul) || !f32c(e) || !w || w->type != GGML_TYPE_F32 || mul->ne[1] != 2 || w->ne[0] != 1 || w->ne[1] != 2 ||
-        w->ne[2] != mul->ne[2] || mul->ne[3] != 1 || !ggml_are_same_shape(mul, e)) return false;
+    if (mul->op != GGML_OP_MUL || !f32c(mul) || !f32c(e) || !w || w->type != GGML_TYPE_F32 || mul->ne[1] != 2 || w->ne[0] != 1 ||
+        w->ne[1] != 2 || w->ne[2] != mul->ne[2] || mul->ne[3] != 1 || !ggml_are_same_shape(mul, e)) return nullptr;
     for (int j = i + 1; j < n && j <= i + 6; ++j) {
         ggml_tensor * c = ggml_graph_node(g, j);
         if (is_view_op(c)) continue;
-        if (c->op != GGML_OP_ADD || !f32c(c) || base_of(c->src[0]) != mul || base_of(c->src[1]) != mul) return false;
+        if (c->op != GGML_OP_ADD || !f32c(c) || base_of(c->src[0]) != mul || base_of(c->src[1]) != mul) return nullptr;
         const ggml_tensor * v0 = c->src[0], * v1 = c->src[1];
-        if (v0->data != mul->data || (const char *) v1->data != (const char *) mul->data + mul->nb[1]) return false;
+        if (v0->data != mul->data || (const char *) v1->data != (const char *) mul->data + mul->nb[1]) return nullptr;
         if (v0->ne[0] != mul->ne[0] || v0->ne[1] != mul->ne[2] || v0->nb[1] != mul->nb[2] || v1->nb[1] != mul->nb[2] ||
-            c->ne[0] != mul->ne[0] || c->ne[1] != mul->ne[2]) return false;
-        if (!dead_after(g, n, i + 1, mul, {c}) || overlaps(c, e) || overlaps(c, w)) return false;
-        moe_combine(ctx, mul, c);
-        ctx.done.push_back(c);
-        return true;
+            c->ne[0] != mul->ne[0] || c->ne[1] != mul->ne[2]) return nullptr;
+        if (!dead_after(g, n, i + 1, mul, {c}) || overlaps(c, e) || overlaps(c, w)) return nullptr;
+        return c;
     }
-    return false;
+    return nullptr;
+}
+
+// the combine as its own launch, or — after the fused router (ctx.moe) — deferred into the
+// residual ADD -> RMS_NORM launch that is the only reader of its slot sum (k_norm_fused's
+// combine source: the sum is never stored)
+static bool try_moe_combine(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * mul = ggml_graph_node(g, i);
+    const bool routed = ctx.moe.mul == mul;
+    ggml_tensor * c = moe_combine_sum(g, i, n);
+    if (!c) {
+        GGML_ASSERT(!routed);   // try_moe_router checked this same pattern
+        return false;
+    }
+    ctx.done.push_back(c);
+    if (routed) {
+        const ggml_tensor * e = mul->src[0];
+        const int ir = next_compute(g, node_index(g, c), n);
+        const ggml_tensor * r = at(g, ir, n);
+        const ggml_tensor * nx = at(g, ir + 1, n);
+        const bool dense = e->nb[1] == (size_t) e->ne[0] * sizeof(float) && e->nb[2] == 2 * e->nb[1];
+        if (dense && r && r->op == GGML_OP_ADD && (r->src[0] == c || r->src[1] == c) && nx && nx->op == GGML_OP_RMS_NORM &&
+            nx->src[0] == r && dead_after(g, n, node_index(g, c) + 1, c, {r}) &&
+            std::find(ctx.done.begin(), ctx.done.end(), r) == ctx.done.end() &&
+            c->ne[1] == 1) {   // one token: one workgroup reads e before any output is stored
+            ctx.moe.comb = c;
+            ctx.moe.e = (const float *) e->data;
+            return true;
+        }
+    }
+    moe_combine(ctx, mul, c, routed ? ctx.moe.wn : nullptr);
+    if (routed) ctx.moe = {};
+    return true;
+}
+
+// a deferred combine (ctx.moe.comb) whose consumer did not take it: launch it now
+static void flush_moe_combine(exec_ctx & ctx) {
+    if (!ctx.moe.comb) return;
+    moe_combine(ctx, ctx.moe.mul, (ggml_tensor *) ctx.moe.comb, ctx.moe.wn);
+    ctx.moe = {};
+}
+
+// The MoE router in one launch (k_moe_router): at the router's f32 MUL_MAT, its SOFT_MAX and the
+// ARGSORT (ggml_top_k) follow after views only.  When the GET_ROWS of the probabilities by the
+// top-k, its SUM_ROWS and DIV are read by nothing but the combine MUL, those three are formed in
+// the same launch into a private scratch and skipped at their own nodes; the combine reads it.
+static bool try_moe_router(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * mm = ggml_graph_node(g, i);
+    if (mm->src[0]->type != GGML_TYPE_F32 || mm->src[0]->ne[1] > 16) return false;
+    const int is = next_compute(g, i, n);
+    ggml_tensor * sm = at(g, is, n);
+    if (!sm || sm->op != GGML_OP_SOFT_MAX || sm->src[0] != mm || sm->src[1] || sm->src[2]) return false;
+    float max_bias = 0.0f;
+    memcpy(&max_bias, (const float *) sm->op_params + 1, sizeof(float));
+    if (max_bias != 0.0f || !f32c(sm)) return false;
+    const int ia = next_compute(g, is, n);
+    ggml_tensor * as = at(g, ia, n);
+    if (!as || as->op != GGML_OP_ARGSORT || as->src[0] != sm || as->op_params[0] != GGML_SORT_ORDER_DESC || as->type != GGML_TYPE_I32)
+        return false;
+    // the weights chain and its combine
+    ggml_tensor * gr = nullptr, * sr = nullptr, * dv = nullptr, * mul = nullptr;
+    for (int k = ia + 1; k < n && k <= ia + 48 && !gr; ++k) {
+        ggml_tensor * c = ggml_graph_node(g, k);
+        if (c->op == GGML_OP_GET_ROWS && base_of(c->src[0]) == sm && base_of(c->src[1]) == as) gr = c;
+    }
+    if (gr) {
+        const int k1 = next_compute(g, node_index(g, gr), n);
+        sr = at(g, k1, n);
+        if (sr && sr->op == GGML_OP_SUM_ROWS && base_of(sr->src[0]) == gr && sr->type == GGML_TYPE_F32) {
+            dv = at(g, next_compute(g, k1, n), n);
+            if (!dv || dv->op != GGML_OP_DIV || base_of(dv->src[0]) != gr || dv->src[1] != sr || dv->type != GGML_TYPE_F32) dv = nullptr;
+        } else {
+            sr = nullptr;
+        }
+    }
+    if (dv) {
+        const int id = node_index(g, dv);
+        for (int k = id + 1; k < n && k <= id + 8; ++k) {
+            ggml_tensor * c = ggml_graph_node(g, k);
+            if (is_view_op(c)) continue;
+            if (c->op == GGML_OP_MUL && base_of(c->src[1]) == dv && moe_combine_sum(g, k, n)) mul = c;
+            break;
+        }
+    }
+    const int64_t T = mm->src[1]->ne[1];
+    const int n_used = gr ? (int) gr->ne[1] : 0;
+    const bool chain = mul && n_used == 2 && gr->ne[0] == 1 && gr->ne[2] == T && ggml_is_contiguous(gr) &&
+                       dead_after(g, n, node_index(g, gr) + 1, gr, {sr, dv}) &&
+                       dead_after(g, n, node_index(g, sr) + 1, sr, {dv}) &&
+                       dead_after(g, n, node_index(g, dv) + 1, dv, {mul});
+    float * wscr = chain ? (float *) ctx.scratch(exec_ctx::MOE_SLOT, 3 * T * n_used * sizeof(float)) : nullptr;
+    if (!moe_router(ctx, mm, sm, as, n_used, wscr)) return false;
+    ctx.done.push_back(sm);
+    ctx.done.push_back(as);
+    if (chain) {
+        ctx.done.push_back(gr);
+        ctx.done.push_back(sr);
+        ctx.done.push_back(dv);
+        ctx.moe = {mul, wscr + 2 * T * n_used, n_used, nullptr, nullptr};
+    }
+    return true;
 }
 
 static bool try_moe_weights(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
@@ -799,6 +915,10 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             ctx.silu_defer = ctx.silu_mul = nullptr;
         }
     }
+    if (ctx.moe.comb && !is_view_op(node) && node != ctx.moe.comb &&
+        !(node->op == GGML_OP_ADD && (node->src[0] == ctx.moe.comb || node->src[1] == ctx.moe.comb))) {
+        flush_moe_combine(ctx);   // something else runs before the residual ADD that takes it
+    }
     if (ggml_is_empty(node)) return 1;
     if (!ctx.done.empty()) {
         auto it = std::find(ctx.done.begin(), ctx.done.end(), node);
@@ -808,6 +928,9 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
         }
     }
     const int n = ggml_graph_n_nodes(cgraph);
+    if (debug_ops() && !is_view_op(node))
+        fprintf(stderr, "[ops] %d %s %s (%s%s%s)\n", i, ggml_op_desc(node), node->name, node->src[0] ? ggml_type_name(node->src[0]->type) : "-",
+                node->src[1] ? " " : "", node->src[1] ? node->src[1]->name : "");
     switch (node->op) {
         case GGML_OP_NONE:
         case GGML_OP_RESHAPE:
@@ -823,6 +946,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             }
         }
             if (fusion_enabled() && gemv_supported(node)) return op_gemv_grouped(ctx, cgraph, i, n);
+            if (fusion_enabled() && try_moe_router(ctx, cgraph, i, n)) return 1;
             op_mul_mat(ctx, node);
             return 1;
         case GGML_OP_GET_ROWS:
@@ -841,7 +965,8 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                 norm_stores(cgraph, n, node, mul, mm, sn, sm);
                 const ggml_tensor * qkey = nullptr;
                 if (ggml_tensor * c = moe_quant_consumer(cgraph, n, mul ? mul : node, mm, &qkey)) mm = c;
-                if (fused_norm(ctx, nullptr, node, mul, mm, sn, sm, qkey)) return mul ? 2 : 1;
+                const ggml_tensor * mm0 = other_type_reader(cgraph, n, mul ? mul : node, mm);
+                if (fused_norm(ctx, nullptr, node, mul, mm, sn, sm, qkey, mm0)) return mul ? 2 : 1;
             }
             op_rms_norm(ctx, node, mul ? mul->src[1] : nullptr, mul);
             return mul ? 2 : 1;
@@ -849,7 +974,14 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
         case GGML_OP_NORM:
             op_norm(ctx, node);
             return 1;
-        case GGML_OP_ADD:
+        case GGML_OP_ADD: {
+            // a deferred MoE combine whose slot sum is an operand here
+            norm_combine nc = {};
+            const norm_combine * pc = nullptr;
+            if (ctx.moe.comb && (node->src[0] == ctx.moe.comb || node->src[1] == ctx.moe.comb)) {
+                nc = {ctx.moe.e, ctx.moe.wn, ctx.moe.n_used, ctx.moe.comb};
+                pc = &nc;
+            }
             // residual ADD feeding the next RMS_NORM (+ norm-weight MUL, + MUL_MAT input)
             if (fusion_enabled()) {
                 ggml_tensor * nx = at(cgraph, i + 1, n);
@@ -875,11 +1007,17 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                         }
                         fprintf(stderr, "\n");
                     }
-                    if (fused_norm(ctx, node, nx, mul, mm, sn, sm, qkey)) return used;
+                    const ggml_tensor * mm0 = other_type_reader(cgraph, n, mul ? mul : nx, mm);
+                    if (fused_norm(ctx, node, nx, mul, mm, sn, sm, qkey, mm0, pc)) {
+                        if (pc) ctx.moe = {};
+                        return used;
+                    }
                 }
             }
+            flush_moe_combine(ctx);
             op_binary(ctx, node);
             return 1;
+        }
         case GGML_OP_MUL:
             if (ctx.silu_defer && node == ctx.silu_mul) {
                 ggml_tensor * sl = ctx.silu_defer;
@@ -928,7 +1066,8 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                         if (!computed_before(ctx, cgraph, c->src[1], i) || !can_hoist(cgraph, i, j, o, 1, skip)) break;
                         ggml_tensor * mm = at(cgraph, j + 1, n);
                         const bool ssilu = !dead_after(cgraph, n, i + 1, node, {c});
-                        const bool smul = !(mm && mm->op == GGML_OP_MUL_MAT && dead_after(cgraph, n, j + 1, c, {mm}));
+                        const bool smul = !(mm && (mm->op == GGML_OP_MUL_MAT || mm->op == GGML_OP_MUL_MAT_ID) &&
+                                            dead_after(cgraph, n, j + 1, c, {mm}));
                         if (fused_silu_mul_quant(ctx, node, c, mm, ssilu, smul)) {
                             if (j == i + 1) return 2;
                             ctx.done.push_back(c);
@@ -962,6 +1101,24 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
             op_soft_max(ctx, node);
             return 1;
         case GGML_OP_MUL_MAT_ID:
+            // MoE gate and up of the same routed slots (graph order gate, SILU, up,
+            // build_moe_ffn :727-741) in one launch
+            if (fusion_enabled()) {
+                ggml_tensor * up = nullptr;
+                int j = i + 1;
+                for (; j < n && j <= i + 4; ++j) {
+                    ggml_tensor * c = ggml_graph_node(cgraph, j);
+                    if (is_view_op(c) || (c->op == GGML_OP_UNARY && c->src[0] == node)) continue;
+                    if (c->op == GGML_OP_MUL_MAT_ID && c->src[1] == node->src[1] && c->src[2] == node->src[2]) up = c;
+                    break;
+                }
+                const ggml_tensor * o[1] = {up};
+                const std::vector<const ggml_tensor *> skip(ctx.done.begin(), ctx.done.end());
+                if (up && !overlaps(up, node) && can_hoist(cgraph, i, j, o, 1, skip) && op_mul_mat_id_pair(ctx, node, up)) {
+                    ctx.done.push_back(up);
+                    return 1;
+                }
+            }
             op_mul_mat_id(ctx, node);
             return 1;
         case GGML_OP_ARGSORT:

@@ -830,14 +830,12 @@ struct moe_route_args {
     int stage;                        // bit 0: SOFT_MAX + ARGSORT; bit 1: GET_ROWS [+ SUM_ROWS + DIV]
 };
 
-__global__ __launch_bounds__(64) void k_moe_route(const moe_route_args a) {
-    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.T) return;
-    const float * x = (const float *) (a.logits + t * a.nb_l);
+// stage 1 [+ 2] of token t for up to 16 experts, the logits at x (global or LDS)
+__device__ __forceinline__ void moe_route16(const moe_route_args & a, int64_t t, const float * x) {
     float * p = (float *) (a.probs + t * a.nb_p);
     int32_t * o = (int32_t *) (a.order + t * a.nb_o);
     const int n = a.n_exp;
-    if ((a.stage & 1) && n <= 16) {
+    {
         // up to 16 experts (Mixtral: 8): the same arithmetic in registers. The global
         // probabilities / order are written once at the end instead of being re-read through every
         // pass (the exchange sort's p[o[j]] was a chain of dependent global loads: 7.3 us a launch)
@@ -907,6 +905,18 @@ __global__ __launch_bounds__(64) void k_moe_route(const moe_route_args a) {
                 }
             }
         }
+    }
+}
+
+__global__ __launch_bounds__(64) void k_moe_route(const moe_route_args a) {
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.T) return;
+    const float * x = (const float *) (a.logits + t * a.nb_l);
+    float * p = (float *) (a.probs + t * a.nb_p);
+    int32_t * o = (int32_t *) (a.order + t * a.nb_o);
+    const int n = a.n_exp;
+    if ((a.stage & 1) && n <= 16) {
+        moe_route16(a, t, x);
         return;
     }
     if ((a.stage & 2) && !(a.stage & 1) && a.n_used <= 8) {
@@ -990,6 +1000,95 @@ __global__ __launch_bounds__(64) void k_moe_route(const moe_route_args a) {
     }
 }
 
+// The router logits (MUL_MAT of the f32 gate_inp [K, n_exp] by the norm output,
+// build_moe_ffn :661) and the route chain in one launch, one workgroup per token: wave e forms
+// logit e in the order the CPU's mat-vec takes for this shape (k_mmv_f_exact: for one token
+// ggml_vec_dot_f32's 4 x 16 AVX-512 accumulators, REDUCE, double tail; for two or more
+// llamafile's 16-lane FMA chain), then thread 0 runs moe_route16 on them from LDS.  With wscr
+// the routed weights, their sum and the normalised weights (GET_ROWS, SUM_ROWS, DIV) go to a
+// private scratch [3][T][n_used] the combine reads.
+struct moe_router_args {
+    const char * W; int64_t nb01; int64_t K;
+    const char * X; int64_t nb11;
+    char * logits; int64_t nb_lo;   // MUL_MAT output row t at t * nb_lo
+    moe_route_args r;
+};
+
+template <bool TINY>
+__global__ __launch_bounds__(1024) void k_moe_router(const moe_router_args a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t t = blockIdx.x;
+    __shared__ float part[16][64];
+    __shared__ float lg[16];
+    const float * w = (const float *) (a.W + wave * a.nb01);
+    const float * x = (const float *) (a.X + t * a.nb11);
+    if constexpr (TINY) {
+        float acc = 0.0f;
+        const int s = lane & 15;
+        if (lane < 16) {
+#pragma unroll 8
+            for (int64_t k = 0; k < a.K; k += 16) acc = fmaf(w[k + s], x[k + s], acc);
+        }
+        acc = __fadd_rn(acc, __shfl_xor(acc, 8, WAVE));
+        acc = __fadd_rn(acc, __shfl_xor(acc, 4, WAVE));
+        acc = __fadd_rn(acc, __shfl_xor(acc, 2, WAVE));
+        acc = __fadd_rn(acc, __shfl_xor(acc, 1, WAVE));
+        if (lane == 0) lg[wave] = acc;
+    } else {
+        const int64_t np = a.K & ~int64_t(63);
+        float acc = 0.0f;
+#pragma unroll 8
+        for (int64_t i = 0; i < np; i += 64) acc = fmaf(w[i + lane], x[i + lane], acc);
+        part[wave][lane] = acc;
+        __syncthreads();
+        if (lane == 0) {
+            const float * pa = part[wave];
+            float v[16];
+#pragma unroll
+            for (int l = 0; l < 16; ++l) v[l] = __fadd_rn(__fadd_rn(pa[l], pa[32 + l]), __fadd_rn(pa[16 + l], pa[48 + l]));
+            double sumf = (double) reduce16_avx512(v);
+            for (int64_t k = np; k < a.K; ++k) sumf += (double) __fmul_rn(w[k], x[k]);
+            lg[wave] = (float) sumf;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float * lo = (float *) (a.logits + t * a.nb_lo);
+        for (int e = 0; e < a.r.n_exp; ++e) lo[e] = lg[e];
+        moe_route16(a.r, t, lg);
+    }
+}
+
+bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr) {
+    const ggml_tensor * W = mm->src[0], * X = mm->src[1];
+    const int64_t n = W->ne[1], K = W->ne[0], T = X->ne[1];
+    if (W->type != GGML_TYPE_F32 || X->type != GGML_TYPE_F32 || n > 16 || n < 1 || W->ne[2] != 1 || W->ne[3] != 1 ||
+        X->ne[2] != 1 || X->ne[3] != 1 || X->nb[0] != 4 || W->nb[0] != 4 || mm->nb[0] != 4 || mm->ne[1] != T) return false;
+    if (!ggml_is_contiguous(sm) || sm->src[0] != mm || !ggml_is_contiguous(as) || as->ne[0] != n || ggml_nrows(as) != T ||
+        sm->ne[0] != n || ggml_nrows(sm) != T) return false;
+    moe_router_args a = {};
+    a.W = (const char *) W->data; a.nb01 = W->nb[1]; a.K = K;
+    a.X = (const char *) X->data; a.nb11 = X->nb[1];
+    a.logits = (char *) mm->data; a.nb_lo = mm->nb[1];
+    moe_route_args & r = a.r;
+    r.probs = (char *) sm->data; r.nb_p = sm->nb[1];
+    r.order = (char *) as->data; r.nb_o = as->nb[1];
+    r.n_exp = (int) n; r.T = T; r.stage = 1;
+    memcpy(&r.scale, sm->op_params, sizeof(float));
+    if (wscr) {
+        r.stage = 3; r.n_used = n_used;
+        r.w = (char *) wscr; r.nb_w = n_used * sizeof(float);
+        r.wsum = (char *) (wscr + T * n_used); r.nb_s = n_used * sizeof(float);
+        r.wn = (char *) (wscr + 2 * T * n_used); r.nb_n = n_used * sizeof(float);
+    }
+    // the tinyBLAS order for >= 2 columns, as mul_mat_vec picks it
+    const bool tiny = T >= 2 && K % 16 == 0 && n % 4 == 0 && ggml_is_contiguous(X);
+    const dim3 block((unsigned) (64 * n));
+    if (tiny) hipLaunchKernelGGL(k_moe_router<true>, dim3((unsigned) T), block, 0, ctx.stream, a);
+    else hipLaunchKernelGGL(k_moe_router<false>, dim3((unsigned) T), block, 0, ctx.stream, a);
+    return true;
+}
+
 // stage 1 (at the SOFT_MAX): probabilities and their descending order; as = the ARGSORT node
 bool moe_route_sort(exec_ctx & ctx, const ggml_tensor * sm, ggml_tensor * as) {
     const int64_t n = sm->ne[0], T = ggml_nrows(sm);
@@ -1040,12 +1139,15 @@ __global__ __launch_bounds__(256) void k_moe_combine(const char * __restrict__ e
     ((float *) (out + t * nb_o1))[i] = __fadd_rn(m0, m1);
 }
 
-void moe_combine(exec_ctx & ctx, const ggml_tensor * mul, ggml_tensor * add) {
+void moe_combine(exec_ctx & ctx, const ggml_tensor * mul, ggml_tensor * add, const float * wscr) {
     const ggml_tensor * e = mul->src[0], * w = mul->src[1];
     const dim3 grid((unsigned) ceil_div(mul->ne[0], 256), (unsigned) mul->ne[2]);
+    // wscr: the router's private copy of the normalised weights ([T][2], k_moe_router)
+    const char * wp = wscr ? (const char *) wscr : (const char *) w->data;
+    const int64_t nbw1 = wscr ? (int64_t) sizeof(float) : (int64_t) w->nb[1];
+    const int64_t nbw2 = wscr ? (int64_t) (2 * sizeof(float)) : (int64_t) w->nb[2];
     hipLaunchKernelGGL(k_moe_combine, grid, dim3(256), 0, ctx.stream, (const char *) e->data, (int64_t) e->nb[1],
-                       (int64_t) e->nb[2], (const char *) w->data, (int64_t) w->nb[1], (int64_t) w->nb[2], (char *) add->data,
-                       (int64_t) add->nb[1], mul->ne[0]);
+                       (int64_t) e->nb[2], wp, nbw1, nbw2, (char *) add->data, (int64_t) add->nb[1], mul->ne[0]);
 }
 
 }  // namespace mi355x

@@ -590,12 +590,37 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
 // rows a phase-1 instruction touches sit in different banks.
 constexpr int PF_CH = 64, PF_P = 16, PF_U = 8;
 
-// y = f16(fma(v_hi, vs, y)): f16_mad on the high half of v
-__device__ __forceinline__ uint32_t f16_mad_hi(uint32_t vbits, float vs, uint32_t ybits) {
-    float t;
-    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,1]" : "=v"(t) : "v"(vbits), "v"(vs), "v"(ybits));
+// two f16 chains in one register (low half = dim 2l, high half = dim 2l + 1):
+// y = f16(fma(v, vs, y)) per half — the f32 fma rounded, then rounded to f16 by
+// v_cvt_pk_f16_f32 (round to nearest even, as v_cvt_f16_f32), three instructions for two steps
+__device__ __forceinline__ uint32_t f16x2_mad(uint32_t vbits, float vs, uint32_t ybits) {
+    float t0, t1;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(t0) : "v"(vbits), "v"(vs), "v"(ybits));
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(t1) : "v"(vbits), "v"(vs), "v"(ybits));
     uint32_t r;
-    asm("v_cvt_f16_f32 %0, %1" : "=v"(r) : "v"(t));
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(t0), "v"(t1));
+    return r;
+}
+
+// y = f16(f32(y) * ms) per half (f16_scale on both halves)
+__device__ __forceinline__ uint32_t f16x2_scale(uint32_t ybits, float ms, float nz) {
+    float t0, t1;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(t0) : "v"(ybits), "v"(ms), "v"(nz));
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(t1) : "v"(ybits), "v"(ms), "v"(nz));
+    uint32_t r;
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(r) : "v"(t0), "v"(t1));
+    return r;
+}
+
+// two fp32 sums of the CPU's sequence, one v_pk_add_f32 (each half an IEEE add)
+__device__ __forceinline__ float2 f32x2_add(float2 a, float2 b) {
+    float2 r;
+    asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float2 f32x2_mul(float2 a, float2 b) {
+    float2 r;
+    asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
 
@@ -750,8 +775,8 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
     asm volatile("" : "+v"(nz));
     // ---- phase-2/3 state of the wave's 4 pairs --------------------------------------------------
     float mc[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};   // running max (uniform)
-    uint32_t y[4][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};          // f16 bits, dims 2 lane, 2 lane + 1
-    float S[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    uint32_t y[4] = {0, 0, 0, 0};                                  // f16 x 2: dims 2 lane, 2 lane + 1
+    float2 S[2] = {{0.0f, 0.0f}, {0.0f, 0.0f}};                      // pairs (0, 1), (2, 3)
     float slope2[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) slope2[i] = slope_of(4 * wave + i);
@@ -835,11 +860,9 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
                     for (int u = 0; u < PF_U; ++u) {
                         const float v4[4] = {vs[u].x, vs[u].y, vs[u].z, vs[u].w};
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            y[i][0] = f16_mad(vv[u], v4[i], y[i][0]);
-                            y[i][1] = f16_mad_hi(vv[u], v4[i], y[i][1]);
-                            S[i] = __fadd_rn(S[i], v4[i]);   // not contracted on the CPU
-                        }
+                        for (int i = 0; i < 4; ++i) y[i] = f16x2_mad(vv[u], v4[i], y[i]);
+                        S[0] = f32x2_add(S[0], make_float2(vs[u].x, vs[u].y));   // not contracted on the CPU
+                        S[1] = f32x2_add(S[1], make_float2(vs[u].z, vs[u].w));
                     }
                 } else {
                     // the same steps, except: a masked position keeps the state (-0 must
@@ -856,14 +879,15 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
                         const float w4[4] = {m4.x, m4.y, m4.z, m4.w};
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
-                            const uint32_t ys0 = f16_scale(y[i][0], w4[i], nz), ys1 = f16_scale(y[i][1], w4[i], nz);
-                            const uint32_t yn0 = f16_mad(vv[u], v4[i], ys0);
-                            const uint32_t yn1 = f16_mad_hi(vv[u], v4[i], ys1);
-                            const float Sn = __fadd_rn(__fmul_rn(S[i], w4[i]), v4[i]);
-                            const bool dd = (dead[i] >> j) & 1;
-                            y[i][0] = dd ? y[i][0] : yn0;
-                            y[i][1] = dd ? y[i][1] : yn1;
-                            S[i] = dd ? S[i] : Sn;
+                            const uint32_t yn = f16x2_mad(vv[u], v4[i], f16x2_scale(y[i], w4[i], nz));
+                            y[i] = (dead[i] >> j) & 1 ? y[i] : yn;
+                        }
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const float2 Sn = f32x2_add(f32x2_mul(S[h], make_float2(w4[2 * h], w4[2 * h + 1])),
+                                                        make_float2(v4[2 * h], v4[2 * h + 1]));
+                            S[h].x = (dead[2 * h] >> j) & 1 ? S[h].x : Sn.x;
+                            S[h].y = (dead[2 * h + 1] >> j) & 1 ? S[h].y : Sn.y;
                         }
                     }
                 }
@@ -893,8 +917,8 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
         const int64_t iq = q0 + p / G;
         if (iq >= a.n_q) continue;
         float * drow = (float *) ((char *) a.dst + iq * a.nb1_dst * a.H + head_of(p) * a.nb1_dst + iq3 * a.nb2_dst);
-        const float rs = 1.0f / S[i];
-        *(float2 *) (drow + 2 * lane) = make_float2(__fmul_rn(h2f((uint16_t) y[i][0]), rs), __fmul_rn(h2f((uint16_t) y[i][1]), rs));
+        const float rs = 1.0f / (i & 1 ? S[i >> 1].y : S[i >> 1].x);
+        *(float2 *) (drow + 2 * lane) = make_float2(__fmul_rn(h2f((uint16_t) y[i]), rs), __fmul_rn(h2f((uint16_t) (y[i] >> 16)), rs));
     }
 }
 

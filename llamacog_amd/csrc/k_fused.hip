@@ -24,9 +24,12 @@ struct norm_fused_args {
     const float * w; float * yw;        // MUL weight / output (nullable)
     int64_t ne0;
     float eps;
-    int qmode;                          // 0 none, 1 Q8_K, 2 Q8_0 (of yw if w else y)
+    int qmode;                          // 0 none, 1 Q8_K, 2 Q8_0 (of yw if w else y), 3 both
     int8_t * qs; float * qd; int16_t * qsum;
+    int8_t * qs0; float * qd0; int16_t * qsum0;   // qmode 3: the Q8_0 one
     int64_t nrows;
+    // MoE combine source instead of a: x = (e[., 0, row] * cw[row, 0] + e[., 1, row] * cw[row, 1]) + b
+    const float * e; const float * cw; int nu;
 };
 
 // one workgroup of BT threads per row; thread t owns the float4s at element 4 (t + BT k), k < NV,
@@ -47,10 +50,20 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
         if (p.w) wv[k] = *(const float4 *) (p.w + 4 * (tid + BT * k));
     }
     double acc = 0.0;
+    const float * e0 = p.e ? p.e + 2 * ro : nullptr, * e1 = p.e ? e0 + p.ne0 : nullptr;
+    const float cw0 = p.e ? p.cw[row * p.nu] : 0.0f, cw1 = p.e ? p.cw[row * p.nu + 1] : 0.0f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
         const int64_t e = 4 * (tid + BT * k);
-        v[k] = *(const float4 *) (p.a + ro + e);
+        if (p.e) {
+            const float4 x0 = *(const float4 *) (e0 + e), x1 = *(const float4 *) (e1 + e);
+            v[k].x = __fadd_rn(__fmul_rn(x0.x, cw0), __fmul_rn(x1.x, cw1));
+            v[k].y = __fadd_rn(__fmul_rn(x0.y, cw0), __fmul_rn(x1.y, cw1));
+            v[k].z = __fadd_rn(__fmul_rn(x0.z, cw0), __fmul_rn(x1.z, cw1));
+            v[k].w = __fadd_rn(__fmul_rn(x0.w, cw0), __fmul_rn(x1.w, cw1));
+        } else {
+            v[k] = *(const float4 *) (p.a + ro + e);
+        }
         if (p.b) {
             const float4 bb = *(const float4 *) (p.b + ro + e);
             v[k].x = __fadd_rn(v[k].x, bb.x); v[k].y = __fadd_rn(v[k].y, bb.y);
@@ -67,7 +80,9 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
         for (int o = 8; o > 0; o >>= 1) t = __dadd_rn(t, __shfl_xor(t, o, WAVE));
         if (lane == 0) {
             float mean;
-            if (!rms_mean_decided(t, p.ne0, mean)) mean = rms_mean_sequential(p.a + ro, p.b ? p.b + ro : nullptr, p.ne0);
+            if (!rms_mean_decided(t, p.ne0, mean))
+                mean = p.e ? rms_mean_sequential_moe(e0, e1, cw0, cw1, p.b + ro, p.ne0)
+                           : rms_mean_sequential(p.a + ro, p.b ? p.b + ro : nullptr, p.ne0);
             smean = mean;
         }
     }
@@ -95,10 +110,13 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
         }
         const float q[4] = {y.x, y.y, y.z, y.w};
         const int64_t c0 = 4 * (int64_t) BT * k + 256 * wave;
-        if (p.qmode == 1) {
+        if (p.qmode & 1) {
             q8K_wave(q, lane, p.qs + ro + c0, p.qsum + row * (p.ne0 / 16) + c0 / 16, p.qd + row * (p.ne0 / 256) + c0 / 256);
-        } else if (p.qmode == 2) {
+        }
+        if (p.qmode == 2) {
             q8_0_wave(q, lane, true, p.qs + ro + c0, p.qd + row * (p.ne0 / 32) + c0 / 32, p.qsum + row * (p.ne0 / 32) + c0 / 32);
+        } else if (p.qmode == 3) {
+            q8_0_wave(q, lane, true, p.qs0 + ro + c0, p.qd0 + row * (p.ne0 / 32) + c0 / 32, p.qsum0 + row * (p.ne0 / 32) + c0 / 32);
         }
     }
 }
@@ -164,7 +182,7 @@ static int consumer_qmode(const ggml_tensor * mm, const ggml_tensor * x) {
 }
 
 bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm,
-                bool store_norm, bool store_mul, const ggml_tensor * qkey) {
+                bool store_norm, bool store_mul, const ggml_tensor * qkey, const ggml_tensor * mm0, const norm_combine * comb) {
     const int64_t ne0 = norm->ne[0];
     // ne0 <= 4096: one float4 per thread; above: whole 4096-element slices per 1024 threads
     if (ne0 % 256 != 0 || (ne0 > 4096 && ne0 % 4096 != 0) || ne0 > 16384) return false;
@@ -174,12 +192,22 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     if (mul && (!f32_contig(mul) || !f32_contig(mul->src[1]) || ggml_nelements(mul->src[1]) != ne0)) return false;
     const ggml_tensor * out = mul ? mul : norm;
     const ggml_tensor * key = qkey ? qkey : out;
-    const int qmode = consumer_qmode(mm, key);
+    int qmode = consumer_qmode(mm, key);
+    // mm0: a later Q8_0 consumer of the same output beside a K-quant first one
+    const bool with0 = qmode == 1 && !qkey && consumer_qmode(mm0, out) == 2;
     const int64_t nrows = ggml_nrows(norm);
 
     norm_fused_args p;
     p.a = add ? (const float *) add->src[0]->data : (const float *) norm->src[0]->data;
     p.b = add ? (const float *) add->src[1]->data : nullptr;
+    p.e = nullptr; p.cw = nullptr; p.nu = 0;
+    if (comb) {
+        // the combine's slot sum is one ADD operand (never stored); the other is the residual
+        if (!add || (add->src[0] != comb->sum && add->src[1] != comb->sum) || comb->n_used != 2) return false;
+        p.b = (const float *) (add->src[0] == comb->sum ? add->src[1] : add->src[0])->data;
+        p.a = nullptr;
+        p.e = comb->e; p.cw = comb->w; p.nu = comb->n_used;
+    }
     p.xsum = add ? (float *) add->data : nullptr;
     p.w = mul ? (const float *) mul->src[1]->data : nullptr;
     // an output nothing reads is not stored; the last one is kept unless it is quantized here
@@ -198,6 +226,13 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     } else {
         p.qs = nullptr; p.qd = nullptr; p.qsum = nullptr;
     }
+    q8_act act0;
+    p.qs0 = nullptr; p.qd0 = nullptr; p.qsum0 = nullptr;
+    if (with0) {
+        carve_act(act0, ctx.scratch(exec_ctx::QSLOT0, q8_act::bytes(ne0, nrows, false)), ne0, nrows, false);
+        p.qs0 = act0.qs; p.qd0 = act0.d; p.qsum0 = act0.s;
+        p.qmode = qmode = 3;
+    }
     // up to 1024 threads per row, one float4 each (512 / 256 threads with several float4 each
     // measured no faster on Llama-3-8B decode, round 2); the canonical slice order j = w + NW k
     // is the same for every split, so the bits would not change
@@ -211,7 +246,10 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
         case 3: hipLaunchKernelGGL(k_norm_fused<3>, grid, block, 0, ctx.stream, p); break;
         default: hipLaunchKernelGGL(k_norm_fused<4>, grid, block, 0, ctx.stream, p); break;
     }
-    if (qmode) ctx.qcache_put(key, qmode == 1, act);
+    if (qmode) ctx.qcache_put(key, qmode != 2, act);
+    if (with0) {
+        ctx.qc0_tensor = out; ctx.qc0_data = out->data; ctx.qc0_act = act0;
+    }
     return true;
 }
 

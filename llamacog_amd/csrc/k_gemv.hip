@@ -59,10 +59,13 @@ struct gemv_args {
     } pro;
     unsigned long long * kt;              // in-graph kernel timeline region (nullable)
     uint32_t wl_off;                      // one-shot kernel: LDS byte offset of the weight slices
-    // MUL_MAT_ID of one token (gemv_mmid; the one-shot kernel's ID instance only): matrix i is
-    // expert *(xids + i * xids_nb0) of the stack at W[i] (xnb02 bytes apart), read on the device;
-    // its activation column is A + i * (xqs_st, xd_st, xs_st) (0: one column shared by the slots)
-    const char * xids; int64_t xids_nb0, xnb02; int xn_as;
+    // MUL_MAT_ID of one token (gemv_mmid; the one-shot kernel's ID instance only): matrix i is a
+    // stack (W[i], experts xnb02 bytes apart) whose routed slots are stacked as its rows: row
+    // s * xme + r is row r of expert *(xids + s * xids_nb0) (read on the device), its output
+    // dst[i][s * xme + r] (the slots' output rows are contiguous), its activation column
+    // A + s * (xqs_st, xd_st, xs_st) (0: one column shared by the slots).  gate and up of the
+    // same slots are two such matrices of one launch
+    const char * xids; int64_t xids_nb0, xnb02, xme; int xn_as;
     int64_t xqs_st, xd_st, xs_st;
 };
 
@@ -395,6 +398,8 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     const int mi = gemv_mat(p, g);
     const int64_t row0 = (g - p.blk0[mi]) * RPG + rowl0;
     const int64_t M = p.M[mi];
+    // ID: the routed slot of this row group (xme % RPG == 0: uniform over the workgroup)
+    const int xsl = ID ? __builtin_amdgcn_readfirstlane((int) ((uint32_t) ((g - p.blk0[mi]) * RPG) / (uint32_t) p.xme)) : 0;
     // ---- activation sources first: pass 0 of x and w for the norm prologue ----
     float4 pxv[4], pwv[4];
     bool pv0 = false;
@@ -415,9 +420,9 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
         const int seg = (nt_w / T::per_block) * T::blk_bytes;
         const uint8_t * Wm = p.W[mi];
         if constexpr (ID) {   // the routed expert (uniform over the workgroup, before any barrier)
-            const int ex = *(const int32_t *) (p.xids + mi * p.xids_nb0);
+            const int ex = *(const int32_t *) (p.xids + xsl * p.xids_nb0);
             if (ex < 0 || ex >= p.xn_as) return;
-            Wm += (int64_t) ex * p.xnb02;
+            Wm += (int64_t) ex * p.xnb02 - (int64_t) xsl * p.xme * p.nb01[mi];
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -440,7 +445,7 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
         __syncthreads();
         T::load(pro_act(p.pro, buf), tt, x);
     } else if constexpr (ID) {   // this slot's column
-        const gemv_act A = {p.A.qs + mi * p.xqs_st, p.A.d + mi * p.xd_st, p.A.s + mi * p.xs_st};
+        const gemv_act A = {p.A.qs + xsl * p.xqs_st, p.A.d + xsl * p.xd_st, p.A.s + xsl * p.xs_st};
         T::load(A, tt, x);
     } else {
         T::load(p.A, tt, x);
@@ -1020,14 +1025,22 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
 // KIND 1 does the same one row per wave with register loads).  Same records and walk (qtypes.h),
 // so the same bits as ggml_compute_forward_mul_mat_id (ggml-cpu.c:1466).  The dense launches are
 // other template instances and carry none of these branches.  GGML_MI355X_MMID_OS=0 keeps k_mmx.
-bool gemv_mmid(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act) {
+bool gemv_mmid(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, ggml_tensor * dst2) {
     static const bool on = !getenv("GGML_MI355X_MMID_OS") || atoi(getenv("GGML_MI355X_MMID_OS")) != 0;
     const ggml_tensor * as = dst->src[0];
     const ggml_tensor * b = dst->src[1];
     const ggml_tensor * ids = dst->src[2];
     const int64_t n_used = ids->ne[0];
-    if (!on || !os_enabled() || ids->ne[1] != 1 || n_used < 1 || n_used > GEMV_MAXMAT) return false;
+    const int nmat = dst2 ? 2 : 1;
+    if (!on || !os_enabled() || ids->ne[1] != 1 || n_used < 1 || n_used > 8) return false;
+    // the slots' output rows contiguous, and whole row groups per slot (RPG <= 8)
+    if (dst->nb[1] != (size_t) as->ne[1] * sizeof(float) || as->ne[1] % 8 != 0) return false;
     if (b->ne[1] != 1 && b->ne[1] != n_used) return false;   // slot e reads column e % ne11
+    if (dst2) {   // the up projection of the same slots: same stack shape, type and input
+        const ggml_tensor * as2 = dst2->src[0];
+        if (as2->type != as->type || !ggml_are_same_shape(as2, as) || as2->nb[1] != as->nb[1] || as2->nb[2] != as->nb[2] ||
+            dst2->src[1] != b || dst2->src[2] != ids || dst2->nb[1] != dst->nb[1]) return false;
+    }
     int per = 0;
     switch (as->type) {
         case GGML_TYPE_Q4_K: case GGML_TYPE_Q4_0:
@@ -1043,23 +1056,25 @@ bool gemv_mmid(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act) {
     gemv_init();
     g_kt_ctx = ctx.kt_buf && ktrace_enabled() ? &ctx : nullptr;
     gemv_args a = {};
-    for (int i = 0; i < (int) n_used; ++i) {
-        a.W[i] = (const uint8_t *) as->data;
+    for (int i = 0; i < nmat; ++i) {
+        const ggml_tensor * d = i == 0 ? dst : dst2;
+        a.W[i] = (const uint8_t *) d->src[0]->data;
         a.nb01[i] = as->nb[1];
-        a.M[i] = as->ne[1];
-        a.dst[i] = (float *) ((char *) dst->data + i * dst->nb[1]);
+        a.M[i] = n_used * as->ne[1];
+        a.dst[i] = (float *) d->data;
     }
     a.A = {act.qs, act.d, act.s};
     a.xids = (const char *) ids->data; a.xids_nb0 = ids->nb[0]; a.xnb02 = as->nb[2]; a.xn_as = (int) as->ne[2];
+    a.xme = as->ne[1];
     if (b->ne[1] > 1) { a.xqs_st = act.qs_stride(); a.xd_st = act.d_stride(); a.xs_st = act.s_stride(); }
     a.ntasks = (int) (nblk * per);
     bool ok = false;
     switch (as->type) {
-        case GGML_TYPE_Q4_K: ok = launch_os_id<g_q4_K>(ctx.stream, a, (int) n_used); break;
-        case GGML_TYPE_Q5_K: ok = launch_os_id<g_q5_K>(ctx.stream, a, (int) n_used); break;
-        case GGML_TYPE_Q6_K: ok = launch_os_id<g_q6_K>(ctx.stream, a, (int) n_used); break;
-        case GGML_TYPE_Q8_0: ok = launch_os_id<g_q8_0>(ctx.stream, a, (int) n_used); break;
-        case GGML_TYPE_Q4_0: ok = launch_os_id<g_q4_0>(ctx.stream, a, (int) n_used); break;
+        case GGML_TYPE_Q4_K: ok = launch_os_id<g_q4_K>(ctx.stream, a, nmat); break;
+        case GGML_TYPE_Q5_K: ok = launch_os_id<g_q5_K>(ctx.stream, a, nmat); break;
+        case GGML_TYPE_Q6_K: ok = launch_os_id<g_q6_K>(ctx.stream, a, nmat); break;
+        case GGML_TYPE_Q8_0: ok = launch_os_id<g_q8_0>(ctx.stream, a, nmat); break;
+        case GGML_TYPE_Q4_0: ok = launch_os_id<g_q4_0>(ctx.stream, a, nmat); break;
         default: break;
     }
     g_kt_ctx = nullptr;

@@ -80,6 +80,7 @@ void quantize_act(exec_ctx & ctx, const ggml_tensor * src, bool k_quant, q8_act 
     GGML_ASSERT(src->type == GGML_TYPE_F32 && src->nb[0] == 4);
     GGML_ASSERT(K % (k_quant ? 256 : 32) == 0);
     carve_act(act, ctx.scratch(slot, q8_act::bytes(K, ncols, k_quant)), K, ncols, k_quant);
+    if (debug_ops()) fprintf(stderr, "[ops]   quantize %s %s K=%lld cols=%lld\n", k_quant ? "q8_K" : "q8_0", src->name, (long long) K, (long long) ncols);
     dim3 grid((unsigned) ceil_div(K, 256), (unsigned) ncols);
     if (k_quant) {
         hipLaunchKernelGGL(k_quantize_q8_K, grid, dim3(64), 0, ctx.stream, (const char *) src->data, K,
@@ -492,7 +493,29 @@ bool mul_mat_id_supported(const ggml_tensor * op) {
 bool mmq_id_supported(const ggml_tensor * dst);
 void mul_mat_q_id(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, const int32_t * cnt, const int32_t * off,
                   const int32_t * list, int64_t n_pairs);
-bool gemv_mmid(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act);
+bool gemv_mmid(exec_ctx & ctx, ggml_tensor * dst, const q8_act & act, ggml_tensor * dst2 = nullptr);
+
+// the gate and up projections of the same routed slots of one token (dst, dst2: same input and
+// ids) as one launch of the one-shot ID instance; false: nothing was launched
+bool op_mul_mat_id_pair(exec_ctx & ctx, ggml_tensor * dst, ggml_tensor * dst2) {
+    const ggml_tensor * as = dst->src[0];
+    const ggml_tensor * b = dst->src[1];
+    const ggml_tensor * ids = dst->src[2];
+    if (ids->ne[1] != 1 || ids->ne[0] > 8 || dst2->src[1] != b || dst2->src[2] != ids) return false;
+    const bool kq = is_k_quant(as->type);
+    hipEvent_t ev_beg = nullptr;
+    const double bytes = 2.0 * ((double) as->nb[2] * (double) std::min<int64_t>(ids->ne[0], as->ne[2]) + (double) ggml_nbytes(dst)) +
+                         (double) ggml_nelements(b) * (kq ? 1.14 : 1.0);
+    q8_act act;
+    if (!ctx.qcache_get(b, kq, act)) {
+        quantize_act(ctx, b, kq, act, exec_ctx::QSLOT);
+        ctx.qcache_put(b, kq, act);
+    }
+    if (ctx.timing) ctx.time_begin(TK_MMV, bytes, ev_beg);
+    const bool ok = gemv_mmid(ctx, dst, act, dst2);
+    if (ctx.timing) ctx.time_end(TK_MMV, ok ? bytes : 0.0, ev_beg);
+    return ok;
+}
 
 void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst) {
     const ggml_tensor * as = dst->src[0];

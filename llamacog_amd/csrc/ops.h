@@ -30,9 +30,10 @@ struct exec_ctx {
     hipStream_t stream = nullptr;
 
     // scratch arena: slot i is a separate region so one op can hold several temps
-    static constexpr int N_SLOTS = 6;   // 5: row-split mat-mul staging (op_mul_mat_split)
-    void *  slot_ptr[N_SLOTS]  = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    size_t  slot_size[N_SLOTS] = {0, 0, 0, 0, 0, 0};
+    static constexpr int N_SLOTS = 7;   // 5: row-split mat-mul staging (op_mul_mat_split)
+    static constexpr int MOE_SLOT = 6;  // the MoE routing weights between router and combine
+    void *  slot_ptr[N_SLOTS]  = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t  slot_size[N_SLOTS] = {0, 0, 0, 0, 0, 0, 0};
     bool    capturing = false;   // hipGraph capture in progress: growing is forbidden
     // bumped whenever a slot is reallocated: a captured hipGraph holds slot addresses in its
     // kernel arguments, so graphs captured under an older generation are dropped (backend.cpp)
@@ -61,7 +62,7 @@ struct exec_ctx {
     const void *        qc_data   = nullptr;
     bool                qc_kquant = false;
     q8_act              qc_act;
-    void qcache_clear() { qc_tensor = nullptr; qc_data = nullptr; }
+    void qcache_clear() { qc_tensor = nullptr; qc_data = nullptr; qc0_tensor = nullptr; qc0_data = nullptr; }
 
     // per-graph RoPE cos/sin table (k_elem.hip rope_table): every layer's fused Q/K rope
     // epilogue reads the same table of the token's position, built once per graph
@@ -79,6 +80,13 @@ struct exec_ctx {
     // gate, SILU, up, MUL): run as one silu*mul kernel at the MUL (dispatch.cpp)
     ggml_tensor * silu_defer = nullptr;
     ggml_tensor * silu_mul = nullptr;
+
+    // MoE decode chain (dispatch.cpp try_moe_router): the router launch wrote the normalised
+    // routing weights of `mul` (the combine's MUL) to MOE_SLOT, so the GET_ROWS / SUM_ROWS / DIV
+    // nodes are skipped; `comb` (the combine's slot-sum ADD) is deferred into the residual ADD +
+    // RMS_NORM launch that reads it (k_norm_fused's combine source)
+    struct moe_pending { const ggml_tensor * mul; const float * wn; int n_used; const ggml_tensor * comb; const float * e; };
+    moe_pending moe = {};
 
     // Dynamic destinations: a KV-cache store (CPY into a view at offset n_past) changes its
     // destination every token while the rest of the graph stays identical.  Kernels read
@@ -101,7 +109,17 @@ struct exec_ctx {
         }
         return nullptr;
     }
+    // a Q8_0 companion of the same activation (slot QSLOT0), written by a fused norm whose
+    // output feeds both K-quant and Q8_0 mat-vecs (Mixtral's Q5_K attn_q beside Q8_0 attn_k/v)
+    static constexpr int QSLOT0 = 4;
+    const ggml_tensor * qc0_tensor = nullptr;
+    const void *        qc0_data   = nullptr;
+    q8_act              qc0_act;
     bool qcache_get(const ggml_tensor * t, bool k_quant, q8_act & act) const {
+        if (!k_quant && qc0_tensor == t && qc0_data == t->data) {
+            act = qc0_act;
+            return true;
+        }
         if (qc_tensor != t || qc_data != t->data || qc_kquant != k_quant) return false;
         act = qc_act;
         return true;
@@ -142,6 +160,7 @@ enum timed_kind { TK_MMV = 0, TK_MMQ = 1, TK_FATTN = 2, TK_OTHER = 3, TK_GRAPH =
 // ggml_backend_mi355x_set_flags (fused/unfused and graph/eager runs are compared
 // bit-for-bit in tests/test_gpu_model.py)
 bool fusion_enabled();
+bool debug_ops();
 bool graphs_enabled();
 // blocks while any thread has a hipGraph capture open (backend.cpp)
 void wait_no_capture();
@@ -180,12 +199,14 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm = n
 void op_argsort(exec_ctx & ctx, ggml_tensor * dst);
 void op_sum_rows(exec_ctx & ctx, ggml_tensor * dst);
 void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst);
+bool op_mul_mat_id_pair(exec_ctx & ctx, ggml_tensor * dst, ggml_tensor * dst2);
 // the MoE router chain (k_elem.hip): SOFT_MAX + ARGSORT in one launch, GET_ROWS + SUM_ROWS + DIV in another
 bool moe_route_sort(exec_ctx & ctx, const ggml_tensor * sm, ggml_tensor * as);
+bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr);
 bool moe_route_weights(exec_ctx & ctx, ggml_tensor * gr, ggml_tensor * sr, ggml_tensor * dv);
 // out = experts[:, 0] * w0 + experts[:, 1] * w1 per token: the MUL by the routing weights and the ADD
 // of its two slot views in one launch (k_elem.hip)
-void moe_combine(exec_ctx & ctx, const ggml_tensor * mul, ggml_tensor * add);
+void moe_combine(exec_ctx & ctx, const ggml_tensor * mul, ggml_tensor * add, const float * wscr = nullptr);
 
 // quantizes ncols rows of an f32 tensor (row i = (i1, i2, i3) flattened) into act
 void quantize_act(exec_ctx & ctx, const ggml_tensor * src, bool k_quant, q8_act & act, int slot);
@@ -220,8 +241,12 @@ void carve_act(q8_act & act, void * base, int64_t K, int64_t ncols, bool k_quant
 // the consuming mat-vecs take the quantized activation from the cache), so it is not written
 // qkey: the tensor the quantized activation is cached under when the consumer `mm` reads a
 // reshape of the chain's output (a MoE MUL_MAT_ID behind the router); nullptr = the output itself
+// a deferred MoE combine as the first operand source of fused_norm's ADD: the experts'
+// outputs e ([ne0, 2, T] contiguous), the routing weights w ([T][n_used]) and the slot-sum node
+struct norm_combine { const float * e; const float * w; int n_used; const ggml_tensor * sum; };
 bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggml_tensor * mul, const ggml_tensor * mm,
-                bool store_norm = true, bool store_mul = true, const ggml_tensor * qkey = nullptr);
+                bool store_norm = true, bool store_mul = true, const ggml_tensor * qkey = nullptr,
+                const ggml_tensor * mm0 = nullptr, const struct norm_combine * comb = nullptr);
 bool fused_mul_quant(exec_ctx & ctx, ggml_tensor * mul, const ggml_tensor * mm);
 bool fused_silu_mul_quant(exec_ctx & ctx, ggml_tensor * silu, ggml_tensor * mul, const ggml_tensor * mm, bool store_silu,
                           bool store_mul = true);

@@ -210,4 +210,16 @@ __device__ __noinline__ float rms_mean_sequential(const float * a, const float *
     return (float) __ddiv_rn(s, (double) n);
 }
 
+// the same with x = (e0 * w0 + e1 * w1) + b: the MoE combine (MUL by the routing weights, ADD of
+// the two slots) feeding the residual ADD
+__device__ __noinline__ float rms_mean_sequential_moe(const float * e0, const float * e1, float w0, float w1,
+                                                      const float * b, int64_t n) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        const float x = __fadd_rn(__fadd_rn(__fmul_rn(e0[i], w0), __fmul_rn(e1[i], w1)), b[i]);
+        s = __dadd_rn(s, (double) __fmul_rn(x, x));
+    }
+    return (float) __ddiv_rn(s, (double) n);
+}
+
 }  // namespace mi355x
