@@ -119,6 +119,8 @@ void exec_ctx::free_scratch() {
     }
     if (fa_cnt) (void) hipFree(fa_cnt);
     fa_cnt = nullptr;
+    if (moe_cnt) (void) hipFree(moe_cnt);
+    moe_cnt = nullptr;
     if (kt_buf) (void) hipFree(kt_buf);
     kt_buf = nullptr;
     kt_cap = kt_off = 0;
@@ -1087,9 +1089,10 @@ static void run_nodes(exec_ctx & ex, ggml_cgraph * cgraph) {
     ex.silu_defer = ex.silu_mul = nullptr;
     ex.pro = {};
     ex.moe = {};
+    ex.moe_pro = {};
     const int n = ggml_graph_n_nodes(cgraph);
     for (int i = 0; i < n;) i += op_compute(ex, cgraph, i);
-    GGML_ASSERT(!ex.moe.comb);   // a deferred combine always meets its residual ADD
+    GGML_ASSERT(!ex.moe.comb && !ex.moe_pro.mm);   // deferred MoE work always meets its consumer
     if (ex.silu_defer) {   // a deferred SILU whose MUL never came
         op_unary(ex, ex.silu_defer);
         ex.silu_defer = ex.silu_mul = nullptr;

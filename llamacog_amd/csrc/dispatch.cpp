@@ -438,6 +438,10 @@ static bool prologues_enabled() {
 // from x in its prologue (k_gemv.hip), so neither the RMS_NORM nor the MUL runs as a node.
 // Same-lane in-place aliases of mm0 / res by the ADD output are safe (each row is read before it
 // is written).
+static bool moe_router_nodes(ggml_cgraph * g, int i, int n, ggml_tensor ** psm, ggml_tensor ** pas);
+static ggml_tensor * moe_quant_consumer(ggml_cgraph * g, int n, const ggml_tensor * out, const ggml_tensor * mm,
+                                        const ggml_tensor ** qkey);
+
 static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tensor * mm0, gemv_epi & epi,
                        std::vector<const ggml_tensor *> & absorbed) {
     const int pa = next_compute(g, i, n);
@@ -456,7 +460,30 @@ static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tenso
     if (mul && (!f32c(mul) || !ggml_is_contiguous(mul->src[1]))) return;
     ggml_tensor * last = mul ? mul : nm;
     ggml_tensor * mm = at(g, next_compute(g, node_index(g, last), n), n);
-    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != last || !gemv_supported(mm)) return;
+    if (!mm || mm->op != GGML_OP_MUL_MAT || mm->src[1] != last) return;
+    if (!gemv_supported(mm)) {
+        // the MoE FFN: the norm is formed by the router launch instead (try_moe_router)
+        ggml_tensor * sm = nullptr, * as = nullptr;
+        const ggml_tensor * qkey = nullptr;
+        if (!mul || !moe_router_nodes(g, node_index(g, mm), n, &sm, &as) || nm->ne[0] % 1024 != 0 || nm->ne[0] > 4096) return;
+        if (!ctx.moe_cnt && !ctx.capturing) {   // the router's arrival counters (k_elem.hip)
+            MI_CHECK(hipMalloc(&ctx.moe_cnt, exec_ctx::MOE_CNT * sizeof(int)));
+            MI_CHECK(hipMemsetAsync(ctx.moe_cnt, 0, exec_ctx::MOE_CNT * sizeof(int), ctx.stream));
+        }
+        if (!ctx.moe_cnt || !dead_after(g, n, pn + 1, nm, {mul})) return;
+        const ggml_tensor * c = moe_quant_consumer(g, n, last, mm, &qkey);
+        if (c && !(c->src[0]->type == GGML_TYPE_Q4_K || c->src[0]->type == GGML_TYPE_Q5_K || c->src[0]->type == GGML_TYPE_Q6_K))
+            qkey = nullptr;
+        epi.rres = (const float *) res->data;
+        epi.rxsum = (float *) ad->data;
+        float eps;
+        memcpy(&eps, nm->op_params, sizeof(float));
+        ctx.moe_pro = {mm, (const float *) ad->data, (const float *) mul->src[1]->data, eps, qkey};
+        absorbed.push_back(ad);
+        absorbed.push_back(nm);
+        absorbed.push_back(mul);
+        return;
+    }
     // every reader of the chain's output must be a decode mat-vec (each forms the activation in
     // its own prologue), and the norm output itself may be read only by the MUL
     std::vector<const ggml_tensor *> readers;
@@ -830,19 +857,33 @@ static void flush_moe_combine(exec_ctx & ctx) {
 // ARGSORT (ggml_top_k) follow after views only.  When the GET_ROWS of the probabilities by the
 // top-k, its SUM_ROWS and DIV are read by nothing but the combine MUL, those three are formed in
 // the same launch into a private scratch and skipped at their own nodes; the combine reads it.
-static bool try_moe_router(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+// the router MUL_MAT at node i (f32 gate_inp, at most 16 experts) and its SOFT_MAX / ARGSORT
+static bool moe_router_nodes(ggml_cgraph * g, int i, int n, ggml_tensor ** psm, ggml_tensor ** pas) {
     ggml_tensor * mm = ggml_graph_node(g, i);
-    if (mm->src[0]->type != GGML_TYPE_F32 || mm->src[0]->ne[1] > 16) return false;
+    if (mm->op != GGML_OP_MUL_MAT || mm->src[0]->type != GGML_TYPE_F32 || mm->src[0]->ne[1] > 16) return false;
     const int is = next_compute(g, i, n);
     ggml_tensor * sm = at(g, is, n);
     if (!sm || sm->op != GGML_OP_SOFT_MAX || sm->src[0] != mm || sm->src[1] || sm->src[2]) return false;
     float max_bias = 0.0f;
     memcpy(&max_bias, (const float *) sm->op_params + 1, sizeof(float));
     if (max_bias != 0.0f || !f32c(sm)) return false;
-    const int ia = next_compute(g, is, n);
-    ggml_tensor * as = at(g, ia, n);
+    ggml_tensor * as = at(g, next_compute(g, is, n), n);
     if (!as || as->op != GGML_OP_ARGSORT || as->src[0] != sm || as->op_params[0] != GGML_SORT_ORDER_DESC || as->type != GGML_TYPE_I32)
         return false;
+    *psm = sm;
+    *pas = as;
+    return true;
+}
+
+static bool try_moe_router(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
+    ggml_tensor * mm = ggml_graph_node(g, i);
+    ggml_tensor * sm = nullptr, * as = nullptr;
+    const bool pro = ctx.moe_pro.mm == mm;
+    if (!moe_router_nodes(g, i, n, &sm, &as)) {
+        GGML_ASSERT(!pro);   // plan_resid_moe checked this same pattern
+        return false;
+    }
+    const int ia = node_index(g, as);
     // the weights chain and its combine
     ggml_tensor * gr = nullptr, * sr = nullptr, * dv = nullptr, * mul = nullptr;
     for (int k = ia + 1; k < n && k <= ia + 48 && !gr; ++k) {
@@ -875,7 +916,19 @@ static bool try_moe_router(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
                        dead_after(g, n, node_index(g, sr) + 1, sr, {dv}) &&
                        dead_after(g, n, node_index(g, dv) + 1, dv, {mul});
     float * wscr = chain ? (float *) ctx.scratch(exec_ctx::MOE_SLOT, 3 * T * n_used * sizeof(float)) : nullptr;
-    if (!moe_router(ctx, mm, sm, as, n_used, wscr)) return false;
+    if (pro) {
+        // the FFN norm formed in this launch (plan_resid_moe): its output stored, its Q8_K
+        // quantization cached for the expert mat-vecs
+        const int64_t K = mm->src[1]->ne[0];
+        q8_act act;
+        carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(K, 1, true)), K, 1, true);
+        const moe_router_pro rp = {ctx.moe_pro.x, ctx.moe_pro.w, ctx.moe_pro.eps, ctx.moe_pro.qkey ? &act : nullptr};
+        GGML_ASSERT(moe_router(ctx, mm, sm, as, n_used, wscr, &rp));
+        if (ctx.moe_pro.qkey) ctx.qcache_put(ctx.moe_pro.qkey, true, act);
+        ctx.moe_pro = {};
+    } else if (!moe_router(ctx, mm, sm, as, n_used, wscr)) {
+        return false;
+    }
     ctx.done.push_back(sm);
     ctx.done.push_back(as);
     if (chain) {

@@ -908,6 +908,81 @@ __device__ __forceinline__ void moe_route16(const moe_route_args & a, int64_t t,
     }
 }
 
+// the exchange sort (DESC) of the first N (value, index) pairs, as ggml's argsort loop
+template <int N>
+__device__ __forceinline__ void xsort_desc(float (&sv)[16], int32_t (&ov)[16]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+#pragma unroll
+        for (int k = j + 1; k < N; ++k) {
+            if (sv[j] < sv[k]) {
+                const float tv = sv[j]; sv[j] = sv[k]; sv[k] = tv;
+                const int32_t ti = ov[j]; ov[j] = ov[k]; ov[k] = ti;
+            }
+        }
+    }
+}
+
+// moe_route16's arithmetic for n < 16 experts with lane i holding expert i's logit (a whole wave
+// calls it): the exps of every expert at once (expf's table loads in flight together, where the
+// one-lane loop waited for each), the double sum, the stores and the exchange sort in order
+__device__ void moe_route_wave(const moe_route_args & a, int64_t t, float lgt) {
+    const int lane = threadIdx.x & 63;
+    const int n = a.n_exp;
+    const float v = lane < n ? __fmul_rn(lgt, a.scale) : -INFINITY;
+    const float mx = wave_max(v);
+    const float e = lane < n ? expf_cr(__fsub_rn(v, mx)) : 0.0f;
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += (double) __shfl(e, i, WAVE);
+    const float inv = (float) (1.0 / s);
+    const float pl = __fmul_rn(e, inv);
+    float * p = (float *) (a.probs + t * a.nb_p);
+    int32_t * o = (int32_t *) (a.order + t * a.nb_o);
+    if (lane < n) p[lane] = pl;
+    float sv[16];
+    int32_t ov[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { sv[i] = __shfl(pl, i, WAVE); ov[i] = i; }
+    switch (n) {
+        case 8: xsort_desc<8>(sv, ov); break;
+        case 4: xsort_desc<4>(sv, ov); break;
+        default:
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+#pragma unroll
+                for (int k = j + 1; k < 16; ++k) {
+                    if (k < n && sv[j] < sv[k]) {
+                        const float tv = sv[j]; sv[j] = sv[k]; sv[k] = tv;
+                        const int32_t ti = ov[j]; ov[j] = ov[k]; ov[k] = ti;
+                    }
+                }
+            }
+    }
+    if (lane != 0) return;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) if (i < n) o[i] = ov[i];
+    if (a.stage & 2) {
+        float * wr = (float *) (a.w + t * a.nb_w);
+        double ws = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k < a.n_used) {
+                wr[k] = sv[k];
+                ws += (double) sv[k];
+            }
+        }
+        if (a.wsum) {
+            const float sf = (float) ws;
+            *(float *) (a.wsum + t * a.nb_s) = sf;
+            if (a.wn) {
+                float * nr = (float *) (a.wn + t * a.nb_n);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) if (k < a.n_used) nr[k] = sv[k] / sf;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(64) void k_moe_route(const moe_route_args a) {
     const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.T) return;
@@ -1012,6 +1087,10 @@ struct moe_router_args {
     const char * X; int64_t nb11;
     char * logits; int64_t nb_lo;   // MUL_MAT output row t at t * nb_lo
     moe_route_args r;
+    // norm prologue (one token, k_moe_router_mw): X = RMS_NORM(px) * pw formed by every workgroup
+    // with k_norm_fused's arithmetic; workgroup 0 stores it (to X) and its Q8_K quantization
+    const float * px; const float * pw; float eps;
+    int8_t * qs; float * qd; int16_t * qsum;
 };
 
 template <bool TINY>
@@ -1026,8 +1105,15 @@ __global__ __launch_bounds__(1024) void k_moe_router(const moe_router_args a) {
         float acc = 0.0f;
         const int s = lane & 15;
         if (lane < 16) {
-#pragma unroll 8
-            for (int64_t k = 0; k < a.K; k += 16) acc = fmaf(w[k + s], x[k + s], acc);
+            int64_t k = 0;
+            for (; k + 32 * 16 <= a.K; k += 32 * 16) {
+                float wv[32], xv[32];
+#pragma unroll
+                for (int u = 0; u < 32; ++u) { wv[u] = w[k + 16 * u + s]; xv[u] = x[k + 16 * u + s]; }
+#pragma unroll
+                for (int u = 0; u < 32; ++u) acc = fmaf(wv[u], xv[u], acc);
+            }
+            for (; k < a.K; k += 16) acc = fmaf(w[k + s], x[k + s], acc);
         }
         acc = __fadd_rn(acc, __shfl_xor(acc, 8, WAVE));
         acc = __fadd_rn(acc, __shfl_xor(acc, 4, WAVE));
@@ -1037,8 +1123,17 @@ __global__ __launch_bounds__(1024) void k_moe_router(const moe_router_args a) {
     } else {
         const int64_t np = a.K & ~int64_t(63);
         float acc = 0.0f;
-#pragma unroll 8
-        for (int64_t i = 0; i < np; i += 64) acc = fmaf(w[i + lane], x[i + lane], acc);
+        int64_t i = 0;
+        // 32 steps of the chain per batch: every load of a batch in flight before its FMAs (a
+        // chain that waits on each load pays the memory latency per step: 10 us a launch)
+        for (; i + 32 * 64 <= np; i += 32 * 64) {
+            float wv[32], xv[32];
+#pragma unroll
+            for (int u = 0; u < 32; ++u) { wv[u] = w[i + 64 * u + lane]; xv[u] = x[i + 64 * u + lane]; }
+#pragma unroll
+            for (int u = 0; u < 32; ++u) acc = fmaf(wv[u], xv[u], acc);
+        }
+        for (; i < np; i += 64) acc = fmaf(w[i + lane], x[i + lane], acc);
         part[wave][lane] = acc;
         __syncthreads();
         if (lane == 0) {
@@ -1052,14 +1147,161 @@ __global__ __launch_bounds__(1024) void k_moe_router(const moe_router_args a) {
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (wave == 0) {
         float * lo = (float *) (a.logits + t * a.nb_lo);
-        for (int e = 0; e < a.r.n_exp; ++e) lo[e] = lg[e];
-        moe_route16(a.r, t, lg);
+        if (lane < a.r.n_exp) lo[lane] = lg[lane];
+        if (a.r.n_exp < 16) moe_route_wave(a.r, t, lane < a.r.n_exp ? lg[lane] : 0.0f);
+        else if (lane == 0) moe_route16(a.r, t, lg);
     }
 }
 
-bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr) {
+// The same over n_exp workgroups per token (grid n_exp x T): workgroup e stages x and router row
+// e in LDS with every load in flight at once (one CU streaming all 8 rows took ~10 us a launch),
+// wave 0 forms logit e in the same order, and the last workgroup of the token to store its logit
+// (arrival counter, self-resetting) runs the route on the logits read back past L1.
+template <bool TINY>
+__global__ __launch_bounds__(256) void k_moe_router_mw(const moe_router_args a, int * cnt) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int e = blockIdx.x;
+    const int64_t t = blockIdx.y;
+    extern __shared__ __attribute__((aligned(16))) float xs[];   // [K] x, [K] w
+    float * ws = xs + a.K;
+    const float * w = (const float *) (a.W + e * a.nb01);
+    const float * x = (const float *) (a.X + t * a.nb11);
+    // every load in flight before the first LDS store (K <= 8192; the launcher checks)
+    if (a.px) {
+        // x = RMS_NORM(px) * pw: thread t owns the float4s at 4 (t + 256 u); the double sum in
+        // any order is decided against the CPU's sequential one (quant_act.h rms_mean_decided)
+        __shared__ double wpart[4];
+        __shared__ float smean;
+        float4 pv[4], nw[4], wv[4];
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = 4 * (tid + 256 * u);
+            if (k < a.K) { pv[u] = *(const float4 *) (a.px + k); nw[u] = *(const float4 *) (a.pw + k); wv[u] = *(const float4 *) (w + k); }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (4 * (tid + 256 * u) < a.K) acc = __dadd_rn(acc, sq4(pv[u]));
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) wpart[wave] = acc;
+        __syncthreads();
+        if (tid == 0) {
+            const double sum = __dadd_rn(__dadd_rn(wpart[0], wpart[1]), __dadd_rn(wpart[2], wpart[3]));
+            float mean;
+            if (!rms_mean_decided(sum, a.K, mean)) mean = rms_mean_sequential(a.px, nullptr, a.K);
+            smean = mean;
+        }
+        __syncthreads();
+        const float scale = 1.0f / sqrtf(smean + a.eps);
+        float * yo = e == 0 ? (float *) (a.X + t * a.nb11) : nullptr;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t k = 4 * (tid + 256 * u);
+            if (k >= a.K) continue;
+            float4 y;
+            y.x = __fmul_rn(__fmul_rn(pv[u].x, scale), nw[u].x); y.y = __fmul_rn(__fmul_rn(pv[u].y, scale), nw[u].y);
+            y.z = __fmul_rn(__fmul_rn(pv[u].z, scale), nw[u].z); y.w = __fmul_rn(__fmul_rn(pv[u].w, scale), nw[u].w);
+            *(float4 *) (xs + k) = y;
+            *(float4 *) (ws + k) = wv[u];
+            if (yo) {
+                *(float4 *) (yo + k) = y;
+                if (a.qs) {   // wave w's 256 elements of pass u: Q8_K block w + 4 u
+                    const float q[4] = {y.x, y.y, y.z, y.w};
+                    const int64_t c0 = 256 * (wave + 4 * u);
+                    q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
+                }
+            }
+        }
+    } else {
+        float4 xv[8], wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = 4 * (tid + 256 * u);
+            if (k < a.K) { xv[u] = *(const float4 *) (x + k); wv[u] = *(const float4 *) (w + k); }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t k = 4 * (tid + 256 * u);
+            if (k < a.K) { *(float4 *) (xs + k) = xv[u]; *(float4 *) (ws + k) = wv[u]; }
+        }
+    }
+    __syncthreads();
+    __shared__ int is_last;
+    if (wave == 0) {
+        float lgt;
+        if constexpr (TINY) {
+            float acc = 0.0f;
+            const int s = lane & 15;
+            if (lane < 16) {
+                int64_t k = 0;
+                for (; k + 16 * 16 <= a.K; k += 16 * 16) {   // LDS reads of a batch ahead of its FMAs
+                    float wv[16], xv[16];
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) { wv[u] = ws[k + 16 * u + s]; xv[u] = xs[k + 16 * u + s]; }
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) acc = fmaf(wv[u], xv[u], acc);
+                }
+                for (; k < a.K; k += 16) acc = fmaf(ws[k + s], xs[k + s], acc);
+            }
+            acc = __fadd_rn(acc, __shfl_xor(acc, 8, WAVE));
+            acc = __fadd_rn(acc, __shfl_xor(acc, 4, WAVE));
+            acc = __fadd_rn(acc, __shfl_xor(acc, 2, WAVE));
+            acc = __fadd_rn(acc, __shfl_xor(acc, 1, WAVE));
+            lgt = acc;
+        } else {
+            const int64_t np = a.K & ~int64_t(63);
+            float acc = 0.0f;
+            int64_t i = 0;
+            for (; i + 16 * 64 <= np; i += 16 * 64) {   // LDS reads of a batch ahead of its FMAs
+                float wv[16], xv[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) { wv[u] = ws[i + 64 * u + lane]; xv[u] = xs[i + 64 * u + lane]; }
+#pragma unroll
+                for (int u = 0; u < 16; ++u) acc = fmaf(wv[u], xv[u], acc);
+            }
+            for (; i < np; i += 64) acc = fmaf(ws[i + lane], xs[i + lane], acc);
+            // the AVX-512 REDUCE of the 4 x 16 accumulators, then _mm512_reduce_add_ps
+            float v[16];
+#pragma unroll
+            for (int l = 0; l < 16; ++l) {
+                const float a0 = __shfl(acc, l, WAVE), a1 = __shfl(acc, 16 + l, WAVE);
+                const float a2 = __shfl(acc, 32 + l, WAVE), a3 = __shfl(acc, 48 + l, WAVE);
+                v[l] = __fadd_rn(__fadd_rn(a0, a2), __fadd_rn(a1, a3));
+            }
+            double sumf = (double) reduce16_avx512(v);
+            for (int64_t k = np; k < a.K; ++k) sumf += (double) __fmul_rn(ws[k], xs[k]);
+            lgt = (float) sumf;
+        }
+        if (lane == 0) {
+            // the logit written through to the coherent level and drained before the counter add;
+            // the last workgroup reads them back with agent-scope (L1-bypassing) loads
+            __hip_atomic_store((float *) (a.logits + t * a.nb_lo) + e, lgt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int prev = __hip_atomic_fetch_add(cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            is_last = prev == a.r.n_exp - 1;
+            if (is_last) __hip_atomic_store(cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    if (is_last && wave == 0) {
+        const float * lo = (const float *) (a.logits + t * a.nb_lo);
+        if (a.r.n_exp < 16) {
+            const float l = lane < a.r.n_exp ? __hip_atomic_load(lo + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+            moe_route_wave(a.r, t, l);
+        } else if (lane == 0) {
+            float lg[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) lg[i] = __hip_atomic_load(lo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            moe_route16(a.r, t, lg);
+        }
+    }
+}
+
+bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr,
+                const moe_router_pro * pro) {
     const ggml_tensor * W = mm->src[0], * X = mm->src[1];
     const int64_t n = W->ne[1], K = W->ne[0], T = X->ne[1];
     if (W->type != GGML_TYPE_F32 || X->type != GGML_TYPE_F32 || n > 16 || n < 1 || W->ne[2] != 1 || W->ne[3] != 1 ||
@@ -1083,6 +1325,24 @@ bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_t
     }
     // the tinyBLAS order for >= 2 columns, as mul_mat_vec picks it
     const bool tiny = T >= 2 && K % 16 == 0 && n % 4 == 0 && ggml_is_contiguous(X);
+    if (!ctx.moe_cnt && !ctx.capturing) {
+        MI_CHECK(hipMalloc(&ctx.moe_cnt, exec_ctx::MOE_CNT * sizeof(int)));
+        MI_CHECK(hipMemsetAsync(ctx.moe_cnt, 0, exec_ctx::MOE_CNT * sizeof(int), ctx.stream));
+    }
+    const size_t lds = 2 * K * sizeof(float);
+    if (pro) {
+        // the norm prologue: one token, K <= 4096 (four float4s per thread), X contiguous
+        if (T != 1 || K % 1024 != 0 || K > 4096 || !ctx.moe_cnt || !ggml_is_contiguous(X)) return false;
+        a.px = pro->x; a.pw = pro->w; a.eps = pro->eps;
+        if (pro->q) { a.qs = pro->q->qs; a.qd = pro->q->d; a.qsum = pro->q->s; }
+    }
+    if (ctx.moe_cnt && T <= exec_ctx::MOE_CNT && K % 4 == 0 && K <= 8192 && lds <= 64 * 1024 && X->nb[1] % 16 == 0 && W->nb[1] % 16 == 0 &&
+        ((uintptr_t) X->data % 16) == 0 && ((uintptr_t) W->data % 16) == 0) {
+        const dim3 grid((unsigned) n, (unsigned) T);
+        if (tiny) hipLaunchKernelGGL(k_moe_router_mw<true>, grid, dim3(256), lds, ctx.stream, a, ctx.moe_cnt);
+        else hipLaunchKernelGGL(k_moe_router_mw<false>, grid, dim3(256), lds, ctx.stream, a, ctx.moe_cnt);
+        return true;
+    }
     const dim3 block((unsigned) (64 * n));
     if (tiny) hipLaunchKernelGGL(k_moe_router<true>, dim3((unsigned) T), block, 0, ctx.stream, a);
     else hipLaunchKernelGGL(k_moe_router<false>, dim3((unsigned) T), block, 0, ctx.stream, a);

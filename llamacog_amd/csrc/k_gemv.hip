@@ -529,13 +529,13 @@ __global__ __launch_bounds__(256) void k_gemv_os(const gemv_args p) {
     kt_exit(p.kt);
 }
 
-template <class T1, class T2, int R2, int WPR, bool PRO, int R1 = 2>
+template <class T1, class T2, int R2, int WPR, bool PRO, int R1 = 2, int WPR2 = WPR>
 __global__ __launch_bounds__(256) void k_gemv_os2(const gemv_args p1, const int64_t ng1, const gemv_args p2) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
     kt_enter(p1.kt);
     const int64_t b = blockIdx.x;
     if (b < ng1) gemv_os_body<T1, R1, WPR, 1, PRO>(p1, b, (uint8_t *) xr + p1.wl_off, xr);
-    else gemv_os_body<T2, R2, WPR, 1, PRO>(p2, b - ng1, (uint8_t *) xr + p2.wl_off, xr);
+    else gemv_os_body<T2, R2, WPR2, 1, PRO>(p2, b - ng1, (uint8_t *) xr + p2.wl_off, xr);
     kt_exit(p1.kt);
 }
 
@@ -739,12 +739,20 @@ template <class T>
 static bool launch_os_id(hipStream_t st, gemv_args & a, int nmat) {
     if (!os_enabled() || !os_aligned<T>(a, nmat)) return false;
     const int wpr = wpr_of(a.ntasks);
-    const int R = std::is_same<T, g_q6_K>::value || wpr == 2 ? 1 : 2;
+    int R = std::is_same<T, g_q6_K>::value || wpr == 2 ? 1 : 2;
+    // GGML_MI355X_MMID_R: rows per wave of the K = 14336 (four waves per row) launches (geometry probe)
+    static const int r4 = getenv("GGML_MI355X_MMID_R") ? atoi(getenv("GGML_MI355X_MMID_R")) : 0;
+    if (wpr == 4 && (r4 == 1 || r4 == 2 || r4 == 4)) R = r4;
+    // GGML_MI355X_MMID_R1: rows per wave of the one-wave-per-row launches (gate / up)
+    static const int r1 = getenv("GGML_MI355X_MMID_R1") ? atoi(getenv("GGML_MI355X_MMID_R1")) : 0;
+    if (wpr == 1 && (r1 == 1 || r1 == 2)) R = r1;
     gemv_args b = a;
-    const size_t lds = R == 2 ? (wpr == 1 ? os_lds_layout<T, 2, 1>(b) : os_lds_layout<T, 2, 4>(b))
+    const size_t lds = R == 4 ? os_lds_layout<T, 4, 4>(b)
+                     : R == 2 ? (wpr == 1 ? os_lds_layout<T, 2, 1>(b) : os_lds_layout<T, 2, 4>(b))
                               : (wpr == 1 ? os_lds_layout<T, 1, 1>(b) : wpr == 2 ? os_lds_layout<T, 1, 2>(b) : os_lds_layout<T, 1, 4>(b));
     if (lds > 64 * 1024) return false;
     switch (R * 8 + wpr) {
+        case 4 * 8 + 4: launch_os_id_v<T, 4, 4>(st, a, nmat); break;
         case 2 * 8 + 1: launch_os_id_v<T, 2, 1>(st, a, nmat); break;
         case 2 * 8 + 4: launch_os_id_v<T, 2, 4>(st, a, nmat); break;
         case 1 * 8 + 1: launch_os_id_v<T, 1, 1>(st, a, nmat); break;
@@ -776,6 +784,31 @@ static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2,
     else hipLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P, R1>), dim3(grid), dim3(64 * NWV), lds, st, a1, ng1, a2)
     if (a1.pro.kind) { OS2_LAUNCH(true); } else { OS2_LAUNCH(false); }
 #undef OS2_LAUNCH
+}
+
+// a K-quant part beside a Q8_0 part (Mixtral: Q5_K attn_q, Q8_0 attn_k / attn_v), each with its
+// own activation quantization and its own waves per row; no prologue
+template <class T1, int R1, int WPR1, class T2, int R2, int WPR2>
+static void launch_os2m_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2, int n2) {
+    constexpr int NWV = 4;
+    const int64_t ng1 = set_groups(a1, n1, (NWV / WPR1) * R1), ng2 = set_groups(a2, n2, (NWV / WPR2) * R2);
+    const size_t off = r16(std::max((size_t) (NWV / WPR1) * R1 * (a1.ntasks / T1::per_block) * T1::RS * 4,
+                                    (size_t) (NWV / WPR2) * R2 * (a2.ntasks / T2::per_block) * T2::RS * 4));
+    a1.wl_off = a2.wl_off = (uint32_t) off;
+    const size_t lds = off + std::max((size_t) 4 * R1 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
+    const unsigned grid = (unsigned) (ng1 + ng2);
+    a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv2+epi", grid, 64 * NWV) : nullptr;
+    if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR1, false, R1, WPR2>), dim3(grid), dim3(64 * NWV), lds, st,
+                                        t_ev_beg, t_ev_end, 0, a1, ng1, a2);
+    else hipLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR1, false, R1, WPR2>), dim3(grid), dim3(64 * NWV), lds, st, a1, ng1, a2);
+}
+
+template <class T1>
+static bool launch_os2m_t(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2, int n2) {
+    if (!os_enabled() || a1.pro.kind || a1.ntasks != WAVE || a2.ntasks != 2 * WAVE ||
+        !os_aligned<T1>(a1, n1) || !os_aligned<g_q8_0>(a2, n2)) return false;
+    launch_os2m_v<T1, 1, 1, g_q8_0, 1, 2>(st, a1, n1, a2, n2);
+    return true;
 }
 
 template <class T>
@@ -866,13 +899,17 @@ static bool launch_mixed(hipStream_t st, ggml_type t1, gemv_args & a1, int n1, g
     if (t1 == GGML_TYPE_Q4_K && t2 == GGML_TYPE_Q6_K) return launch_pipe2_t<g_q4_K, g_q6_K>(st, a1, n1, a2, n2);
     if (t1 == GGML_TYPE_Q4_K && t2 == GGML_TYPE_Q5_K) return launch_pipe2_t<g_q4_K, g_q5_K>(st, a1, n1, a2, n2);
     if (t1 == GGML_TYPE_Q5_K && t2 == GGML_TYPE_Q6_K) return launch_pipe2_t<g_q5_K, g_q6_K>(st, a1, n1, a2, n2);
+    if (t1 == GGML_TYPE_Q5_K && t2 == GGML_TYPE_Q8_0) return launch_os2m_t<g_q5_K>(st, a1, n1, a2, n2);
+    if (t1 == GGML_TYPE_Q4_K && t2 == GGML_TYPE_Q8_0) return launch_os2m_t<g_q4_K>(st, a1, n1, a2, n2);
     return false;
 }
 
 bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c) {
     const ggml_type t1 = mm0->src[0]->type, t2 = c->src[0]->type;
     return ((t1 == GGML_TYPE_Q4_K && (t2 == GGML_TYPE_Q6_K || t2 == GGML_TYPE_Q5_K)) ||
-                  (t1 == GGML_TYPE_Q5_K && t2 == GGML_TYPE_Q6_K));
+            (t1 == GGML_TYPE_Q5_K && t2 == GGML_TYPE_Q6_K) ||
+            // a Q8_0 part with its own activation (Mixtral's attn_k / attn_v beside the Q5_K attn_q)
+            ((t1 == GGML_TYPE_Q5_K || t1 == GGML_TYPE_Q4_K) && t2 == GGML_TYPE_Q8_0));
 }
 
 static bool is_kq(ggml_type t) { return t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K; }
@@ -972,9 +1009,18 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
     for (int i = 0; i < nmat; ++i) {
         const ggml_type ti = mms[i]->src[0]->type;
         if (ti == wt) ia[n1++] = i;
-        else { GGML_ASSERT((wt2 == wt || wt2 == ti) && is_kq(ti) && kq); wt2 = ti; ib[n2++] = i; }
+        else { GGML_ASSERT((wt2 == wt || wt2 == ti) && (is_kq(ti) || ti == GGML_TYPE_Q8_0) && kq); wt2 = ti; ib[n2++] = i; }
+    }
+    // a Q8_0 second part reads the Q8_0 quantization of the same input (the fused norm's
+    // companion, else quantized here)
+    q8_act act2 = act;
+    const bool q0 = n2 && wt2 == GGML_TYPE_Q8_0;
+    if (q0 && !pro && !ctx.qcache_get(src1, false, act2)) {
+        quantize_act(ctx, src1, false, act2, exec_ctx::QSLOT0);
+        ctx.qc0_tensor = src1; ctx.qc0_data = src1->data; ctx.qc0_act = act2;
     }
     auto one = [&](ggml_type t, gemv_args & d, int cnt) {
+        const int64_t nblk = src1->ne[0] / ggml_blck_size(t);
         switch (t) {
             case GGML_TYPE_Q4_K: d.ntasks = (int) (nblk * 4); launch_t<g_q4_K>(ctx.stream, d, cnt); break;
             case GGML_TYPE_Q5_K: d.ntasks = (int) (nblk * 4); launch_t<g_q5_K>(ctx.stream, d, cnt); break;
@@ -999,6 +1045,11 @@ void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         gemv_args a1 = a, a2 = a;
         part(a1, ia, n1);
         part(a2, ib, n2);
+        if (q0) {
+            a2.ntasks = (int) (src1->ne[0] / 32);
+            a2.A = {act2.qs, act2.d, act2.s};
+            a2.pro.qmode = 2;
+        }
         if (!launch_mixed(ctx.stream, wt, a1, n1, wt2, a2, n2)) {
             one(wt, a1, n1);
             if (ctx.timing) {   // the second launch is timed as its own mat-vec

@@ -42,6 +42,9 @@ struct exec_ctx {
     // arrival counters of the flash-attention output quantization (k_fattn_exact.hip)
     static constexpr int FA_CNT = 1024;
     int *   fa_cnt = nullptr;
+    // arrival counters of the multi-workgroup MoE router, one per token (k_elem.hip)
+    static constexpr int MOE_CNT = 4096;
+    int *   moe_cnt = nullptr;
     // the pending prologue: the chain whose output `last` (and its data pointer) the next decode
     // mat-vecs read; they form it from x and w in their launch (kind 1: RMS_NORM(x) [* w])
     // instead of a launch of its own (dispatch.cpp)
@@ -87,6 +90,10 @@ struct exec_ctx {
     // RMS_NORM launch that reads it (k_norm_fused's combine source)
     struct moe_pending { const ggml_tensor * mul; const float * wn; int n_used; const ggml_tensor * comb; const float * e; };
     moe_pending moe = {};
+    // the FFN norm the router launch forms (dispatch.cpp plan_resid_moe): x the residual sum the
+    // producer stored, w the norm weight; qkey the expert mat-vecs' input for the Q8_K cache
+    struct moe_norm_pending { const ggml_tensor * mm; const float * x; const float * w; float eps; const ggml_tensor * qkey; };
+    moe_norm_pending moe_pro = {};
 
     // Dynamic destinations: a KV-cache store (CPY into a view at offset n_past) changes its
     // destination every token while the rest of the graph stays identical.  Kernels read
@@ -202,7 +209,11 @@ void op_mul_mat_id(exec_ctx & ctx, ggml_tensor * dst);
 bool op_mul_mat_id_pair(exec_ctx & ctx, ggml_tensor * dst, ggml_tensor * dst2);
 // the MoE router chain (k_elem.hip): SOFT_MAX + ARGSORT in one launch, GET_ROWS + SUM_ROWS + DIV in another
 bool moe_route_sort(exec_ctx & ctx, const ggml_tensor * sm, ggml_tensor * as);
-bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr);
+// the router's input formed in the router launch: RMS_NORM(x) * w (eps), stored to the router's
+// src1 and, with q, quantized to Q8_K (the expert mat-vecs' activation)
+struct moe_router_pro { const float * x; const float * w; float eps; const q8_act * q; };
+bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr,
+                const moe_router_pro * pro = nullptr);
 bool moe_route_weights(exec_ctx & ctx, ggml_tensor * gr, ggml_tensor * sr, ggml_tensor * dv);
 // out = experts[:, 0] * w0 + experts[:, 1] * w1 per token: the MUL by the routing weights and the ADD
 // of its two slot views in one launch (k_elem.hip)
