@@ -1068,6 +1068,14 @@ static void kt_collect(mi_backend_ctx * ctx) {
             if (w == 0) w0e = we;
         }
         if (s0 == ~0ull) continue;
+        // GGML_MI355X_KTRACE_RAW=<name>: every slot of that launch's workgroup 0, in us from its start
+        static const char * raw = getenv("GGML_MI355X_KTRACE_RAW");
+        if (raw && strcmp(raw, l.name) == 0) {
+            const unsigned long long * r = h.data() + l.off;
+            fprintf(stderr, "[ktraw] %s:", l.name);
+            for (unsigned k = 1; k < l.stride; ++k) fprintf(stderr, " %.2f", r[k] >= r[0] ? (r[k] - r[0]) * tick_ns / 1e3 : -1.0);
+            fprintf(stderr, "\n");
+        }
         g_kt_samples.push_back({gs, (int) i, l.name, l.nwg, (s0 - base) * tick_ns, (sl - base) * tick_ns, (e1 - base) * tick_ns,
                                 w0e ? (w0e - base) * tick_ns : 0.0, nl ? life / nl * tick_ns : 0.0});
     }

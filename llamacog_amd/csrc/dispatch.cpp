@@ -1188,7 +1188,7 @@ int op_compute(exec_ctx & ctx, ggml_cgraph * cgraph, int i) {
                 ggml_tensor * c = at(cgraph, i + 2, n);
                 if (r && c && (r->op == GGML_OP_RESHAPE || r->op == GGML_OP_VIEW) && r->view_src == node &&
                     r->data == node->data && ggml_is_contiguous(r) && c->op == GGML_OP_MUL_MAT && c->src[1] == r &&
-                    gemv_supported(c)) {
+                    (gemv_supported(c) || mmq_supported(c))) {   // decode mat-vec / prefill MFMA tile
                     mm = c;
                 }
             }

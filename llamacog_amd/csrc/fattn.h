@@ -41,6 +41,9 @@ void launch_fattn_exact(hipStream_t stream, const fa_args & a, int64_t nq3);
 constexpr int FA_DEC2_NQ4_MIN = 256;
 int fattn_dec2_threads(const fa_args & a);   // the launch's workgroup size (timeline slots)
 bool fattn_dec2_ok(const fa_args & a, int64_t nq3);
+// the prefill batch tile (k_fattn_pf) runs this batch and can quantize its output (qmode 1):
+// f16 cache, D = 128, a GQA group of 4, 8 or 16 heads
+bool fattn_pf_quant_ok(const fa_args & a);
 void launch_fattn_dec2(hipStream_t stream, const fa_args & a, int64_t nq3);
 void fattn_scores_d128(hipStream_t st, const float * q, const uint16_t * k, int64_t n, float * s);
 // long-context decode (D = 128): the scores of every position by a (position block x KV head)

@@ -914,11 +914,12 @@ __device__ __forceinline__ void xsort_desc(float (&sv)[16], int32_t (&ov)[16]) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
 #pragma unroll
-        for (int k = j + 1; k < N; ++k) {
-            if (sv[j] < sv[k]) {
-                const float tv = sv[j]; sv[j] = sv[k]; sv[k] = tv;
-                const int32_t ti = ov[j]; ov[j] = ov[k]; ov[k] = ti;
-            }
+        for (int k = j + 1; k < N; ++k) {   // selects, not branches
+            const bool c = sv[j] < sv[k];
+            const float a = sv[j], b = sv[k];
+            const int32_t ia = ov[j], ib = ov[k];
+            sv[j] = c ? b : a; sv[k] = c ? a : b;
+            ov[j] = c ? ib : ia; ov[k] = c ? ia : ib;
         }
     }
 }
@@ -926,14 +927,16 @@ __device__ __forceinline__ void xsort_desc(float (&sv)[16], int32_t (&ov)[16]) {
 // moe_route16's arithmetic for n < 16 experts with lane i holding expert i's logit (a whole wave
 // calls it): the exps of every expert at once (expf's table loads in flight together, where the
 // one-lane loop waited for each), the double sum, the stores and the exchange sort in order
-__device__ void moe_route_wave(const moe_route_args & a, int64_t t, float lgt) {
+__device__ void moe_route_wave(const moe_route_args & a, int64_t t, float lgt, const uint64_t * etab) {
     const int lane = threadIdx.x & 63;
     const int n = a.n_exp;
     const float v = lane < n ? __fmul_rn(lgt, a.scale) : -INFINITY;
     const float mx = wave_max(v);
-    const float e = lane < n ? expf_cr(__fsub_rn(v, mx)) : 0.0f;
+    const float e = lane < n ? lx_expf_t(__fsub_rn(v, mx), etab) : 0.0f;   // expf_cr, its table from LDS
+    // uniform values by v_readlane (a shuffle per step was a ds_bpermute round trip each)
     double s = 0.0;
-    for (int i = 0; i < n; ++i) s += (double) __shfl(e, i, WAVE);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) if (i < n) s += (double) __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), i));
     const float inv = (float) (1.0 / s);
     const float pl = __fmul_rn(e, inv);
     float * p = (float *) (a.probs + t * a.nb_p);
@@ -941,6 +944,8 @@ __device__ void moe_route_wave(const moe_route_args & a, int64_t t, float lgt) {
     if (lane < n) p[lane] = pl;
     float sv[16];
     int32_t ov[16];
+    // the sort on per-lane copies (a shuffle keeps them in VGPRs: branch-free selects, where the
+    // scalar copies became a branch per compare-exchange)
 #pragma unroll
     for (int i = 0; i < 16; ++i) { sv[i] = __shfl(pl, i, WAVE); ov[i] = i; }
     switch (n) {
@@ -1091,6 +1096,7 @@ struct moe_router_args {
     // with k_norm_fused's arithmetic; workgroup 0 stores it (to X) and its Q8_K quantization
     const float * px; const float * pw; float eps;
     int8_t * qs; float * qd; int16_t * qsum;
+    unsigned long long * kt;        // in-graph kernel timeline region (nullable)
 };
 
 template <bool TINY>
@@ -1150,7 +1156,7 @@ __global__ __launch_bounds__(1024) void k_moe_router(const moe_router_args a) {
     if (wave == 0) {
         float * lo = (float *) (a.logits + t * a.nb_lo);
         if (lane < a.r.n_exp) lo[lane] = lg[lane];
-        if (a.r.n_exp < 16) moe_route_wave(a.r, t, lane < a.r.n_exp ? lg[lane] : 0.0f);
+        if (a.r.n_exp < 16) moe_route_wave(a.r, t, lane < a.r.n_exp ? lg[lane] : 0.0f, lx_exp2f_tab);
         else if (lane == 0) moe_route16(a.r, t, lg);
     }
 }
@@ -1162,6 +1168,9 @@ __global__ __launch_bounds__(1024) void k_moe_router(const moe_router_args a) {
 template <bool TINY>
 __global__ __launch_bounds__(256) void k_moe_router_mw(const moe_router_args a, int * cnt) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    kt_enter(a.kt);
+    __shared__ uint64_t etab[32];   // expf's table, fetched with the first loads
+    const uint64_t et = lx_exp2f_tab[tid & 31];
     const int e = blockIdx.x;
     const int64_t t = blockIdx.y;
     extern __shared__ __attribute__((aligned(16))) float xs[];   // [K] x, [K] w
@@ -1228,6 +1237,7 @@ __global__ __launch_bounds__(256) void k_moe_router_mw(const moe_router_args a, 
             if (k < a.K) { *(float4 *) (xs + k) = xv[u]; *(float4 *) (ws + k) = wv[u]; }
         }
     }
+    if (tid < 32) etab[tid] = et;
     __syncthreads();
     __shared__ int is_last;
     if (wave == 0) {
@@ -1263,15 +1273,15 @@ __global__ __launch_bounds__(256) void k_moe_router_mw(const moe_router_args a, 
                 for (int u = 0; u < 16; ++u) acc = fmaf(wv[u], xv[u], acc);
             }
             for (; i < np; i += 64) acc = fmaf(ws[i + lane], xs[i + lane], acc);
-            // the AVX-512 REDUCE of the 4 x 16 accumulators, then _mm512_reduce_add_ps
-            float v[16];
-#pragma unroll
-            for (int l = 0; l < 16; ++l) {
-                const float a0 = __shfl(acc, l, WAVE), a1 = __shfl(acc, 16 + l, WAVE);
-                const float a2 = __shfl(acc, 32 + l, WAVE), a3 = __shfl(acc, 48 + l, WAVE);
-                v[l] = __fadd_rn(__fadd_rn(a0, a2), __fadd_rn(a1, a3));
-            }
-            double sumf = (double) reduce16_avx512(v);
+            // the AVX-512 REDUCE of the 4 x 16 accumulators, then _mm512_reduce_add_ps, as
+            // lane-parallel halvings (k_moe_router1)
+            float r = __fadd_rn(acc, __shfl_down(acc, 32, WAVE));
+            r = __fadd_rn(r, __shfl_down(r, 16, WAVE));
+            r = __fadd_rn(__shfl_down(r, 8, WAVE), r);
+            r = __fadd_rn(__shfl_down(r, 4, WAVE), r);
+            r = __fadd_rn(r, __shfl_down(r, 2, WAVE));
+            r = __fadd_rn(r, __shfl_down(r, 1, WAVE));
+            double sumf = (double) r;
             for (int64_t k = np; k < a.K; ++k) sumf += (double) __fmul_rn(ws[k], xs[k]);
             lgt = (float) sumf;
         }
@@ -1290,7 +1300,7 @@ __global__ __launch_bounds__(256) void k_moe_router_mw(const moe_router_args a, 
         const float * lo = (const float *) (a.logits + t * a.nb_lo);
         if (a.r.n_exp < 16) {
             const float l = lane < a.r.n_exp ? __hip_atomic_load(lo + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
-            moe_route_wave(a.r, t, l);
+            moe_route_wave(a.r, t, l, etab);
         } else if (lane == 0) {
             float lg[16];
 #pragma unroll
@@ -1298,6 +1308,106 @@ __global__ __launch_bounds__(256) void k_moe_router_mw(const moe_router_args a, 
             moe_route16(a.r, t, lg);
         }
     }
+    kt_exit(a.kt);   // waves 1-3: the hand-off; wave 0 of the last workgroup: after the route
+}
+
+// One token, K = 64 KS, in ONE workgroup of 64 n_exp threads with no hand-off: wave e holds its
+// router row's 64-step slice of every AVX-512 accumulator lane in registers (all KS loads in
+// flight at once), the input (or its norm prologue) is staged once in LDS, the waves' chains run
+// side by side, and wave 0 routes from the logits in LDS.
+template <int KS>
+__global__ __launch_bounds__(1024) void k_moe_router1(const moe_router_args a) {
+    constexpr int K = 64 * KS;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int NT = blockDim.x, n = a.r.n_exp;
+    kt_enter(a.kt);
+    __shared__ uint64_t etab[32];
+    __shared__ __attribute__((aligned(16))) float xs[K];
+    __shared__ double wpart[16];
+    __shared__ float smean, lg[16];
+    const float * w = (const float *) (a.W + wave * a.nb01);
+    float wv[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) wv[s] = w[64 * s + lane];
+    const uint64_t et = lx_exp2f_tab[tid & 31];   // stored to LDS once the loads are all issued
+    const int NV = K / 4;   // float4s of the row
+    // phase stamps (GGML_MI355X_KTRACE_RAW=moe_router): slot 2 + i, written by thread 0
+    auto stamp = [&](int i) { if (a.kt && tid == 0) a.kt[2 + i] = __builtin_amdgcn_s_memrealtime(); };
+    if (a.px) {
+        // x and the norm weight both in flight with the router rows (the weight's first touch
+        // is a memory round trip of its own); NV <= 4 NT (the launcher checks)
+        float4 x4[4], w4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int v = tid + NT * u;
+            if (v < NV) { x4[u] = *(const float4 *) (a.px + 4 * v); w4[u] = *(const float4 *) (a.pw + 4 * v); }
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) if (tid + NT * u < NV) acc = __dadd_rn(acc, sq4(x4[u]));
+        acc = wave_sum(acc);
+        if (lane == 0) wpart[wave] = acc;
+        __syncthreads();
+        stamp(0);
+        if (tid == 0) {
+            double sum = 0.0;
+            for (int i = 0; i < NT / 64; ++i) sum = __dadd_rn(sum, wpart[i]);
+            float mean;
+            if (!rms_mean_decided(sum, K, mean)) mean = rms_mean_sequential(a.px, nullptr, K);
+            smean = mean;
+        }
+        __syncthreads();
+        const float scale = 1.0f / sqrtf(smean + a.eps);
+        float * yo = (float *) a.X;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int v = tid + NT * u;
+            if (v >= NV) continue;
+            float4 y;
+            y.x = __fmul_rn(__fmul_rn(x4[u].x, scale), w4[u].x); y.y = __fmul_rn(__fmul_rn(x4[u].y, scale), w4[u].y);
+            y.z = __fmul_rn(__fmul_rn(x4[u].z, scale), w4[u].z); y.w = __fmul_rn(__fmul_rn(x4[u].w, scale), w4[u].w);
+            *(float4 *) (xs + 4 * v) = y;
+            *(float4 *) (yo + 4 * v) = y;
+            if (a.qs) {   // wave w's 256 elements of this pass are one Q8_K block (NT % 64 == 0)
+                const float q[4] = {y.x, y.y, y.z, y.w};
+                const int64_t c0 = 4 * (int64_t) (v - lane);
+                q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
+            }
+        }
+    } else {
+        for (int v = tid; v < NV; v += NT) *(float4 *) (xs + 4 * v) = *(const float4 *) ((const float *) a.X + 4 * v);
+    }
+    if (tid < 32) etab[tid] = et;
+    stamp(1);
+    __syncthreads();
+    stamp(2);
+    float acc = 0.0f;
+#pragma unroll
+    for (int s0 = 0; s0 < KS; s0 += 16) {   // LDS reads of a batch ahead of its FMAs
+        float xv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xv[u] = s0 + u < KS ? xs[64 * (s0 + u) + lane] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) if (s0 + u < KS) acc = fmaf(wv[s0 + u], xv[u], acc);
+    }
+    // REDUCE of the 4 x 16 accumulators, (a[l] + a[32 + l]) + (a[16 + l] + a[48 + l]), then the
+    // _mm512_reduce_add_ps tree (k_mmv_f_exact's order) as lane-parallel halvings
+    float r = __fadd_rn(acc, __shfl_down(acc, 32, WAVE));
+    r = __fadd_rn(r, __shfl_down(r, 16, WAVE));
+    r = __fadd_rn(__shfl_down(r, 8, WAVE), r);
+    r = __fadd_rn(__shfl_down(r, 4, WAVE), r);
+    r = __fadd_rn(r, __shfl_down(r, 2, WAVE));
+    r = __fadd_rn(r, __shfl_down(r, 1, WAVE));
+    if (lane == 0) {
+        const float l = r;   // (float) of the double sum of one float
+        lg[wave] = l;
+        ((float *) a.logits)[wave] = l;
+    }
+    stamp(3);
+    __syncthreads();
+    stamp(4);
+    if (wave == 0) moe_route_wave(a.r, 0, lane < n ? lg[lane] : 0.0f, etab);
+    if (a.kt && tid == 0) a.kt[1] = __builtin_amdgcn_s_memrealtime();
 }
 
 bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr,
@@ -1330,6 +1440,17 @@ bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_t
         MI_CHECK(hipMemsetAsync(ctx.moe_cnt, 0, exec_ctx::MOE_CNT * sizeof(int), ctx.stream));
     }
     const size_t lds = 2 * K * sizeof(float);
+    // one token, K = 4096: the single-workgroup kernel (GGML_MI355X_ROUTER1=0: the counter one)
+    static const bool one = !getenv("GGML_MI355X_ROUTER1") || atoi(getenv("GGML_MI355X_ROUTER1")) != 0;
+    if (one && T == 1 && K == 4096 && ggml_is_contiguous(X) && n >= 4 && n < 16 && (uintptr_t) X->data % 16 == 0) {
+        if (pro) {
+            a.px = pro->x; a.pw = pro->w; a.eps = pro->eps;
+            if (pro->q) { a.qs = pro->q->qs; a.qd = pro->q->d; a.qsum = pro->q->s; }
+        }
+        a.kt = ctx.kt_take("moe_router", 1, (unsigned) (64 * n));
+        hipLaunchKernelGGL(k_moe_router1<64>, dim3(1), dim3((unsigned) (64 * n)), 0, ctx.stream, a);
+        return true;
+    }
     if (pro) {
         // the norm prologue: one token, K <= 4096 (four float4s per thread), X contiguous
         if (T != 1 || K % 1024 != 0 || K > 4096 || !ctx.moe_cnt || !ggml_is_contiguous(X)) return false;
@@ -1339,6 +1460,7 @@ bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_t
     if (ctx.moe_cnt && T <= exec_ctx::MOE_CNT && K % 4 == 0 && K <= 8192 && lds <= 64 * 1024 && X->nb[1] % 16 == 0 && W->nb[1] % 16 == 0 &&
         ((uintptr_t) X->data % 16) == 0 && ((uintptr_t) W->data % 16) == 0) {
         const dim3 grid((unsigned) n, (unsigned) T);
+        a.kt = T == 1 ? ctx.kt_take("moe_router", (unsigned) n, 256) : nullptr;
         if (tiny) hipLaunchKernelGGL(k_moe_router_mw<true>, grid, dim3(256), lds, ctx.stream, a, ctx.moe_cnt);
         else hipLaunchKernelGGL(k_moe_router_mw<false>, grid, dim3(256), lds, ctx.stream, a, ctx.moe_cnt);
         return true;

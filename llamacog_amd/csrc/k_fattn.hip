@@ -95,6 +95,13 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
             a.qs = act.qs; a.qd = act.d; a.qsum = act.s;
             a.cnt = ctx.fa_cnt;
         }
+    } else if (mm && a.n_q > 1 && nq3 == 1 && fattn_pf_quant_ok(a) && mm->src[1]->ne[0] == a.H * a.D &&
+               ggml_nrows(mm->src[1]) == a.n_q && ggml_is_contiguous(dst) &&
+               (mm->src[0]->type == GGML_TYPE_Q4_K || mm->src[0]->type == GGML_TYPE_Q5_K || mm->src[0]->type == GGML_TYPE_Q6_K)) {
+        // prefill: the batch tile quantizes its rows' output (k_fattn_pf), two Q8_K blocks a wave
+        carve_act(act, ctx.scratch(exec_ctx::QSLOT, q8_act::bytes(a.H * a.D, a.n_q, true)), a.H * a.D, a.n_q, true);
+        a.qmode = 1;
+        a.qs = act.qs; a.qd = act.d; a.qsum = act.s;
     }
     // decode (one query row): two heads per workgroup with the scores produced under the
     // recurrence (k_fattn_dec2) where it applies, else k_fattn_exact, one workgroup per head;

@@ -920,6 +920,36 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
         const float rs = 1.0f / (i & 1 ? S[i >> 1].y : S[i >> 1].x);
         *(float2 *) (drow + 2 * lane) = make_float2(__fmul_rn(h2f((uint16_t) y[i]), rs), __fmul_rn(h2f((uint16_t) (y[i] >> 16)), rs));
     }
+    // the output's Q8_K quantization for the next MUL_MAT (qmode 1): the wave's four heads are
+    // 512 consecutive values of one token's row = two Q8_K blocks; lane l gathers elements
+    // 4l .. 4l + 3 of each block (dims 2 lane, 2 lane + 1 of the lanes 2l, 2l + 1) for q8K_wave
+    if (a.qmode == 1) {
+        const int64_t iq = q0 + (4 * wave) / G;   // uniform over the wave (G >= 4)
+        if (iq < a.n_q) {
+            float o[4][2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float rs = 1.0f / (i & 1 ? S[i >> 1].y : S[i >> 1].x);
+                o[i][0] = __fmul_rn(h2f((uint16_t) y[i]), rs);
+                o[i][1] = __fmul_rn(h2f((uint16_t) (y[i] >> 16)), rs);
+            }
+            const int KR = a.H * D;
+            const int s0 = (2 * lane) & 63, s1 = (2 * lane + 1) & 63;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                float q[4];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const float lo0 = __shfl(o[2 * b][0], c ? s1 : s0, WAVE), hi0 = __shfl(o[2 * b][1], c ? s1 : s0, WAVE);
+                    const float lo1 = __shfl(o[2 * b + 1][0], c ? s1 : s0, WAVE), hi1 = __shfl(o[2 * b + 1][1], c ? s1 : s0, WAVE);
+                    q[2 * c] = lane < 32 ? lo0 : lo1;
+                    q[2 * c + 1] = lane < 32 ? hi0 : hi1;
+                }
+                const int64_t c0 = iq * KR + (int64_t) head_of(4 * wave + 2 * b) * D;
+                q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
+            }
+        }
+    }
 }
 
 // ==== decode, D = 128, f16 cache: two heads per workgroup, scores produced under the recurrence ====
@@ -1316,6 +1346,12 @@ void launch_fattn_dec2(hipStream_t st, const fa_args & a, int64_t nq3) {
     else hipLaunchKernelGGL(k_fattn_dec2<2>, grid, dim3(64 * (4 + 2 * 2)), 0, st, a);
 }
 
+bool fattn_pf_quant_ok(const fa_args & a) {
+    const int64_t G = a.H / a.Hkv;
+    return a.k_type == GGML_TYPE_F16 && a.v_type == GGML_TYPE_F16 && a.D == 128 && a.n_q >= 16 && a.H % a.Hkv == 0 &&
+           (G == 4 || G == 8 || G == 16);
+}
+
 void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     GGML_ASSERT(a0.H % a0.Hkv == 0);
     fa_args a = a0;
@@ -1351,7 +1387,8 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     }
     // prefill, f16 cache, D = 128: query blocks x the GQA group
     const int64_t G = a.H / a.Hkv;
-    if (a.D == 128 && a.n_q >= 16 && a.qmode == 0 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) {
+    if (a.D == 128 && a.n_q >= 16 && (a.qmode == 0 || (a.qmode == 1 && fattn_pf_quant_ok(a))) &&
+        (G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) {
         const dim3 g((unsigned) ceil_div(a.n_q, (int64_t) PF_P / G), (unsigned) (a.Hkv * nq3));
         switch (G) {
             case 1:  hipLaunchKernelGGL(k_fattn_pf<1>, g, dim3(256), 0, st, a); break;

@@ -175,7 +175,11 @@ static int consumer_qmode(const ggml_tensor * mm, const ggml_tensor * x) {
     if (!mm || (mm->op != GGML_OP_MUL_MAT && mm->op != GGML_OP_MUL_MAT_ID) || mm->src[1] != x) return 0;
     const ggml_type t = mm->src[0]->type;
     if (!mmv_q_supported_type(t)) return 0;
-    if (mm->src[1]->ne[1] * mm->src[1]->ne[2] * mm->src[1]->ne[3] > 8) return 0;   // mat-vec path only
+    split_parts sp;
+    if (tensor_split_parts(mm->src[0], sp)) return 0;   // row-split weights read the f32 input
+    // MUL_MAT_ID: the decode path only (batches gather their own quantization); a MUL_MAT of any
+    // width reads the cache (mat-vec and MFMA prefill tiles alike)
+    if (mm->op == GGML_OP_MUL_MAT_ID && mm->src[1]->ne[1] * mm->src[1]->ne[2] * mm->src[1]->ne[3] > 8) return 0;
     const bool kq = t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q5_K || t == GGML_TYPE_Q6_K;
     if (x->ne[0] % (kq ? 256 : 32) != 0) return 0;
     return kq ? 1 : 2;
