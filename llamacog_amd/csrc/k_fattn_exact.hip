@@ -1563,7 +1563,8 @@ __device__ __forceinline__ float fal_dmax(float v) {
     return fmaxf(v, __int_as_float(t));
 }
 
-// the chain holds the f16 V values as 32-bit words (as halves it measured 7 % slower at 4096)
+// the chain holds the f16 V values as 32-bit words (as halves it measured 7 % slower at 4096; as a
+// 16-bit asm operand the compiler packed pairs with v_perm and unpacked them again)
 typedef uint32_t fal_v16;
 #define FAL_MAD f16_mad
 template <int VT, int NM>   // V type: 0 f16, 1 q8_0, 2 q4_0; NM: positions held (n_kv <= NM)
@@ -1681,6 +1682,10 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
         }
     }
     if (lane == 0) { sm.wmax[wave] = run; sm.wlast[wave] = wlast; }
+    // phase stamps (GGML_MI355X_KTRACE_RAW=fa_chain): slots 2.. written by thread 0 in place of
+    // waves 1-3's exit stamps
+    auto stamp = [&](int i) { if (a.kt && tid == 0) a.kt[(1 + FAL_THREADS / 64) * blockIdx.x + 2 + i] = __builtin_amdgcn_s_memrealtime(); };
+    stamp(0);
     __syncthreads();   // (also publishes exptab)
     float Mprev = -INFINITY;
     for (int w2 = 0; w2 < wave; ++w2) Mprev = fmaxf(Mprev, sm.wmax[w2]);
@@ -1737,13 +1742,53 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
         sm.gb[nrun / 64] |= (uint8_t) (1u << ((nrun % 64) / U));   // the partial batch (if any)
     }
     __syncthreads();
+    stamp(1);
 
     // ---- the recurrence: wave 0, one of the workgroup's dims per lane; waves 1-3 keep two chunks
-    // in flight ----
+    // in flight; wave 1 also runs the S chain (the CPU's running sum, independent of the dims),
+    // so the dims' chain wave issues nothing but its own steps ----
     const int d = lane;
     uint32_t yb = 0;     // f16 bits (f16 V)
     float yf = 0.0f;     // f32 accumulator (quantized V)
     float S = 0.0f;
+    // S over chunk c (wave 1; every lane alike): the same steps as the dims' chain takes — a
+    // fast batch adds vs, a batch with a max update or a masked position scales first (ms != 1)
+    // and keeps the state where masked; the chunk's coefficients are in (published by the
+    // barrier that starts the iteration)
+    auto s_chunk = [&](int c) {
+        const int jc = c * CV, nr = min(CV, nrun - jc), nb = (nr + U - 1) / U;
+        uint32_t flags = 0;
+#pragma unroll
+        for (int k = 0; k < CV / 64; ++k) flags |= (uint32_t) sm.gb[jc / 64 + k] << (8 * k);
+        for (int h0 = 0; h0 < nb; h0 += 64 / U) {   // 64 positions: their vs read at once
+            float4 v4[64 / 4];
+#pragma unroll
+            for (int k = 0; k < 64 / 4; ++k) v4[k] = *(const float4 *) (sm.sc + jc + U * h0 + 4 * k);
+#pragma unroll
+            for (int bb = 0; bb < 64 / U; ++bb) {
+                const int b = h0 + bb;
+                if (b >= nb) break;
+                const float vs[U] = {v4[2 * bb].x, v4[2 * bb].y, v4[2 * bb].z, v4[2 * bb].w,
+                                     v4[2 * bb + 1].x, v4[2 * bb + 1].y, v4[2 * bb + 1].z, v4[2 * bb + 1].w};
+                static_assert(U == 8, "two float4 per batch");
+                if (!((flags >> b) & 1u)) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) S = __fadd_rn(S, vs[u]);   // not contracted on the CPU
+                } else {
+                    const int j = jc + U * b;
+                    const uint32_t db = (sm.dead[j / 32] >> (j % 32)) & ((1u << U) - 1);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const float ms = sm.cm[j + u];
+                        const bool live = ((db >> u) & 1u) == 0;
+                        const bool upd = __float_as_uint(ms) != 0x3f800000u;
+                        const float Ss = upd ? __fmul_rn(S, ms) : S;
+                        S = live ? __fadd_rn(Ss, vs[u]) : S;
+                    }
+                }
+            }
+        }
+    };
     for (int c = 0; c < nchunk; ++c) {
         const int st = c % NSTG;
         // this wave's stage-c instructions have landed (those of c + 1 may still be in flight)
@@ -1751,11 +1796,12 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
         __syncthreads();   // stage c is in; every chain lane is done with chunk c - 1's stage
         if (wave >= 1) {
             pend = c + 2 < nchunk ? stage((c + 2) % NSTG, (int64_t) (c + 2) * CV, min(CV, nrun - (c + 2) * CV)) : 0;
-            // the next chunk's coefficients, by one stager wave in turn, while the chain runs this one
-            if (c + 1 < nchunk && (c + 1) % 3 == wave - 1) {
+            // the next chunk's coefficients, by waves 2 and 3 in turn, while the chain runs this one
+            if (c + 1 < nchunk && wave >= 2 && (c + 1) % 2 == wave - 2) {
 #pragma unroll
                 for (int g2 = 0; g2 < CV / 64; ++g2) coef64((c + 1) * CV + 64 * g2);
             }
+            if (wave == 1) s_chunk(c);
             continue;
         }
         const int jc = c * CV;                  // first position of the chunk
@@ -1786,20 +1832,22 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             };
             auto run = [&](const fal_v16 (&vv)[U], const float (&vs)[U]) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    yb = FAL_MAD(vv[u], vs[u], yb);
-                    S = __fadd_rn(S, vs[u]);   // not contracted on the CPU
-                }
+                for (int u = 0; u < U; ++u) yb = FAL_MAD(vv[u], vs[u], yb);
             };
+            // the next batch's LDS reads are issued before this batch's steps (a scheduling
+            // barrier: the compiler otherwise sank the vs reads to the top of their own batch and
+            // waited on them there)
             auto fast_run = [&](int j0, int nf) {
                 fal_v16 va[U], vb[U];
                 float sa[U], sb[U];
                 ldb(j0, va, sa);
                 for (int k = 0; k < nf; k += 2) {
                     ldb(j0 + (k + 1) * U, vb, sb);
+                    __builtin_amdgcn_sched_barrier(0);
                     run(va, sa);
                     if (k + 1 >= nf) break;
                     ldb(j0 + (k + 2) * U, va, sa);
+                    __builtin_amdgcn_sched_barrier(0);
                     run(vb, sb);
                 }
             };
@@ -1816,11 +1864,8 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
                     float t = __fmul_rn(h2f((uint16_t) yb), ms[u]);
                     asm("" : "+v"(t));   // two roundings, as f16r
                     const uint32_t ys = upd ? (uint32_t) f2h(t) : yb;
-                    const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
                     const uint32_t yn = FAL_MAD(vv[u], vs[u], ys);
-                    const float Sn = __fadd_rn(Ss, vs[u]);
                     yb = live ? yn : yb;
-                    S = live ? Sn : S;
                 }
             };
             int b = 0;
@@ -1860,10 +1905,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             };
             auto run = [&](const vraw & vv, const float (&vs)[U]) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    yf = fmaf(deq(vv, u), vs[u], yf);   // ggml_vec_mad_f32
-                    S = __fadd_rn(S, vs[u]);
-                }
+                for (int u = 0; u < U; ++u) yf = fmaf(deq(vv, u), vs[u], yf);   // ggml_vec_mad_f32
             };
             auto fast_run = [&](int j0, int nf) {
                 vraw va, vb;
@@ -1888,9 +1930,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
                     const bool live = ((db >> u) & 1u) == 0;
                     const bool upd = __float_as_uint(ms[u]) != 0x3f800000u;
                     const float ys = upd ? __fmul_rn(yf, ms[u]) : yf;   // ggml_vec_scale_f32
-                    const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
                     yf = live ? fmaf(deq(vv, u), vs[u], ys) : yf;
-                    S = live ? __fadd_rn(Ss, vs[u]) : S;
                 }
             };
             int b = 0;
@@ -1904,7 +1944,11 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     }
 
     // ---- output and its optional quantization (k_fattn_exact's epilogue) ----
-    // (wave 0 holds the workgroup's DH outputs, dims DH·dh ..)
+    // (wave 0 holds the workgroup's DH outputs, dims DH·dh ..; wave 1 the sum S)
+    if (wave == 1 && lane == 0) sm.wmax[0] = S;
+    stamp(2);
+    __syncthreads();
+    S = sm.wmax[0];
     float * drow = (float *) ((char *) a.dst + h * a.nb1_dst + iq3 * a.nb2_dst) + DH * dh;
     const float o = wave == 0 ? __fmul_rn(VT ? yf : h2f((uint16_t) yb), 1.0f / S) : 0.0f;
     if (wave == 0) {
@@ -1944,7 +1988,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
         }
     }
-    kt_exit(a.kt);
+    if (wave == 0) kt_exit(a.kt);
 }
 
 // the long-context pair applies: one query row, D = 128, a cache longer than FA_LONG_MIN (and
