@@ -1631,20 +1631,25 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     const int nq = (int) ((n_kv + 255) / 256);   // 64-position groups per wave (uniform)
     // expf's 32-entry 2^(i/32) table in LDS: a global-table gather per position put one memory
     // round trip into every group of the coefficient pass
+    // (its global load is issued with the score loads and stored to LDS after them: a store right
+    // behind the load waited a memory round trip before any score load was issued)
     __shared__ uint64_t exptab[32];
-    if (tid < 32) exptab[tid] = lx_exp2f_tab[tid];
+    const uint64_t etv = lx_exp2f_tab[tid & 31];
     const int seg0 = wave * 64 * nq;   // (positions < NM: 32-bit arithmetic)
     const int nkv = (int) n_kv;
     float sv[NT];
-    uint16_t mvb[NT];
+    // mask values held as 32-bit words: as 16-bit halves each pair was packed right behind its
+    // load, a wait per 64-position group (16 serial memory round trips at 4096 positions)
+    uint32_t mvb[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
         if (i < nq) {
             const int jc = min(seg0 + 64 * i + lane, nkv - 1);
-            mvb[i] = mrow ? *(const uint16_t *) (mrow + 2 * jc) : (uint16_t) 0;
+            mvb[i] = mrow ? (uint32_t) *(const uint16_t *) (mrow + 2 * jc) : 0u;
             sv[i] = srow[jc];
         }
     }
+    if (tid < 32) exptab[tid] = etv;
 
     // phase A: each group's own inclusive max-scan and total (the groups are independent, so their
     // latency chains interleave: one wave per SIMD has nothing else to hide them behind), then the
@@ -1655,7 +1660,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     for (int i = 0; i < NT; ++i) {
         if (i < nq) {   // (a guard, not a break: the loop stays unrolled and the arrays in registers)
             const int j = seg0 + 64 * i + lane;
-            const bool live = j < nkv && h2f(mvb[i]) != -INFINITY;
+            const bool live = j < nkv && h2f((uint16_t) mvb[i]) != -INFINITY;
             const float sj = live ? sv[i] : -INFINITY;
             sv[i] = sj;
             float v = sj;
@@ -1697,7 +1702,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
         if (i < nq) {   // (a guard, not a break: the loop stays unrolled and the arrays in registers)
             const int j = seg0 + 64 * i + lane;
             const float sj = sv[i];
-            const bool live = j < nkv && h2f(mvb[i]) != -INFINITY;
+            const bool live = j < nkv && h2f((uint16_t) mvb[i]) != -INFINITY;
             const float ex = __shfl_up(pm[i], 1, WAVE);
             const float M = fmaxf(Mprev, lane > 0 ? ex : carry[i]);
             const bool upd = live && sj > M;
