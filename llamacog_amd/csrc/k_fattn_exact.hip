@@ -996,7 +996,7 @@ struct dc_smem {
     int mseq[2];                        // [head]: chunk number + 1 that mpub belongs to
     int qseq[2][2];                     // [head][half]: chunk number + 1 whose odd-quarter scores are in
     float mcar[2];                      // [head]: running max through the whole chunk
-    uint64_t etab[32];                  // expf's table (lx_exp2f_tab)
+    uint64_t etab[8][32];               // expf's table (lx_exp2f_tab), a copy per producer wave
     float ol[2 * 128];
     uint16_t vl[2][2][DC_CH * 128];     // [head][stage][position][dim]
 };
@@ -1017,7 +1017,6 @@ __global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_ar
     __shared__ __attribute__((aligned(16))) dc_smem sm;
     const int64_t nchunk = (a.n_kv + CH - 1) / CH;
     const char * mrow = a.mask ? a.mask + (0 % a.mask_ne1) * a.nbm1 : nullptr;
-    if (tid < 32) sm.etab[tid] = lx_exp2f_tab[tid];
     if (tid < 2) { sm.mseq[tid] = 0; sm.mcar[tid] = -INFINITY; }
     if (tid < 4) sm.qseq[tid >> 1][tid & 1] = 0;
     __syncthreads();
@@ -1027,6 +1026,11 @@ __global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_ar
         // even quarters also form the prefix max and coefficients of their half (64 hf .. +63) =====
         const int pw = wave - 4, ph = pw / NQ, qt = pw % NQ, hf = qt / (NQ / 2);
         const bool cw = NQ == 2 || (qt & 1) == 0;   // the coefficient wave of half hf
+        // expf's table: this wave's own copy, its load issued before the mask / K / q loads and
+        // stored once they are all out (one wave filling a shared copy before the launch's first
+        // barrier held every wave behind a memory round trip)
+        const uint64_t etv = lx_exp2f_tab[lane & 31];
+        const uint64_t * etab = sm.etab[pw];
         const int64_t h = 2 * hp + ph, hk = h / G;
         const int qd = lane & 3;
         const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
@@ -1064,6 +1068,7 @@ __global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_ar
                 qf[m][0] = f16r(q4[m].x); qf[m][1] = f16r(q4[m].y); qf[m][2] = f16r(q4[m].z); qf[m][3] = f16r(q4[m].w);
             }
         }
+        if (lane < 32) sm.etab[pw][lane] = etv;   // read back only by this wave (in order)
         float nz = -0.0f;
         asm volatile("" : "+v"(nz));
         const float slope = a.max_bias > 0.0f
@@ -1184,8 +1189,8 @@ __global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_ar
                         const float M = fmaxf(base, dpp_ninf<0x138>(smx));   // max over every position before jl
                         float msv, vsv;
                         if (!live) { msv = 1.0f; vsv = 0.0f; }
-                        else if (sj > M) { msv = M == -INFINITY ? 0.0f : lx_expf_t(M - sj, (const uint64_t *) sm.etab); vsv = 1.0f; }
-                        else { msv = 1.0f; vsv = lx_expf_t(sj - M, (const uint64_t *) sm.etab); }
+                        else if (sj > M) { msv = M == -INFINITY ? 0.0f : lx_expf_t(M - sj, etab); vsv = 1.0f; }
+                        else { msv = 1.0f; vsv = lx_expf_t(sj - M, etab); }
                         cmp[jl] = msv;
                         scp[jl] = vsv;
                         // batch flags: a dead position, a max update or padding past nrun
