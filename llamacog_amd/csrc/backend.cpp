@@ -217,6 +217,29 @@ static enum ggml_status mi_buf_init_tensor(ggml_backend_buffer_t buffer, ggml_te
     return GGML_STATUS_SUCCESS;
 }
 
+// GGML_MI355X_HOSTPROF=1: host time inside the plugin's entry points, summed per kind and printed
+// every 64 graph computes (diagnostic; what libllama spends outside them is the rest of a step)
+enum { HP_SUPPORTS, HP_SET_ASYNC, HP_GET_ASYNC, HP_SET, HP_GET, HP_COMPUTE, HP_SYNC, HP_N };
+static const bool g_hostprof = getenv("GGML_MI355X_HOSTPROF") && atoi(getenv("GGML_MI355X_HOSTPROF")) != 0;
+static std::atomic<long long> g_hp_ns[HP_N];
+static std::atomic<long long> g_hp_cnt[HP_N];
+struct hp_scope {
+    int k; std::chrono::steady_clock::time_point t0;
+    explicit hp_scope(int kind) : k(kind) { if (g_hostprof) t0 = std::chrono::steady_clock::now(); }
+    ~hp_scope() {
+        if (!g_hostprof) return;
+        g_hp_ns[k] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        g_hp_cnt[k] += 1;
+    }
+};
+static void hp_report() {
+    static const char * nm[HP_N] = {"supports_op", "set_async", "get_async", "buf_set", "buf_get", "graph_compute", "synchronize"};
+    fprintf(stderr, "[hostprof]");
+    for (int k = 0; k < HP_N; ++k) fprintf(stderr, " %s %lld x %.1f us", nm[k], g_hp_cnt[k].load(), g_hp_cnt[k] ? g_hp_ns[k].load() / 1e3 / g_hp_cnt[k].load() : 0.0);
+    fprintf(stderr, "\n");
+    for (int k = 0; k < HP_N; ++k) { g_hp_ns[k] = 0; g_hp_cnt[k] = 0; }
+}
+
 static void mi_buf_memset_tensor(ggml_backend_buffer_t buffer, ggml_tensor * tensor, uint8_t value, size_t offset, size_t size) {
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(ctx->device));
@@ -225,6 +248,7 @@ static void mi_buf_memset_tensor(ggml_backend_buffer_t buffer, ggml_tensor * ten
 }
 
 static void mi_buf_set_tensor(ggml_backend_buffer_t buffer, ggml_tensor * tensor, const void * data, size_t offset, size_t size) {
+    hp_scope hp_(HP_SET);
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(ctx->device));
     MI_CHECK(hipMemcpyAsync((char *) tensor->data + offset, data, size, hipMemcpyHostToDevice, hipStreamPerThread));
@@ -232,6 +256,7 @@ static void mi_buf_set_tensor(ggml_backend_buffer_t buffer, ggml_tensor * tensor
 }
 
 static void mi_buf_get_tensor(ggml_backend_buffer_t buffer, const ggml_tensor * tensor, void * data, size_t offset, size_t size) {
+    hp_scope hp_(HP_GET);
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(ctx->device));
     MI_CHECK(hipMemcpyAsync(data, (const char *) tensor->data + offset, size, hipMemcpyDeviceToHost, hipStreamPerThread));
@@ -927,7 +952,11 @@ static void graph_signature(ggml_cgraph * cgraph, std::vector<int64_t> & sig) {
     }
     // sorted: ~11 lookups per node over ~650 nodes every token (host time of graph_compute)
     std::sort(dyn.begin(), dyn.end());
-    auto is_dyn = [&](const ggml_tensor * t) { return std::binary_search(dyn.begin(), dyn.end(), t); };
+    // only CPY nodes and their destinations (views of the caches) can be in the list: every other
+    // tensor skips the search (~11 lookups per node over ~650 nodes every token)
+    auto is_dyn = [&](const ggml_tensor * t) {
+        return (t->op == GGML_OP_CPY || t->op == GGML_OP_VIEW) && std::binary_search(dyn.begin(), dyn.end(), t);
+    };
     auto put_tensor = [&](const ggml_tensor * t) {
         sig.push_back(is_dyn(t) ? 0 : (int64_t) (intptr_t) t->data);
         sig.push_back((int64_t) t->type);
@@ -977,12 +1006,14 @@ static void mi_backend_free(ggml_backend_t backend) {
 }
 
 static void mi_backend_set_tensor_async(ggml_backend_t backend, ggml_tensor * tensor, const void * data, size_t offset, size_t size) {
+    hp_scope hp_(HP_SET_ASYNC);
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
     MI_CHECK(hipMemcpyAsync((char *) tensor->data + offset, data, size, hipMemcpyHostToDevice, ctx->ex.stream));
 }
 
 static void mi_backend_get_tensor_async(ggml_backend_t backend, const ggml_tensor * tensor, void * data, size_t offset, size_t size) {
+    hp_scope hp_(HP_GET_ASYNC);
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
     MI_CHECK(hipMemcpyAsync(data, (const char *) tensor->data + offset, size, hipMemcpyDeviceToHost, ctx->ex.stream));
@@ -1082,6 +1113,7 @@ static void kt_collect(mi_backend_ctx * ctx) {
 }
 
 static void mi_backend_synchronize(ggml_backend_t backend) {
+    hp_scope hp_(HP_SYNC);
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
     MI_CHECK(hipStreamSynchronize(ctx->ex.stream));
@@ -1179,6 +1211,9 @@ static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
 }
 
 static enum ggml_status mi_backend_graph_compute(ggml_backend_t backend, ggml_cgraph * cgraph) {
+    static long hp_graphs = 0;
+    if (g_hostprof && ++hp_graphs % 64 == 0) hp_report();
+    hp_scope hp_(HP_COMPUTE);
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
     ctx->ex.timing = g_timing.load(std::memory_order_relaxed) != 0;
@@ -1326,6 +1361,7 @@ static ggml_backend_buffer_type_t mi_dev_get_host_buffer_type(ggml_backend_dev_t
 }
 
 static bool mi_dev_supports_op(ggml_backend_dev_t dev, const ggml_tensor * op) {
+    hp_scope hp_(HP_SUPPORTS);
     return mi_split_op_ok(dev, op) && op_supported(op);
 }
 
