@@ -343,12 +343,17 @@ def weight_bytes_per_token(cfg: ModelConfig) -> int:
     return tot
 
 
+def model_path(config: str, seed: int = 0, n_layer: int | None = None) -> str:
+    """Where ensure() keeps the synthetic GGUF of a config (LLAMACOG_MODEL_DIR, default /tmp)."""
+    root = os.environ.get("LLAMACOG_MODEL_DIR", "/tmp/llamacog_amd_models")
+    suffix = f"-{n_layer}l" if n_layer else ""
+    return os.path.join(root, f"{config}{suffix}-s{seed}.gguf")
+
+
 def ensure(config: str, path: str | None = None, seed: int = 0, n_layer: int | None = None) -> str:
     cfg = CONFIGS[config]
     if path is None:
-        root = os.environ.get("LLAMACOG_MODEL_DIR", "/tmp/llamacog_amd_models")
-        suffix = f"-{n_layer}l" if n_layer else ""
-        path = os.path.join(root, f"{config}{suffix}-s{seed}.gguf")
+        path = model_path(config, seed, n_layer)
     if not os.path.exists(path):
         write_gguf(cfg, path, seed=seed, n_layer=n_layer)
     return path

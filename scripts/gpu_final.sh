@@ -8,6 +8,7 @@ OUT=gpurun_out/${OUT:-r02}
 mkdir -p $OUT
 # the box's clocks and power (boxes differ by up to ~30 % in decode tok/s)
 (rocm-smi --showclocks --showpower --showmaxpower --showperflevel > $OUT/devinfo.txt 2>&1 || true)
+(df -h /tmp >> $OUT/devinfo.txt 2>&1 || true)
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; grep -E "FAILED|Error" $OUT/pytest_gpu.log | head; tail -5 $OUT/pytest_gpu.log; exit 1; }
 grep -E "passed|failed" $OUT/pytest_gpu.log | tail -1
 timeout -k 10 300 python -c 'import __graft_entry__ as g; g.smoke()' > $OUT/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -5 $OUT/smoke.log; exit 1; }

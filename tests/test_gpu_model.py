@@ -103,19 +103,32 @@ def test_greedy_llama3_8b_full_depth_q4km():
     _check(_greedy("llama3-8b-q4km", 32, 16, True))
 
 
+def _greedy_then_drop(cfg, *args, **kw):
+    """_greedy on a full-size model whose GGUF is deleted afterwards: the 8B, Mixtral and 70B files
+    (5 + 32 + 40 GB) together filled a GPU box's /tmp and the tests after them could not write
+    their own models"""
+    try:
+        return _greedy(cfg, *args, **kw)
+    finally:
+        try:
+            os.remove(gs.model_path(cfg))
+        except OSError:
+            pass
+
+
 def test_greedy_mixtral_full_depth_q5km():
     """All 32 layers of Mixtral-8x7B Q5_K_M (BASELINE.json configs[4]): 8 experts per layer with
     top-2 routing, Q5_K experts, the use_more_bits Q6_K ffn_down layers and Q8_0 attn_k / attn_v
     (src/llama-quant.cpp:300-311); prompt 16 (expert-sorted batch MUL_MAT_ID) then 4 decode steps,
     bit-identical to the CPU backend."""
-    _check(_greedy("mixtral-8x7b-q5km", 16, 4, True))
+    _check(_greedy_then_drop("mixtral-8x7b-q5km", 16, 4, True))
 
 
 def test_greedy_llama3_70b_full_depth_q4km():
     """All 80 layers of Llama-3-70B Q4_K_M (BASELINE.json configs[3], here on one GPU: 41.9 GB of
     weights in one 288 GB HBM): attn_v Q5_K / Q6_K by the 70B rule, the Q4_K / Q6_K ffn_down
     alternation at K = 28672; prompt 8 then 2 decode steps, bit-identical to the CPU backend."""
-    _check(_greedy("llama3-70b-q4km", 8, 2, True))
+    _check(_greedy_then_drop("llama3-70b-q4km", 8, 2, True))
 
 
 def test_greedy_llama3_70b_2layer_q4km():
