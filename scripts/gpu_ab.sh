@@ -1,5 +1,5 @@
 # A/B of one plugin switch: model bit-identity with the switch on, then decode tg off/on/off/on
-# and the in-graph kernel timeline off/on.   VAR=GGML_MI355X_TAILS bash scripts/gpu_ab.sh
+# and the in-graph kernel timeline off/on.   VAR=GGML_MI355X_ROUTER1 ON=1 OFF=0 bash scripts/gpu_ab.sh
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$PWD}
