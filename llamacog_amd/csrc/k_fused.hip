@@ -199,7 +199,9 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     const int64_t nrows = ggml_nrows(norm);
     // batches keep the stand-alone quantizer: one 1024-thread workgroup per row quantizing its 16
     // blocks ran pp512's norms at 20 us a launch against 7.3 + 6.8 us for norm + k_quantize_q8_K
-    int qmode = nrows <= 8 ? consumer_qmode(mm, key) : 0;
+    // (GGML_MI355X_NORM_BQ=1: quantize batches here too — with NORM_NV, a geometry probe)
+    static const bool bq = getenv("GGML_MI355X_NORM_BQ") && atoi(getenv("GGML_MI355X_NORM_BQ")) != 0;
+    int qmode = nrows <= 8 || bq ? consumer_qmode(mm, key) : 0;
     // mm0: a later Q8_0 consumer of the same output beside a K-quant first one
     const bool with0 = qmode == 1 && !qkey && consumer_qmode(mm0, out) == 2;
 
@@ -242,7 +244,11 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     // up to 1024 threads per row, one float4 each (512 / 256 threads with several float4 each
     // measured no faster on Llama-3-8B decode, round 2); the canonical slice order j = w + NW k
     // is the same for every split, so the bits would not change
-    const int nv = ne0 <= 4096 ? 1 : (int) (ne0 / 4096);
+    int nv = ne0 <= 4096 ? 1 : (int) (ne0 / 4096);
+    // GGML_MI355X_NORM_NV=<2,4>: batches (more than 8 rows) on ne0 / (4 nv)-thread workgroups, nv
+    // float4s per thread (the canonical slice order j = w + NW k is the same, so are the bits)
+    static const int nvb = getenv("GGML_MI355X_NORM_NV") ? atoi(getenv("GGML_MI355X_NORM_NV")) : 0;
+    if (nrows > 8 && (nvb == 2 || nvb == 4) && ne0 % (1024 * nvb) == 0 && ne0 / (4 * nvb) >= 256) nv = nvb;
     const dim3 block((unsigned) (ne0 / (4 * nv)));
     p.nrows = nrows;
     const dim3 grid((unsigned) nrows);
