@@ -34,13 +34,18 @@ def _run(tiny_dir, gpus, nproc=2):
     bench = [os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--cpu", "--config", "tiny-q4km",
              "--steps", "4", "--warmup", "1", "--pp", "0", "--roofline-steps", "0", "--no-cpu-baseline",
              "--model-dir", tiny_dir, "--split-config", "tiny-q4km", "--split-steps", "3", "--split-warmup", "1", "--split-pp", "32"]
-    if nproc > 1:
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
-               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + bench
-    else:
-        cmd = [sys.executable] + bench
     env = dict(os.environ, OMP_NUM_THREADS="2")
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    # the rendezvous port is picked free and then released; another process can take it before
+    # torch.distributed.run binds it, so a multi-process run gets one retry on a fresh port
+    for attempt in range(2 if nproc > 1 else 1):
+        if nproc > 1:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                   "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + bench
+        else:
+            cmd = [sys.executable] + bench
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+        if out.returncode == 0:
+            break
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout      # rank 0 only
