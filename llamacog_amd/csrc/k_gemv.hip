@@ -745,14 +745,16 @@ static bool launch_os_id(hipStream_t st, gemv_args & a, int nmat) {
     if (wpr == 4 && (r4 == 1 || r4 == 2 || r4 == 4)) R = r4;
     // GGML_MI355X_MMID_R1: rows per wave of the one-wave-per-row launches (gate / up)
     static const int r1 = getenv("GGML_MI355X_MMID_R1") ? atoi(getenv("GGML_MI355X_MMID_R1")) : 0;
-    if (wpr == 1 && (r1 == 1 || r1 == 2)) R = r1;
+    if (wpr == 1 && (r1 == 1 || r1 == 2 || r1 == 4)) R = r1;
+    if (a.xme % ((4 / wpr) * R) != 0) return false;   // whole row groups per routed slot
     gemv_args b = a;
-    const size_t lds = R == 4 ? os_lds_layout<T, 4, 4>(b)
+    const size_t lds = R == 4 ? (wpr == 1 ? os_lds_layout<T, 4, 1>(b) : os_lds_layout<T, 4, 4>(b))
                      : R == 2 ? (wpr == 1 ? os_lds_layout<T, 2, 1>(b) : os_lds_layout<T, 2, 4>(b))
                               : (wpr == 1 ? os_lds_layout<T, 1, 1>(b) : wpr == 2 ? os_lds_layout<T, 1, 2>(b) : os_lds_layout<T, 1, 4>(b));
     if (lds > 64 * 1024) return false;
     switch (R * 8 + wpr) {
         case 4 * 8 + 4: launch_os_id_v<T, 4, 4>(st, a, nmat); break;
+        case 4 * 8 + 1: launch_os_id_v<T, 4, 1>(st, a, nmat); break;
         case 2 * 8 + 1: launch_os_id_v<T, 2, 1>(st, a, nmat); break;
         case 2 * 8 + 4: launch_os_id_v<T, 2, 4>(st, a, nmat); break;
         case 1 * 8 + 1: launch_os_id_v<T, 1, 1>(st, a, nmat); break;
