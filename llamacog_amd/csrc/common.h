@@ -107,6 +107,28 @@ __device__ __forceinline__ float dppf_xor4(float v) {
     return __int_as_float((threadIdx.x & 4) ? up : dn);
 }
 __device__ __forceinline__ int oct_sum(int v) { v = quad_sum(v); return v + dpp<DPP_HMIRROR>(v); }
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = (uint64_t) __double_as_longlong(v);
+    const uint32_t lo = (uint32_t) dpp<CTRL>((int) (uint32_t) b), hi = (uint32_t) dpp<CTRL>((int) (uint32_t) (b >> 32));
+    return __longlong_as_double((long long) (((uint64_t) hi << 32) | lo));
+}
+// a wave-uniform double sum (all 64 lanes active) in a fixed order that is NOT the shuffle
+// tree's: rows by DPP, then the four row sums by readlane.  For sums whose result is decided
+// against the CPU's own order afterwards (rms_mean_decided)
+__device__ __forceinline__ double wave_sum_rows_f64(double v) {
+    v = __dadd_rn(v, dpp_f64<DPP_XOR1>(v));
+    v = __dadd_rn(v, dpp_f64<DPP_XOR2>(v));
+    v = __dadd_rn(v, dpp_f64<DPP_HMIRROR>(v));
+    v = __dadd_rn(v, dpp_f64<DPP_MIRROR>(v));
+    auto rl = [&](int l) {
+        const uint64_t b = (uint64_t) __double_as_longlong(v);
+        const uint32_t lo = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) b, l);
+        const uint32_t hi = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (b >> 32), l);
+        return __longlong_as_double((long long) (((uint64_t) hi << 32) | lo));
+    };
+    return __dadd_rn(__dadd_rn(rl(0), rl(16)), __dadd_rn(rl(32), rl(48)));
+}
 // wave-uniform max / min of unsigned 32-bit values (all 64 lanes active): rows by DPP, then
 // the four row results by readlane
 __device__ __forceinline__ uint32_t wave_umax(uint32_t v) {

@@ -931,7 +931,14 @@ __device__ void moe_route_wave(const moe_route_args & a, int64_t t, float lgt, c
     const int lane = threadIdx.x & 63;
     const int n = a.n_exp;
     const float v = lane < n ? __fmul_rn(lgt, a.scale) : -INFINITY;
-    const float mx = wave_max(v);
+    // the max of lanes 0..15 (n < 16) by DPP within row 0, then broadcast (the shuffle tree was
+    // six ds_bpermute round trips)
+    float m = v;
+    m = fmaxf(m, dppf_xor1(m));
+    m = fmaxf(m, dppf_xor2(m));
+    m = fmaxf(m, __int_as_float(dpp<DPP_HMIRROR>(__float_as_int(m))));
+    m = fmaxf(m, __int_as_float(dpp<DPP_MIRROR>(__float_as_int(m))));
+    const float mx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 0));
     const float e = lane < n ? lx_expf_t(__fsub_rn(v, mx), etab) : 0.0f;   // expf_cr, its table from LDS
     // uniform values by v_readlane (a shuffle per step was a ds_bpermute round trip each)
     double s = 0.0;
@@ -942,6 +949,38 @@ __device__ void moe_route_wave(const moe_route_args & a, int64_t t, float lgt, c
     float * p = (float *) (a.probs + t * a.nb_p);
     int32_t * o = (int32_t *) (a.order + t * a.nb_o);
     if (lane < n) p[lane] = pl;
+    // distinct probabilities: the exchange sort's result is the descending order, so each lane
+    // forms its own rank and every output is stored in parallel; a tie (or a NaN) takes the
+    // exchange sort below, whose order among equal values is its own
+    {
+        const float me = lane < n ? pl : -INFINITY;
+        int rank = 0;
+        bool tie = !(me == me);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const float pj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(me), j));
+            rank += pj > me ? 1 : 0;
+            tie = tie || (pj == me && j != lane);
+        }
+        if (__ballot(lane < n && tie) == 0 && a.n_used <= n) {
+            if (lane < n) o[rank] = lane;
+            if (a.stage & 2) {
+                const bool top = lane < n && rank < a.n_used;
+                if (top) ((float *) (a.w + t * a.nb_w))[rank] = pl;
+                if (a.wsum) {
+                    double ws = 0.0;   // in rank order, as the CPU's SUM_ROWS
+                    for (int k = 0; k < a.n_used; ++k) {
+                        const int src = __builtin_ctzll(__ballot(lane < n && rank == k));
+                        ws += (double) __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pl), src));
+                    }
+                    const float sf = (float) ws;
+                    if (lane == 0) *(float *) (a.wsum + t * a.nb_s) = sf;
+                    if (a.wn && top) ((float *) (a.wn + t * a.nb_n))[rank] = pl / sf;
+                }
+            }
+            return;
+        }
+    }
     float sv[16];
     int32_t ov[16];
     // the sort on per-lane copies (a shuffle keeps them in VGPRs: branch-free selects, where the
@@ -1326,26 +1365,29 @@ __global__ __launch_bounds__(1024) void k_moe_router1(const moe_router_args a) {
     __shared__ double wpart[16];
     __shared__ float smean, lg[16];
     const float * w = (const float *) (a.W + wave * a.nb01);
-    float wv[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) wv[s] = w[64 * s + lane];
-    const uint64_t et = lx_exp2f_tab[tid & 31];   // stored to LDS once the loads are all issued
     const int NV = K / 4;   // float4s of the row
-    // phase stamps (GGML_MI355X_KTRACE_RAW=moe_router): slot 2 + i, written by thread 0
-    auto stamp = [&](int i) { if (a.kt && tid == 0) a.kt[2 + i] = __builtin_amdgcn_s_memrealtime(); };
+    // x and the norm weight first, then the router rows: the loads return in order, so the norm
+    // runs while the 128 KiB of rows are still arriving (issued behind the rows, the norm waited
+    // for all of them: 2.3 us to its first sum); NV <= 4 NT (the launcher checks)
+    float4 x4[4], w4[4];
     if (a.px) {
-        // x and the norm weight both in flight with the router rows (the weight's first touch
-        // is a memory round trip of its own); NV <= 4 NT (the launcher checks)
-        float4 x4[4], w4[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int v = tid + NT * u;
             if (v < NV) { x4[u] = *(const float4 *) (a.px + 4 * v); w4[u] = *(const float4 *) (a.pw + 4 * v); }
         }
+    }
+    float wv[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) wv[s] = w[64 * s + lane];
+    const uint64_t et = lx_exp2f_tab[tid & 31];   // stored to LDS once the loads are all issued
+    // phase stamps (GGML_MI355X_KTRACE_RAW=moe_router): slot 2 + i, written by thread 0
+    auto stamp = [&](int i) { if (a.kt && tid == 0) a.kt[2 + i] = __builtin_amdgcn_s_memrealtime(); };
+    if (a.px) {
         double acc = 0.0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) if (tid + NT * u < NV) acc = __dadd_rn(acc, sq4(x4[u]));
-        acc = wave_sum(acc);
+        acc = wave_sum_rows_f64(acc);   // any order: the mean is decided against the CPU's below
         if (lane == 0) wpart[wave] = acc;
         __syncthreads();
         stamp(0);
@@ -1368,12 +1410,8 @@ __global__ __launch_bounds__(1024) void k_moe_router1(const moe_router_args a) {
             y.z = __fmul_rn(__fmul_rn(x4[u].z, scale), w4[u].z); y.w = __fmul_rn(__fmul_rn(x4[u].w, scale), w4[u].w);
             *(float4 *) (xs + 4 * v) = y;
             *(float4 *) (yo + 4 * v) = y;
-            if (a.qs) {   // wave w's 256 elements of this pass are one Q8_K block (NT % 64 == 0)
-                const float q[4] = {y.x, y.y, y.z, y.w};
-                const int64_t c0 = 4 * (int64_t) (v - lane);
-                q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
-            }
         }
+        // (its Q8_K quantization runs after the logits, on the waves the route leaves idle)
     } else {
         for (int v = tid; v < NV; v += NT) *(float4 *) (xs + 4 * v) = *(const float4 *) ((const float *) a.X + 4 * v);
     }
@@ -1392,12 +1430,16 @@ __global__ __launch_bounds__(1024) void k_moe_router1(const moe_router_args a) {
     }
     // REDUCE of the 4 x 16 accumulators, (a[l] + a[32 + l]) + (a[16 + l] + a[48 + l]), then the
     // _mm512_reduce_add_ps tree (k_mmv_f_exact's order) as lane-parallel halvings
-    float r = __fadd_rn(acc, __shfl_down(acc, 32, WAVE));
-    r = __fadd_rn(r, __shfl_down(r, 16, WAVE));
-    r = __fadd_rn(__shfl_down(r, 8, WAVE), r);
-    r = __fadd_rn(__shfl_down(r, 4, WAVE), r);
-    r = __fadd_rn(r, __shfl_down(r, 2, WAVE));
-    r = __fadd_rn(r, __shfl_down(r, 1, WAVE));
+    // (lane i + 32 / i + 16 by gfx950's cross-row permlane swaps, i + 8 .. i + 1 by DPP row shifts:
+    // the shuffles were six ds_bpermute round trips)
+    const auto h32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc), __float_as_uint(acc), false, false);
+    float r = __fadd_rn(acc, __uint_as_float(h32[1]));   // lanes 0..31: + lane i + 32
+    const auto h16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+    r = __fadd_rn(r, __uint_as_float(h16[1]));           // lanes 0..15: + lane i + 16
+    r = __fadd_rn(__int_as_float(dpp<0x108>(__float_as_int(r))), r);   // row_shl:8
+    r = __fadd_rn(__int_as_float(dpp<0x104>(__float_as_int(r))), r);
+    r = __fadd_rn(r, __int_as_float(dpp<0x102>(__float_as_int(r))));
+    r = __fadd_rn(r, __int_as_float(dpp<0x101>(__float_as_int(r))));
     if (lane == 0) {
         const float l = r;   // (float) of the double sum of one float
         lg[wave] = l;
@@ -1406,7 +1448,18 @@ __global__ __launch_bounds__(1024) void k_moe_router1(const moe_router_args a) {
     stamp(3);
     __syncthreads();
     stamp(4);
-    if (wave == 0) moe_route_wave(a.r, 0, lane < n ? lg[lane] : 0.0f, etab);
+    if (wave == 0) {
+        moe_route_wave(a.r, 0, lane < n ? lg[lane] : 0.0f, etab);
+    } else if (a.px && a.qs) {
+        // the normalized row's Q8_K blocks from LDS, by waves 1.. while wave 0 routes (formed
+        // before the logits, they cost 0.5 us on the path to the route): lane l quantizes
+        // elements 4l .. 4l + 3 of its block, as the norm's own wave did
+        for (int b = wave - 1; b < K / 256; b += NT / 64 - 1) {
+            const float4 y = *(const float4 *) (xs + 256 * b + 4 * lane);
+            const float q[4] = {y.x, y.y, y.z, y.w};
+            q8K_wave(q, lane, a.qs + 256 * b, a.qsum + 16 * b, a.qd + b);
+        }
+    }
     if (a.kt && tid == 0) a.kt[1] = __builtin_amdgcn_s_memrealtime();
 }
 

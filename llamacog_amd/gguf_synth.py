@@ -59,6 +59,10 @@ class ModelConfig:
     # attn_v: Q4_K -> Q5_K); a real 70B is recognised by its 80 layers, the 2-layer parity model
     # of the same shapes sets it explicitly
     v_q5k_70b: bool = False
+    # router rows 2i + 1 equal to rows 2i (ffn_gate_inp): every token's expert probabilities come in
+    # equal pairs, so the top-k ARGSORT meets ties (its exchange order decides which slot each
+    # tied expert takes)
+    router_ties: bool = False
 
     @property
     def head_dim(self) -> int:
@@ -85,6 +89,10 @@ CONFIGS = {
     # Q5_K experts, layer 1 the use_more_bits Q6_K ffn_down
     "mixtral-2l-q5km": ModelConfig("Mixtral-8x7B-2layer-synthetic", 4096, 2, 32, 8, 14336, 32000, "q5_k_m",
                                    n_ctx_train=32768, rope_base=1000000.0, n_expert=8, n_expert_used=2),
+    # the same with tied router rows (the router's tie path)
+    "mixtral-2l-ties-q5km": ModelConfig("Mixtral-8x7B-2layer-ties-synthetic", 4096, 2, 32, 8, 14336, 32000, "q5_k_m",
+                                        n_ctx_train=32768, rope_base=1000000.0, n_expert=8, n_expert_used=2,
+                                        router_ties=True),
     # fast parity models: full Llama-3-8B layer shapes, 2 layers
     "llama3-8b-2l-q4km": ModelConfig("Llama-3-8B-2layer-synthetic", 4096, 2, 32, 8, 14336, 128256, "q4_k_m"),
     "llama3-8b-2l-q8_0": ModelConfig("Llama-3-8B-2layer-q8-synthetic", 4096, 2, 32, 8, 14336, 128256, "q8_0"),
@@ -94,6 +102,8 @@ CONFIGS = {
     # small Mixtral-style MoE (4 experts, top-2), Q5_K_M
     "tiny-moe-q5km": ModelConfig("tiny-moe-synthetic", 512, 4, 8, 2, 1024, 4096, "q5_k_m", n_ctx_train=2048,
                                  n_expert=4, n_expert_used=2),
+    "tiny-moe-ties-q5km": ModelConfig("tiny-moe-ties-synthetic", 512, 4, 8, 2, 1024, 4096, "q5_k_m", n_ctx_train=2048,
+                                      n_expert=4, n_expert_used=2, router_ties=True),
 }
 
 
@@ -320,6 +330,9 @@ def write_gguf(cfg: ModelConfig, path: str, seed: int = 0, n_layer: int | None =
             # per-tensor seed: files are identical regardless of which tensors were generated
             rng = np.random.default_rng([seed, idx])
             data = tensor_data(name, ne, t, rng)
+            if cfg.router_ties and name.endswith("ffn_gate_inp.weight"):
+                rows = data.view(np.float32).reshape(ne[1], ne[0])
+                rows[1::2] = rows[0::2]
             assert data.nbytes == nbytes(ne, t), (name, data.nbytes, nbytes(ne, t))
             f.write(data.tobytes())
             f.write(b"\0" * ((-data.nbytes) % ALIGN))

@@ -84,6 +84,15 @@ def test_greedy_mixtral_2layer_q5km():
     _check(_greedy("mixtral-2l-q5km", 32, 16, True))
 
 
+@pytest.mark.parametrize("cfg", ["tiny-moe-ties-q5km", "mixtral-2l-ties-q5km"])
+def test_greedy_moe_router_ties(cfg):
+    """Router rows in equal pairs (gguf_synth router_ties): every token's expert probabilities tie,
+    so the top-k order among equal values is the CPU's exchange sort's own (ggml-cpu/ops.cpp
+    argsort); the fused router's rank path must hand such tokens to its exchange sort.  The
+    Mixtral shapes take the one-workgroup router (K = 4096), the tiny model the counter one."""
+    _check(_greedy(cfg, 16, 16, True))
+
+
 def test_greedy_llama3_8b_2layer_q4km():
     _check(_greedy("llama3-8b-2l-q4km", 32, 16, True))
 
