@@ -59,6 +59,10 @@ struct gemv_args {
     } pro;
     unsigned long long * kt;              // in-graph kernel timeline region (nullable)
     uint32_t wl_off;                      // one-shot kernel: LDS byte offset of the weight slices
+    // one-shot kernel: LDS bytes between a wave's row slices (os_geo SLICE, or the slice itself
+    // rounded to 16 B when compact), the records' LDS byte offset and their dwords per row (in
+    // place: a row's records overwrite its own slice once fetched, os_lds_layout)
+    uint32_t sls, rec_off, rec_st;
     // MUL_MAT_ID of one token (gemv_mmid; the one-shot kernel's ID instance only): matrix i is a
     // stack (W[i], experts xnb02 bytes apart) whose routed slots are stacked as its rows: row
     // s * xme + r is row r of expert *(xids + s * xids_nb0) (read on the device), its output
@@ -414,7 +418,7 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     float rc = 0.0f;
     if (MODE == 0 && p.rres) rc = p.rres[min((W1 ? grow0 + wrc1 : row0 + wrc), p.M[0] - 1)];
     // ---- weight DMA: this wave's R row slices -> its LDS region (nt: read once per token) ----
-    uint8_t * mine = wl + (size_t) wave * R * G::SLICE;
+    uint8_t * mine = wl + (size_t) wave * R * p.sls;
     {
         const int nt_w = min(WAVE, p.ntasks - WAVE * wsub);
         const int seg = (nt_w / T::per_block) * T::blk_bytes;
@@ -430,8 +434,10 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
 #pragma unroll
             for (int i = 0; i < G::NI; ++i) {
                 const int off = min(i * 1024 + 16 * lane, seg - 16);
-                __builtin_amdgcn_global_load_lds((const void *) (src + off), (gemv_lds_t) (mine + r * G::SLICE + i * 1024), 16, 0,
-                                                 MI_WNT ? 2 : 0);
+                // lanes past the slice write nothing (a compact stride leaves no padding after it)
+                if (i * 1024 + 16 * lane < seg)
+                    __builtin_amdgcn_global_load_lds((const void *) (src + off), (gemv_lds_t) (mine + r * p.sls + i * 1024), 16, 0,
+                                                     MI_WNT ? 2 : 0);
             }
         }
     }
@@ -464,17 +470,18 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     }
     // ---- this wave's weights are in LDS (the issuing wave's vmcnt covers its own DMAs) ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t * xb = xr;
+    uint32_t * xb = xr + p.rec_off / 4;
+    const int rst = (int) p.rec_st;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         typename T::raw w;
-        T::template fetch<typename lds_loader<T>::type>(mine + r * G::SLICE - (int64_t) wsub * G::SEG, tt, w);
-        T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * nb * T::RS);
+        T::template fetch<typename lds_loader<T>::type>(mine + r * p.sls - (int64_t) wsub * G::SEG, tt, w);
+        T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * rst);
     }
     if constexpr (W1) {
         __syncthreads();   // every wave's records are in
         if (wave != 0) return;
-        const float v = T::walk(xb + (size_t) wrc1 * nb * T::RS, nb, ws1);
+        const float v = T::walk(xb + (size_t) wrc1 * rst, nb, ws1);
         const int64_t row = grow0 + wr1;
         if (wr1 < RPG && ws1 == 0 && row < M) {
             if (p.rres) p.rxsum[row] = __fadd_rn(v, rc);   // ADD(v, res): the CPU's single f32 add
@@ -490,11 +497,11 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     constexpr bool W1E = WPR == 1 && MODE != 0 && RPG * T::LPR <= WAVE;
     if constexpr (W1E) {
         if (wave == 0) {
-            const float v = T::walk(xb + (size_t) wrc1 * nb * T::RS, nb, ws1);
+            const float v = T::walk(xb + (size_t) wrc1 * rst, nb, ws1);
             if (wr1 < RPG && ws1 == 0) res[wr1] = v;
         }
     } else if (wsub == 0) {
-        const float v = T::walk(xb + (size_t) (rowl0 + wrc) * nb * T::RS, nb, ws);
+        const float v = T::walk(xb + (size_t) (rowl0 + wrc) * rst, nb, ws);
         if (wr < R && ws == 0) {
             if constexpr (MODE == 0) {
                 if (row0 + wr < M) {
@@ -648,16 +655,39 @@ static bool os_aligned(const gemv_args & a, int nmat) {
     return true;
 }
 
+// GGML_MI355X_OS_COMPACT=0: row slices at os_geo's 1-KiB multiple and records in a region of
+// their own (A/B); default: slices at their own size rounded to 16 B, and at one wave per row
+// the records in place over the slices
+static bool os_compact() {
+    static const bool on = !getenv("GGML_MI355X_OS_COMPACT") || atoi(getenv("GGML_MI355X_OS_COMPACT")) != 0;
+    return on;
+}
+
+// the plain slice layout (the two-body launches): records first, slices at os_geo's stride
+template <class T, int R, int WPR>
+static void os_plain_geo(gemv_args & a) {
+    a.sls = os_geo<T>::SLICE;
+    a.rec_off = 0;
+    a.rec_st = (uint32_t) ((a.ntasks / T::per_block) * T::RS);
+}
+
 template <class T, int R, int WPR>
 static size_t os_lds_layout(gemv_args & a) {
     constexpr int RPG = (4 / WPR) * R;
-    size_t off = r16((size_t) RPG * (a.ntasks / T::per_block) * T::RS * 4);
+    const int64_t nb = a.ntasks / T::per_block;
+    const uint32_t sls = os_compact() ? (uint32_t) r16(os_geo<T>::SEG) : (uint32_t) os_geo<T>::SLICE;
+    // in place: one wave per row (a row's records are its own wave's) and a row's records fit its slice
+    const bool inplace = os_compact() && WPR == 1 && (size_t) nb * T::RS * 4 <= sls;
+    size_t off = inplace ? 0 : r16((size_t) RPG * nb * T::RS * 4);
     if (a.pro.kind) {
         a.pro.lds_off = (uint32_t) off;
         off = r16(off + pro_lds_bytes(a.pro.n, a.pro.qmode));
     }
     a.wl_off = (uint32_t) off;
-    return off + (size_t) 4 * R * os_geo<T>::SLICE;
+    a.sls = sls;
+    a.rec_off = inplace ? (uint32_t) off : 0;
+    a.rec_st = inplace ? sls / 4 : (uint32_t) (nb * T::RS);
+    return off + (size_t) 4 * R * sls;
 }
 
 template <class T, int R, int WPR, int MODE>
@@ -777,6 +807,8 @@ static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2,
         off = r16(off + pro_lds_bytes(a1.pro.n, a1.pro.qmode));
     }
     a1.wl_off = a2.wl_off = (uint32_t) off;
+    os_plain_geo<T1, R1, WPR>(a1);
+    os_plain_geo<T2, R2, WPR>(a2);
     const size_t lds = off + std::max((size_t) 4 * R1 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
     const unsigned grid = (unsigned) (ng1 + ng2);
     a1.kt = g_kt_ctx ? g_kt_ctx->kt_take(a1.pro.kind ? "gemv2+pro+epi" : "gemv2+epi", grid, 64 * NWV) : nullptr;
@@ -797,6 +829,8 @@ static void launch_os2m_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2
     const size_t off = r16(std::max((size_t) (NWV / WPR1) * R1 * (a1.ntasks / T1::per_block) * T1::RS * 4,
                                     (size_t) (NWV / WPR2) * R2 * (a2.ntasks / T2::per_block) * T2::RS * 4));
     a1.wl_off = a2.wl_off = (uint32_t) off;
+    os_plain_geo<T1, R1, WPR1>(a1);
+    os_plain_geo<T2, R2, WPR2>(a2);
     const size_t lds = off + std::max((size_t) 4 * R1 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
     const unsigned grid = (unsigned) (ng1 + ng2);
     a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv2+epi", grid, 64 * NWV) : nullptr;
