@@ -63,6 +63,7 @@ struct gemv_args {
     // rounded to 16 B when compact), the records' LDS byte offset and their dwords per row (in
     // place: a row's records overwrite its own slice once fetched, os_lds_layout)
     uint32_t sls, rec_off, rec_st;
+    int rec_bar;                          // in place at several waves per row: all fetches, a barrier, then the records
     // MUL_MAT_ID of one token (gemv_mmid; the one-shot kernel's ID instance only): matrix i is a
     // stack (W[i], experts xnb02 bytes apart) whose routed slots are stacked as its rows: row
     // s * xme + r is row r of expert *(xids + s * xids_nb0) (read on the device), its output
@@ -472,11 +473,22 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t * xb = xr + p.rec_off / 4;
     const int rst = (int) p.rec_st;
+    if (WPR > 1 && R > 1 && p.rec_bar) {
+        // a row's records go over wave 0's slice of it, written by all of the row's waves: every
+        // wave has fetched its slices before any record is stored
+        typename T::raw w[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        typename T::raw w;
-        T::template fetch<typename lds_loader<T>::type>(mine + r * p.sls - (int64_t) wsub * G::SEG, tt, w);
-        T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * rst);
+        for (int r = 0; r < R; ++r) T::template fetch<typename lds_loader<T>::type>(mine + r * p.sls - (int64_t) wsub * G::SEG, tt, w[r]);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r) T::rec(w[r], tt, x, active, xb + (size_t) (rowl0 + r) * rst);
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            typename T::raw w;
+            T::template fetch<typename lds_loader<T>::type>(mine + r * p.sls - (int64_t) wsub * G::SEG, tt, w);
+            T::rec(w, tt, x, active, xb + (size_t) (rowl0 + r) * rst);
+        }
     }
     if constexpr (W1) {
         __syncthreads();   // every wave's records are in
@@ -668,6 +680,7 @@ template <class T, int R, int WPR>
 static void os_plain_geo(gemv_args & a) {
     a.sls = os_geo<T>::SLICE;
     a.rec_off = 0;
+    a.rec_bar = 0;
     a.rec_st = (uint32_t) ((a.ntasks / T::per_block) * T::RS);
 }
 
@@ -676,8 +689,14 @@ static size_t os_lds_layout(gemv_args & a) {
     constexpr int RPG = (4 / WPR) * R;
     const int64_t nb = a.ntasks / T::per_block;
     const uint32_t sls = os_compact() ? (uint32_t) r16(os_geo<T>::SEG) : (uint32_t) os_geo<T>::SLICE;
-    // in place: one wave per row (a row's records are its own wave's) and a row's records fit its slice
-    const bool inplace = os_compact() && WPR == 1 && (size_t) nb * T::RS * 4 <= sls;
+    // in place: a row's records fit a slice; at one wave per row they overwrite the row's own
+    // slice once fetched, at several (GGML_MI355X_OS_IPW=0: not in place) wave 0's slice of the
+    // row after a barrier behind every wave's fetches
+    static const bool ipw = !getenv("GGML_MI355X_OS_IPW") || atoi(getenv("GGML_MI355X_OS_IPW")) != 0;
+    // (not at one row per wave group: there the barrier's registers cost more workgroups per CU
+    // than the records' LDS, Q6_K down 72 vs 57 VGPRs)
+    const bool inplace = os_compact() && (WPR == 1 || (ipw && R > 1)) && (size_t) nb * T::RS * 4 <= sls;
+    a.rec_bar = inplace && WPR > 1;
     size_t off = inplace ? 0 : r16((size_t) RPG * nb * T::RS * 4);
     if (a.pro.kind) {
         a.pro.lds_off = (uint32_t) off;
