@@ -129,6 +129,13 @@ __device__ __forceinline__ double wave_sum_rows_f64(double v) {
     };
     return __dadd_rn(__dadd_rn(rl(0), rl(16)), __dadd_rn(rl(32), rl(48)));
 }
+// the sum of a 16-lane row by DPP (every lane of the row holds it); same caveat on the order
+__device__ __forceinline__ double row_sum16_f64(double v) {
+    v = __dadd_rn(v, dpp_f64<DPP_XOR1>(v));
+    v = __dadd_rn(v, dpp_f64<DPP_XOR2>(v));
+    v = __dadd_rn(v, dpp_f64<DPP_HMIRROR>(v));
+    return __dadd_rn(v, dpp_f64<DPP_MIRROR>(v));
+}
 // wave-uniform max / min of unsigned 32-bit values (all 64 lanes active): rows by DPP, then
 // the four row results by readlane
 __device__ __forceinline__ uint32_t wave_umax(uint32_t v) {

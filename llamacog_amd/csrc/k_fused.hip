@@ -71,13 +71,14 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
         }
         acc = __dadd_rn(acc, sq4(v[k]));
     }
-    acc = wave_sum(acc);
+    // (DPP sums in any order — the mean is decided against the CPU's sequential one below; the
+    // shuffle trees were ds_bpermute round trips on the path to every consumer of the norm)
+    acc = wave_sum_rows_f64(acc);
     if (lane == 0) wpart[wave] = acc;
     __syncthreads();
     if (wave == 0) {
         double t = lane < NW ? wpart[lane] : 0.0;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) t = __dadd_rn(t, __shfl_xor(t, o, WAVE));
+        t = row_sum16_f64(t);
         if (lane == 0) {
             float mean;
             if (!rms_mean_decided(t, p.ne0, mean))

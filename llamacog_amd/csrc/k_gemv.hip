@@ -105,7 +105,7 @@ __device__ __forceinline__ bool pro_load(const gemv_args::pro_t & r, int ps, flo
 // rms_mean_decided; undecided: the CPU's loop)
 __device__ float pro_scale(const gemv_args::pro_t & r, double s) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    s = wave_sum(s);
+    s = wave_sum_rows_f64(s);   // (DPP: any order, decided below)
     __shared__ double wp[4];
     __shared__ float pm;
     if (lane == 0) wp[wave] = s;
