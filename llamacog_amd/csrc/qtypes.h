@@ -430,9 +430,10 @@ struct g_q6_K {
 
 // Q8_0, vec_dot order (arch/x86/quants.c:965; tinyBLAS_Q0_AVX, llamafile/sgemm.cpp:914-961, has
 // the same for batches).  Task = one 32-block; its eight dot4 are the eight classes.
-// Record: cls[8], dx·dy.
+// Record: cls[8], dx·dy — nine dwords, stored one by one (padded to 12 for 16-B stores it held
+// Mixtral's Q8_0 K / V launches to 6 workgroups per CU by LDS)
 struct g_q8_0 {
-    static constexpr int per_block = 1, blk_bytes = 34, RS = 12, LPR = 8;   // 16-B aligned records
+    static constexpr int per_block = 1, blk_bytes = 34, RS = 9, LPR = 8;
     struct act { int4 a0, a1; float dy; };
     __device__ static void load(const gemv_act & A, int t, act & x) {
         const int4 * ap = (const int4 *) (A.qs + (int64_t) t * 32);
@@ -449,11 +450,11 @@ struct g_q8_0 {
     __device__ static void rec(const raw & w, int t, const act & x, bool active, uint32_t * rr) {
         if (!active) return;
         uint32_t * r = rr + t * RS;
-        *(uint4 *) r = make_uint4((uint32_t) dot4(w.qa.x, x.a0.x, 0), (uint32_t) dot4(w.qa.y, x.a0.y, 0),
-                                  (uint32_t) dot4(w.qa.z, x.a0.z, 0), (uint32_t) dot4(w.qa.w, x.a0.w, 0));
-        *(uint4 *) (r + 4) = make_uint4((uint32_t) dot4(w.qb.x, x.a1.x, 0), (uint32_t) dot4(w.qb.y, x.a1.y, 0),
-                                        (uint32_t) dot4(w.qb.z, x.a1.z, 0), (uint32_t) dot4(w.qb.w, x.a1.w, 0));
-        *(uint4 *) (r + 8) = make_uint4(asu(h2f((uint16_t) w.d16) * x.dy), 0u, 0u, 0u);
+        r[0] = (uint32_t) dot4(w.qa.x, x.a0.x, 0); r[1] = (uint32_t) dot4(w.qa.y, x.a0.y, 0);
+        r[2] = (uint32_t) dot4(w.qa.z, x.a0.z, 0); r[3] = (uint32_t) dot4(w.qa.w, x.a0.w, 0);
+        r[4] = (uint32_t) dot4(w.qb.x, x.a1.x, 0); r[5] = (uint32_t) dot4(w.qb.y, x.a1.y, 0);
+        r[6] = (uint32_t) dot4(w.qb.z, x.a1.z, 0); r[7] = (uint32_t) dot4(w.qb.w, x.a1.w, 0);
+        r[8] = asu(h2f((uint16_t) w.d16) * x.dy);
     }
     __device__ static float walk(const uint32_t * rr, int nb, int s) { return hsum8_lanes(class_chain(rr, nb, RS, 8, s)); }
 };
