@@ -40,7 +40,7 @@ MFMA_I8_PEAK_TOPS = 5000.0
 # algorithmic work of one pp512 of Llama-3-8B: 2*6.98e9*512 layer matmuls +
 # output (last token) + attention
 PP512_FLOP = 7.22e12
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r05", "final3", "pmc_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r05", "final4", "pmc_traffic.json")
 
 
 def parse():
@@ -374,7 +374,7 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, gpu, n_ctx, r):
             "peak_measured": round(hbm, 1) if hbm > 0 else None,
             "frac_of_measured": round(achieved / hbm, 4) if achieved and hbm > 0 else None,
             "traffic": traffic,
-            "traffic_source": "profiles/r05/final3/pmc_traffic.json: a separate rocprofv3 --pmc FETCH_SIZE pass (scripts/gpu_r05_bench.sh), not this run" if traffic else None,
+            "traffic_source": "profiles/r05/final4/pmc_traffic.json: a separate rocprofv3 --pmc FETCH_SIZE pass (scripts/gpu_r05_bench.sh), not this run" if traffic else None,
             # the event-timed pass runs eagerly (hipGraph replay off, so every GEMV launch carries
             # its own events); the replayed product path's per-launch times are in the in-graph
             # timeline (scripts/ktrace.py, profiles/r04/ktrace_base.txt)
