@@ -40,7 +40,13 @@ MFMA_I8_PEAK_TOPS = 5000.0
 # algorithmic work of one pp512 of Llama-3-8B: 2*6.98e9*512 layer matmuls +
 # output (last token) + attention
 PP512_FLOP = 7.22e12
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r05", "final4", "pmc_traffic.json")
+# HBM bytes per decode-GEMV launch from a separate rocprofv3 --pmc FETCH_SIZE pass of the SAME
+# model (scripts/gpu_r06_bench.sh, scripts/pmc_traffic.py), one file per --config
+TRAFFIC_DIR = os.path.join("profiles", "r06", "pmc")
+
+
+def traffic_file(config):
+    return os.path.join(TRAFFIC_DIR, f"pmc_traffic_{config}.json")
 
 
 def parse():
@@ -359,9 +365,10 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, gpu, n_ctx, r):
         # HBM bytes per GEMV launch from the PMC pass (rocprofv3 --pmc FETCH_SIZE, x2 gfx950
         # correction), committed with its command under profiles/ (scripts/gpu_final.sh, scripts/pmc_traffic.py)
         traffic = None
-        if os.path.exists(TRAFFIC_FILE):
+        tf = traffic_file(a.config) if not a.layers else None
+        if tf and os.path.exists(os.path.join(REPO, tf)):
             try:
-                traffic = json.load(open(TRAFFIC_FILE)).get("gemv_bytes_per_launch")
+                traffic = json.load(open(os.path.join(REPO, tf))).get("gemv_bytes_per_launch")
             except Exception:
                 traffic = None
         roof = {
@@ -374,7 +381,7 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, gpu, n_ctx, r):
             "peak_measured": round(hbm, 1) if hbm > 0 else None,
             "frac_of_measured": round(achieved / hbm, 4) if achieved and hbm > 0 else None,
             "traffic": traffic,
-            "traffic_source": "profiles/r05/final4/pmc_traffic.json: a separate rocprofv3 --pmc FETCH_SIZE pass (scripts/gpu_r05_bench.sh), not this run" if traffic else None,
+            "traffic_source": f"{tf}: a separate rocprofv3 --pmc FETCH_SIZE pass of {a.config} (scripts/gpu_r06_bench.sh), not this run" if traffic else None,
             # the event-timed pass runs eagerly (hipGraph replay off, so every GEMV launch carries
             # its own events); the replayed product path's per-launch times are in the in-graph
             # timeline (scripts/ktrace.py, profiles/r04/ktrace_base.txt)

@@ -149,6 +149,11 @@ void exec_ctx::time_end(int kind, double bytes, hipEvent_t beg) {
     pending.push_back({beg, end, bytes, kind});
 }
 
+// a timed region that launched nothing: its begin event goes back to the pool, no sample
+void exec_ctx::time_cancel(hipEvent_t beg) {
+    if (beg) event_pool.push_back(beg);
+}
+
 void exec_ctx::collect_timing() {
     if (pending.empty()) return;
     std::lock_guard<std::mutex> lk(g_timing_mtx);
@@ -191,9 +196,12 @@ struct mi_buffer_ctx {
     void * dev_ptr;
 };
 
+static void up_drain(int device);
+
 static void mi_buf_free(ggml_backend_buffer_t buffer) {
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(ctx->device));
+    up_drain(ctx->device);   // no upload still writes into it
     MI_CHECK(hipFree(ctx->dev_ptr));
     delete ctx;
 }
@@ -235,14 +243,105 @@ struct hp_scope {
 static void hp_report() {
     static const char * nm[HP_N] = {"supports_op", "set_async", "get_async", "buf_set", "buf_get", "graph_compute", "synchronize"};
     fprintf(stderr, "[hostprof]");
-    for (int k = 0; k < HP_N; ++k) fprintf(stderr, " %s %lld x %.1f us", nm[k], g_hp_cnt[k].load(), g_hp_cnt[k] ? g_hp_ns[k].load() / 1e3 / g_hp_cnt[k].load() : 0.0);
+    for (int k = 0; k < HP_N; ++k) {
+        // swap-and-read: scopes still closing on other threads land in the next report
+        const long long c = g_hp_cnt[k].exchange(0), ns = g_hp_ns[k].exchange(0);
+        fprintf(stderr, " %s %lld x %.1f us", nm[k], c, c ? ns / 1e3 / c : 0.0);
+    }
     fprintf(stderr, "\n");
-    for (int k = 0; k < HP_N; ++k) { g_hp_ns[k] = 0; g_hp_cnt[k] = 0; }
+}
+
+// ------------------------------------------------------------------------------------------
+// small host -> device uploads.  The scheduler copies a decode step's graph inputs (positions,
+// KQ mask, output ids, the CPU split's embedding rows) with the synchronous set_tensor
+// (ggml-backend.cpp:1374-1398; ggml-cuda.cu:604-610 copies and waits).  A set of at most UP_MAX
+// bytes is instead copied into a pinned staging ring and issued as hipMemcpyAsync on the
+// device's upload stream: the caller's buffer is free on return (the memcpy), and every later
+// user of the device's memory is ordered behind the uploads:
+//   * a backend stream (graph_compute, the async tensor calls) waits on an event recorded after
+//     the last upload, once per new upload (up_fence);
+//   * the synchronous buffer calls (get / memset / copy / clear / free / a large set) drain the
+//     upload stream first (up_drain).
+// The scheduler synchronises with the previous use of an input before it sets it (the lines
+// cited above), so the write-after-read order is the synchronous copy's.
+// GGML_MI355X_ASYNC_SET=0 keeps the synchronous copy.
+// ------------------------------------------------------------------------------------------
+struct mi_upload {
+    std::mutex mtx;
+    hipStream_t stream = nullptr;
+    char * ring = nullptr;       // pinned staging
+    size_t head = 0;
+    uint64_t seq = 0;            // uploads issued
+    uint64_t drained = 0;        // uploads known complete
+    hipEvent_t ev = nullptr;
+    uint64_t ev_seq = 0;         // the upload ev was last recorded behind
+};
+static constexpr size_t UP_MAX = 64 << 10, UP_RING = 8 << 20;
+static constexpr int UP_MAXDEV = 64;
+static mi_upload g_up[UP_MAXDEV];
+
+static bool up_enabled() {
+    static const bool on = !getenv("GGML_MI355X_ASYNC_SET") || atoi(getenv("GGML_MI355X_ASYNC_SET")) != 0;
+    return on;
+}
+
+static void up_drain_locked(mi_upload & u) {
+    if (u.drained == u.seq) return;
+    MI_CHECK(hipStreamSynchronize(u.stream));
+    u.drained = u.seq;
+}
+
+// every upload to this HIP device is complete (the synchronous buffer calls)
+static void up_drain(int device) {
+    if (device < 0 || device >= UP_MAXDEV) return;
+    mi_upload & u = g_up[device];
+    std::lock_guard<std::mutex> lk(u.mtx);
+    up_drain_locked(u);
+}
+
+// stream st (of this HIP device) waits for every upload issued so far; seen = the upload count
+// it last waited for (per backend)
+static void up_fence(int device, hipStream_t st, uint64_t & seen) {
+    if (device < 0 || device >= UP_MAXDEV) return;
+    mi_upload & u = g_up[device];
+    std::lock_guard<std::mutex> lk(u.mtx);
+    if (u.seq == seen) return;
+    if (u.drained != u.seq) {
+        if (u.ev_seq != u.seq) {
+            MI_CHECK(hipEventRecord(u.ev, u.stream));
+            u.ev_seq = u.seq;
+        }
+        MI_CHECK(hipStreamWaitEvent(st, u.ev, 0));
+    }
+    seen = u.seq;
+}
+
+// the asynchronous small set (current device = device); false: the caller copies synchronously
+static bool up_set(int device, void * dst, const void * data, size_t size) {
+    if (!up_enabled() || size > UP_MAX || device < 0 || device >= UP_MAXDEV) return false;
+    mi_upload & u = g_up[device];
+    std::lock_guard<std::mutex> lk(u.mtx);
+    if (!u.stream) {
+        MI_CHECK(hipStreamCreateWithFlags(&u.stream, hipStreamNonBlocking));
+        MI_CHECK(hipHostMalloc((void **) &u.ring, UP_RING, hipHostMallocDefault));
+        MI_CHECK(hipEventCreateWithFlags(&u.ev, hipEventDisableTiming));
+    }
+    const size_t n = (size + 255) & ~size_t(255);
+    if (u.head + n > UP_RING) {   // wrap: the copies still reading the ring are waited for
+        up_drain_locked(u);
+        u.head = 0;
+    }
+    memcpy(u.ring + u.head, data, size);
+    MI_CHECK(hipMemcpyAsync(dst, u.ring + u.head, size, hipMemcpyHostToDevice, u.stream));
+    u.head += n;
+    ++u.seq;
+    return true;
 }
 
 static void mi_buf_memset_tensor(ggml_backend_buffer_t buffer, ggml_tensor * tensor, uint8_t value, size_t offset, size_t size) {
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(ctx->device));
+    up_drain(ctx->device);
     MI_CHECK(hipMemsetAsync((char *) tensor->data + offset, value, size, hipStreamPerThread));
     MI_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
@@ -251,6 +350,8 @@ static void mi_buf_set_tensor(ggml_backend_buffer_t buffer, ggml_tensor * tensor
     hp_scope hp_(HP_SET);
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(ctx->device));
+    if (up_set(ctx->device, (char *) tensor->data + offset, data, size)) return;
+    up_drain(ctx->device);
     MI_CHECK(hipMemcpyAsync((char *) tensor->data + offset, data, size, hipMemcpyHostToDevice, hipStreamPerThread));
     MI_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
@@ -259,6 +360,7 @@ static void mi_buf_get_tensor(ggml_backend_buffer_t buffer, const ggml_tensor * 
     hp_scope hp_(HP_GET);
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(ctx->device));
+    up_drain(ctx->device);
     MI_CHECK(hipMemcpyAsync(data, (const char *) tensor->data + offset, size, hipMemcpyDeviceToHost, hipStreamPerThread));
     MI_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
@@ -270,6 +372,8 @@ static bool mi_buf_cpy_tensor(ggml_backend_buffer_t buffer, const ggml_tensor * 
     auto * sctx = (mi_buffer_ctx *) src->buffer->context;
     auto * dctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(dctx->device));
+    up_drain(sctx->device);
+    up_drain(dctx->device);
     if (sctx->device == dctx->device) {
         MI_CHECK(hipMemcpyAsync(dst->data, src->data, ggml_nbytes(src), hipMemcpyDeviceToDevice, hipStreamPerThread));
     } else {
@@ -282,6 +386,7 @@ static bool mi_buf_cpy_tensor(ggml_backend_buffer_t buffer, const ggml_tensor * 
 static void mi_buf_clear(ggml_backend_buffer_t buffer, uint8_t value) {
     auto * ctx = (mi_buffer_ctx *) buffer->context;
     MI_CHECK(hipSetDevice(ctx->device));
+    up_drain(ctx->device);
     MI_CHECK(hipMemsetAsync(ctx->dev_ptr, value, buffer->size, hipStreamPerThread));
     MI_CHECK(hipStreamSynchronize(hipStreamPerThread));
 }
@@ -721,6 +826,7 @@ struct mi_backend_ctx {
     std::vector<graph_entry> graphs;   // small LRU of recently seen graphs
     uint64_t use_clock = 0;
     bool graphs_broken = false;        // capture failed once: stay eager
+    uint64_t up_seen = 0;              // uploads this stream has waited for (up_fence)
     // hand-off events of cpy_tensor_async (recorded on this stream, waited on by the
     // destination's): a ring created once instead of an event per copy
     std::vector<hipEvent_t> xev;
@@ -1009,6 +1115,7 @@ static void mi_backend_set_tensor_async(ggml_backend_t backend, ggml_tensor * te
     hp_scope hp_(HP_SET_ASYNC);
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
+    up_fence(ctx->device, ctx->ex.stream, ctx->up_seen);
     MI_CHECK(hipMemcpyAsync((char *) tensor->data + offset, data, size, hipMemcpyHostToDevice, ctx->ex.stream));
 }
 
@@ -1016,6 +1123,7 @@ static void mi_backend_get_tensor_async(ggml_backend_t backend, const ggml_tenso
     hp_scope hp_(HP_GET_ASYNC);
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
+    up_fence(ctx->device, ctx->ex.stream, ctx->up_seen);
     MI_CHECK(hipMemcpyAsync(data, (const char *) tensor->data + offset, size, hipMemcpyDeviceToHost, ctx->ex.stream));
 }
 
@@ -1035,6 +1143,10 @@ static bool mi_backend_cpy_tensor_async(ggml_backend_t backend_src, ggml_backend
     auto * sctx = (mi_backend_ctx *) backend_src->context;
     auto * dctx = (mi_backend_ctx *) backend_dst->context;
     const size_t n = ggml_nbytes(dst);
+    MI_CHECK(hipSetDevice(sctx->device));
+    up_fence(sctx->device, sctx->ex.stream, sctx->up_seen);
+    MI_CHECK(hipSetDevice(dctx->device));
+    up_fence(dctx->device, dctx->ex.stream, dctx->up_seen);
     static const p2p_mode mode = p2p_mode_env();
     if (sctx->device != dctx->device && mode != P2P_PEER &&
         p2p_send_recv(src->data, sctx->device, sctx->ex.stream, dst->data, dctx->device, dctx->ex.stream, n)) {
@@ -1211,11 +1323,12 @@ static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
 }
 
 static enum ggml_status mi_backend_graph_compute(ggml_backend_t backend, ggml_cgraph * cgraph) {
-    static long hp_graphs = 0;
-    if (g_hostprof && ++hp_graphs % 64 == 0) hp_report();
+    static std::atomic<long> hp_graphs{0};
+    if (g_hostprof && (hp_graphs.fetch_add(1) + 1) % 64 == 0) hp_report();
     hp_scope hp_(HP_COMPUTE);
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
+    up_fence(ctx->device, ctx->ex.stream, ctx->up_seen);   // the graph's inputs (set_tensor) are in
     ctx->ex.timing = g_timing.load(std::memory_order_relaxed) != 0;
     // whole-graph timing (kind TK_GRAPH: device time between events around the graph;
     // TK_GRAPH_HOST: host time spent in this call) — works with hipGraph replay

@@ -466,11 +466,11 @@ static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tenso
         ggml_tensor * sm = nullptr, * as = nullptr;
         const ggml_tensor * qkey = nullptr;
         if (!mul || !moe_router_nodes(g, node_index(g, mm), n, &sm, &as) || nm->ne[0] % 1024 != 0 || nm->ne[0] > 4096) return;
-        if (!ctx.moe_cnt && !ctx.capturing) {   // the router's arrival counters (k_elem.hip)
-            MI_CHECK(hipMalloc(&ctx.moe_cnt, exec_ctx::MOE_CNT * sizeof(int)));
-            MI_CHECK(hipMemsetAsync(ctx.moe_cnt, 0, exec_ctx::MOE_CNT * sizeof(int), ctx.stream));
-        }
-        if (!ctx.moe_cnt || !dead_after(g, n, pn + 1, nm, {mul})) return;
+        // the router kernel moe_router will pick must be one that forms the norm (k_elem.hip
+        // moe_router_path); the counter kernel's arrival counters exist before the plan relies on them
+        const int path = moe_router_path(mm, true);
+        if (path == MOE_RNONE || (path == MOE_RMW && !moe_router_counters(ctx))) return;
+        if (!dead_after(g, n, pn + 1, nm, {mul})) return;
         const ggml_tensor * c = moe_quant_consumer(g, n, last, mm, &qkey);
         if (c && !(c->src[0]->type == GGML_TYPE_Q4_K || c->src[0]->type == GGML_TYPE_Q5_K || c->src[0]->type == GGML_TYPE_Q6_K))
             qkey = nullptr;
@@ -880,7 +880,7 @@ static bool try_moe_router(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     ggml_tensor * sm = nullptr, * as = nullptr;
     const bool pro = ctx.moe_pro.mm == mm;
     if (!moe_router_nodes(g, i, n, &sm, &as)) {
-        GGML_ASSERT(!pro);   // plan_resid_moe checked this same pattern
+        GGML_ASSERT(!pro);   // plan_resid's MoE branch checked this same pattern
         return false;
     }
     const int ia = node_index(g, as);
@@ -917,7 +917,7 @@ static bool try_moe_router(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
                        dead_after(g, n, node_index(g, dv) + 1, dv, {mul});
     float * wscr = chain ? (float *) ctx.scratch(exec_ctx::MOE_SLOT, 3 * T * n_used * sizeof(float)) : nullptr;
     if (pro) {
-        // the FFN norm formed in this launch (plan_resid_moe): its output stored, its Q8_K
+        // the FFN norm formed in this launch (plan_resid's MoE branch): its output stored, its Q8_K
         // quantization cached for the expert mat-vecs
         const int64_t K = mm->src[1]->ne[0];
         q8_act act;

@@ -1463,6 +1463,34 @@ __global__ __launch_bounds__(1024) void k_moe_router1(const moe_router_args a) {
     if (a.kt && tid == 0) a.kt[1] = __builtin_amdgcn_s_memrealtime();
 }
 
+// which router kernel takes MUL_MAT node mm: MOE_R1 the one-workgroup kernel (one token, K = 4096),
+// MOE_RMW the multi-workgroup counter kernel, MOE_RPLAIN the per-token fallback, MOE_RNONE none.
+// With the norm prologue (pro) only the first two form the FFN norm; plan_resid (dispatch.cpp)
+// asks this same predicate before it hands the norm to the router launch
+int moe_router_path(const ggml_tensor * mm, bool pro) {
+    const ggml_tensor * W = mm->src[0], * X = mm->src[1];
+    const int64_t n = W->ne[1], K = W->ne[0], T = X->ne[1];
+    if (W->type != GGML_TYPE_F32 || X->type != GGML_TYPE_F32 || n > 16 || n < 1 || W->ne[2] != 1 || W->ne[3] != 1 ||
+        X->ne[2] != 1 || X->ne[3] != 1 || X->nb[0] != 4 || W->nb[0] != 4 || mm->nb[0] != 4 || mm->ne[1] != T) return MOE_RNONE;
+    static const bool one = !getenv("GGML_MI355X_ROUTER1") || atoi(getenv("GGML_MI355X_ROUTER1")) != 0;
+    if (one && T == 1 && K == 4096 && ggml_is_contiguous(X) && n >= 4 && n < 16 && (uintptr_t) X->data % 16 == 0) return MOE_R1;
+    // the norm prologue of the counter kernel: one token, K <= 4096 (four float4s per thread), X contiguous
+    if (pro && (T != 1 || K % 1024 != 0 || K > 4096 || !ggml_is_contiguous(X))) return MOE_RNONE;
+    const size_t lds = 2 * K * sizeof(float);
+    if (T <= exec_ctx::MOE_CNT && K % 4 == 0 && K <= 8192 && lds <= 64 * 1024 && X->nb[1] % 16 == 0 && W->nb[1] % 16 == 0 &&
+        ((uintptr_t) X->data % 16) == 0 && ((uintptr_t) W->data % 16) == 0) return MOE_RMW;
+    return pro ? MOE_RNONE : MOE_RPLAIN;
+}
+
+// the multi-workgroup router's arrival counters, allocated once per context (not during capture)
+bool moe_router_counters(exec_ctx & ctx) {
+    if (!ctx.moe_cnt && !ctx.capturing) {
+        MI_CHECK(hipMalloc(&ctx.moe_cnt, exec_ctx::MOE_CNT * sizeof(int)));
+        MI_CHECK(hipMemsetAsync(ctx.moe_cnt, 0, exec_ctx::MOE_CNT * sizeof(int), ctx.stream));
+    }
+    return ctx.moe_cnt != nullptr;
+}
+
 bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr,
                 const moe_router_pro * pro) {
     const ggml_tensor * W = mm->src[0], * X = mm->src[1];
@@ -1488,36 +1516,28 @@ bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_t
     }
     // the tinyBLAS order for >= 2 columns, as mul_mat_vec picks it
     const bool tiny = T >= 2 && K % 16 == 0 && n % 4 == 0 && ggml_is_contiguous(X);
-    if (!ctx.moe_cnt && !ctx.capturing) {
-        MI_CHECK(hipMalloc(&ctx.moe_cnt, exec_ctx::MOE_CNT * sizeof(int)));
-        MI_CHECK(hipMemsetAsync(ctx.moe_cnt, 0, exec_ctx::MOE_CNT * sizeof(int), ctx.stream));
+    int path = moe_router_path(mm, pro != nullptr);
+    if (path == MOE_RMW && !moe_router_counters(ctx)) path = pro ? MOE_RNONE : MOE_RPLAIN;
+    if (path == MOE_RNONE) return false;
+    if (pro) {
+        a.px = pro->x; a.pw = pro->w; a.eps = pro->eps;
+        if (pro->q) { a.qs = pro->q->qs; a.qd = pro->q->d; a.qsum = pro->q->s; }
     }
-    const size_t lds = 2 * K * sizeof(float);
-    // one token, K = 4096: the single-workgroup kernel (GGML_MI355X_ROUTER1=0: the counter one)
-    static const bool one = !getenv("GGML_MI355X_ROUTER1") || atoi(getenv("GGML_MI355X_ROUTER1")) != 0;
-    if (one && T == 1 && K == 4096 && ggml_is_contiguous(X) && n >= 4 && n < 16 && (uintptr_t) X->data % 16 == 0) {
-        if (pro) {
-            a.px = pro->x; a.pw = pro->w; a.eps = pro->eps;
-            if (pro->q) { a.qs = pro->q->qs; a.qd = pro->q->d; a.qsum = pro->q->s; }
-        }
+    if (path == MOE_R1) {
         a.kt = ctx.kt_take("moe_router", 1, (unsigned) (64 * n));
         hipLaunchKernelGGL(k_moe_router1<64>, dim3(1), dim3((unsigned) (64 * n)), 0, ctx.stream, a);
         return true;
     }
-    if (pro) {
-        // the norm prologue: one token, K <= 4096 (four float4s per thread), X contiguous
-        if (T != 1 || K % 1024 != 0 || K > 4096 || !ctx.moe_cnt || !ggml_is_contiguous(X)) return false;
-        a.px = pro->x; a.pw = pro->w; a.eps = pro->eps;
-        if (pro->q) { a.qs = pro->q->qs; a.qd = pro->q->d; a.qsum = pro->q->s; }
-    }
-    if (ctx.moe_cnt && T <= exec_ctx::MOE_CNT && K % 4 == 0 && K <= 8192 && lds <= 64 * 1024 && X->nb[1] % 16 == 0 && W->nb[1] % 16 == 0 &&
-        ((uintptr_t) X->data % 16) == 0 && ((uintptr_t) W->data % 16) == 0) {
+    if (path == MOE_RMW) {
+        const size_t lds = 2 * K * sizeof(float);
         const dim3 grid((unsigned) n, (unsigned) T);
         a.kt = T == 1 ? ctx.kt_take("moe_router", (unsigned) n, 256) : nullptr;
         if (tiny) hipLaunchKernelGGL(k_moe_router_mw<true>, grid, dim3(256), lds, ctx.stream, a, ctx.moe_cnt);
         else hipLaunchKernelGGL(k_moe_router_mw<false>, grid, dim3(256), lds, ctx.stream, a, ctx.moe_cnt);
         return true;
     }
+    // the per-token kernel ignores the prologue's sources: never reached with pro (moe_router_path)
+    GGML_ASSERT(!pro);
     const dim3 block((unsigned) (64 * n));
     if (tiny) hipLaunchKernelGGL(k_moe_router<true>, dim3((unsigned) T), block, 0, ctx.stream, a);
     else hipLaunchKernelGGL(k_moe_router<false>, dim3((unsigned) T), block, 0, ctx.stream, a);

@@ -513,7 +513,11 @@ bool op_mul_mat_id_pair(exec_ctx & ctx, ggml_tensor * dst, ggml_tensor * dst2) {
     }
     if (ctx.timing) ctx.time_begin(TK_MMV, bytes, ev_beg);
     const bool ok = gemv_mmid(ctx, dst, act, dst2);
-    if (ctx.timing) ctx.time_end(TK_MMV, ok ? bytes : 0.0, ev_beg);
+    // declined: the caller's op_mul_mat_id times the same work, so no sample here
+    if (ctx.timing) {
+        if (ok) ctx.time_end(TK_MMV, bytes, ev_beg);
+        else ctx.time_cancel(ev_beg);
+    }
     return ok;
 }
 

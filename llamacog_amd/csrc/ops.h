@@ -90,7 +90,7 @@ struct exec_ctx {
     // RMS_NORM launch that reads it (k_norm_fused's combine source)
     struct moe_pending { const ggml_tensor * mul; const float * wn; int n_used; const ggml_tensor * comb; const float * e; };
     moe_pending moe = {};
-    // the FFN norm the router launch forms (dispatch.cpp plan_resid_moe): x the residual sum the
+    // the FFN norm the router launch forms (dispatch.cpp plan_resid, its MoE branch): x the residual sum the
     // producer stored, w the norm weight; qkey the expert mat-vecs' input for the Q8_K cache
     struct moe_norm_pending { const ggml_tensor * mm; const float * x; const float * w; float eps; const ggml_tensor * qkey; };
     moe_norm_pending moe_pro = {};
@@ -157,6 +157,7 @@ struct exec_ctx {
     hipEvent_t get_event();
     void   time_begin(int kind, double bytes, hipEvent_t & beg);
     void   time_end(int kind, double bytes, hipEvent_t beg);
+    void   time_cancel(hipEvent_t beg);
     void   collect_timing();  // after a stream synchronize
 };
 
@@ -212,6 +213,9 @@ bool moe_route_sort(exec_ctx & ctx, const ggml_tensor * sm, ggml_tensor * as);
 // the router's input formed in the router launch: RMS_NORM(x) * w (eps), stored to the router's
 // src1 and, with q, quantized to Q8_K (the expert mat-vecs' activation)
 struct moe_router_pro { const float * x; const float * w; float eps; const q8_act * q; };
+enum { MOE_RNONE = 0, MOE_R1, MOE_RMW, MOE_RPLAIN };
+int moe_router_path(const ggml_tensor * mm, bool pro);
+bool moe_router_counters(exec_ctx & ctx);
 bool moe_router(exec_ctx & ctx, ggml_tensor * mm, const ggml_tensor * sm, ggml_tensor * as, int n_used, float * wscr,
                 const moe_router_pro * pro = nullptr);
 bool moe_route_weights(exec_ctx & ctx, ggml_tensor * gr, ggml_tensor * sr, ggml_tensor * dv);

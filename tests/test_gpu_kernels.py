@@ -274,6 +274,42 @@ def test_flash_attn_f16_decode_masks_vs_oracle(K, n_kv, Hkv, G, pattern):
     assert_bits(out, ref, f"flash_attn f16 decode {pattern} n_kv={n_kv} G={G}")
 
 
+@pytest.mark.parametrize("n_kv,live,pattern", [(256, 9, "tail"), (256, 136, "tail"), (256, 129, "holes"),
+                                               (256, 256, "increasing"), (128, 100, "tail"), (64, 64, "increasing"),
+                                               (200, 137, "holes"), (1, 1, "tail"), (7, 3, "single"), (256, 250, "sparse")])
+def test_flash_attn_f16_decode_short_vs_oracle(K, n_kv, live, pattern):
+    """The short-context decode kernel (k_fattn_dsh: at most 256 cached positions, tg128's depths):
+    libllama's padded cache (live positions then -inf up to n_kv, a multiple of 256 in the graph),
+    holes and a lone live position inside batches, a single-position cache, and scores rising at
+    every position so the running max updates on every step (every batch takes the general step)."""
+    rng = np.random.default_rng(n_kv * 13 + live)
+    D, Hkv, G = 128, 8, 4
+    H = Hkv * G
+    q = (rng.standard_normal((1, H, D)) * 2).astype(np.float32)
+    kf = rng.standard_normal((n_kv, Hkv, D)).astype(np.float32)
+    if pattern == "increasing":
+        # K row j leans on the group's first query head more and more: its score rises with j
+        for hk in range(Hkv):
+            qd = q[0, hk * G] / np.linalg.norm(q[0, hk * G])
+            kf[:, hk, :] = 0.005 * kf[:, hk, :] + np.arange(n_kv, dtype=np.float32)[:, None] * 0.05 * qd[None, :]
+    k = kf.astype(np.float16)
+    v = rng.standard_normal((n_kv, Hkv, D)).astype(np.float16)
+    m = np.zeros((1, n_kv), dtype=np.float16)
+    m[0, live:] = -np.inf
+    if pattern == "holes":
+        m[0, :live][rng.random(live) < 0.3] = -np.inf
+        m[0, live - 1] = 0
+    elif pattern == "single":
+        m[0, :] = -np.inf
+        m[0, live - 1] = 0
+    elif pattern == "sparse":
+        m[0, :live][rng.random(live) < 0.9] = -np.inf
+        m[0, 0] = 0
+    out = K.flash_attn(q, k.view(np.uint8), v.view(np.uint8), m.view(np.uint16), O.F16, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    ref = O.flash_attn(q, k.view(np.uint8), v.view(np.uint8), m.view(np.uint16), O.F16, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    assert_bits(out, ref, f"flash_attn f16 short decode {pattern} n_kv={n_kv} live={live}")
+
+
 @pytest.mark.parametrize("name,Kd,M", [("q4_K", 4096, 256), ("q5_K", 4096, 200), ("q6_K", 4096, 136),
                                         ("q4_K", 14336, 128), ("q6_K", 14336, 64), ("q4_K", 4096, 100)])
 def test_mul_mat_prefill_bit_exact(K, name, Kd, M):

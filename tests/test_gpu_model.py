@@ -106,10 +106,26 @@ def test_greedy_llama3_8b_2layer_prompt512():
 def test_greedy_llama3_8b_full_depth_q4km():
     """The model bench.py times (BASELINE.json configs[1] / [2]): all 32 layers of Llama-3-8B
     Q4_K_M, where the use_more_bits alternation of Q4_K / Q6_K attn_v and ffn_down over the layers
-    (src/llama-quant.cpp:185-187: 16 Q6_K layers) and the Q6_K output head appear together.  A
-    32-token prompt (MFMA prefill tiles) then 16 greedy tokens (the replayed decode graph): ids and
-    every logit bit-identical to the CPU backend (tools/main/main.cpp --temp 0's selection)."""
-    _check(_greedy("llama3-8b-q4km", 32, 16, True))
+    (src/llama-quant.cpp:185-187: 16 Q6_K layers) and the Q6_K output head appear together.  The
+    benchmarked workload itself (tools/llama-bench/llama-bench.cpp:1747-1795): a 512-token prompt
+    (pp512's ubatch: MFMA prefill tiles, prefill flash attention through all 32 layers) then 128
+    greedy tokens (tg128: the replayed decode graph at KV depths 513..640, past the short-context
+    FA's 256-position chunk): ids and every logit bit-identical to the CPU backend
+    (tools/main/main.cpp --temp 0's selection).  Then, after clearing the cache, an 8-token prompt
+    and 128 tokens: tg128's own depth range (9..136, the short-context decode FA bench.py times)."""
+    path = gs.ensure("llama3-8b-q4km")
+    rng = np.random.default_rng(99)
+    p512 = [1] + rng.integers(300, gs.CONFIGS["llama3-8b-q4km"].n_vocab, 511).tolist()
+    p8 = p512[:8]
+    res = ({}, {})
+    for gpu in (True, False):
+        m = la.Model(path, gpu=gpu, n_ctx=1024, flash_attn=True, n_threads=16)
+        res[0][gpu] = m.greedy(p512, 128)
+        m.clear()
+        res[1][gpu] = m.greedy(p8, 128)
+        m.close()
+    _check(res[0])
+    _check(res[1])
 
 
 def _greedy_then_drop(cfg, *args, **kw):
@@ -128,9 +144,10 @@ def _greedy_then_drop(cfg, *args, **kw):
 def test_greedy_mixtral_full_depth_q5km():
     """All 32 layers of Mixtral-8x7B Q5_K_M (BASELINE.json configs[4]): 8 experts per layer with
     top-2 routing, Q5_K experts, the use_more_bits Q6_K ffn_down layers and Q8_0 attn_k / attn_v
-    (src/llama-quant.cpp:300-311); prompt 16 (expert-sorted batch MUL_MAT_ID) then 4 decode steps,
+    (src/llama-quant.cpp:300-311); prompt 64 (expert-sorted batch MUL_MAT_ID on the MFMA tile:
+    >= 64 routed pairs per batch) then 32 decode steps (the one-shot ID GEMV and the fused router),
     bit-identical to the CPU backend."""
-    _check(_greedy_then_drop("mixtral-8x7b-q5km", 16, 4, True))
+    _check(_greedy_then_drop("mixtral-8x7b-q5km", 64, 32, True))
 
 
 def test_greedy_llama3_70b_full_depth_q4km():
