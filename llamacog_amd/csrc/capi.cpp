@@ -560,6 +560,7 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
     // 3: the decode flash attention of 0 over a q8_0 cache
     const ggml_type fa_kv = which == 3 ? GGML_TYPE_Q8_0 : GGML_TYPE_F16;
     if (which == 3) which = 0;
+    const bool fa_probe = which == 2;
     if (which == 2) {
         MI_CHECK(hipMalloc(&prof, 8 * sizeof(unsigned long long)));
         MI_CHECK(hipMemset(prof, 0, 8 * sizeof(unsigned long long)));
@@ -725,7 +726,10 @@ extern "C" GGML_BACKEND_API double mi355x_bench_op(int which, int64_t a, int64_t
         const char * nm[8] = {"A(mask)", "0(V issue)", "1(scores)", "2(softmax coef)", "3(wait V)", "3(recurrence)", "-", "-"};
         const char * nmp[8] = {"barrier+wait", "1(scores)", "2(coef)", "3(recurrence)", "chunks", "-", "-", "-"};
         const char * nmd[8] = {"p:mask", "p:V issue", "p:scores", "p:coef", "p:V wait", "p:barrier", "chain busy", "chain wait"};
+        const char * nms[8] = {"p0:loads in", "p0:barrier", "p0:block 0 ready", "p0:done", "c0:barrier", "c0:block 0 seen", "c0:chain end", "quantized"};
+        const bool dsh = fa_probe && a <= 256 && (getenv("GGML_MI355X_FA_DSH") == nullptr || atoi(getenv("GGML_MI355X_FA_DSH")) != 0);
         if (which == 302) for (int i = 0; i < 8; ++i) nm[i] = nmp[i];
+        else if (dsh) for (int i = 0; i < 8; ++i) nm[i] = nms[i];
         else if (getenv("GGML_MI355X_FA_DEC2") == nullptr || atoi(getenv("GGML_MI355X_FA_DEC2")) != 0) for (int i = 0; i < 8; ++i) nm[i] = nmd[i];
         fprintf(stderr, "FA phases (s_memtime ticks per launch, wg 0):");
         for (int i = 0; i < 8; ++i) fprintf(stderr, " %s=%.0f", nm[i], (double) h[i] / (iters + 3));

@@ -73,11 +73,14 @@ __device__ __forceinline__ int dot4(int a, int b, int c) { return __builtin_amdg
 // host can rebuild every instrumented launch's start, dispatch ramp, end and the gaps between
 // launches inside a REPLAYED hipGraph (rocprofv3 cannot trace replayed graphs on ROCm 7.2).
 __device__ __forceinline__ unsigned kt_wg() { return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); }
-__device__ __forceinline__ void kt_enter(unsigned long long * kt) {
-    if (kt && threadIdx.x == 0) kt[(1 + blockDim.x / 64) * kt_wg()] = __builtin_amdgcn_s_memrealtime();
+// stride: the region's slots per workgroup (exec_ctx::kt_take's 1 + threads / 64), passed in by the
+// kernel: blockDim is a 16-bit load from the dispatch packet, a memory round trip that held wave 0
+// of every traced workgroup at its entry
+__device__ __forceinline__ void kt_enter(unsigned long long * kt, unsigned stride) {
+    if (kt && threadIdx.x == 0) kt[stride * kt_wg()] = __builtin_amdgcn_s_memrealtime();
 }
-__device__ __forceinline__ void kt_exit(unsigned long long * kt) {
-    if (kt && (threadIdx.x & 63) == 0) kt[(1 + blockDim.x / 64) * kt_wg() + 1 + threadIdx.x / 64] = __builtin_amdgcn_s_memrealtime();
+__device__ __forceinline__ void kt_exit(unsigned long long * kt, unsigned stride) {
+    if (kt && (threadIdx.x & 63) == 0) kt[stride * kt_wg() + 1 + threadIdx.x / 64] = __builtin_amdgcn_s_memrealtime();
 }
 
 template <typename T>

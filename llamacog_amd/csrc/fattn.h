@@ -41,6 +41,10 @@ void launch_fattn_exact(hipStream_t stream, const fa_args & a, int64_t nq3);
 constexpr int FA_DEC2_NQ4_MIN = 256;
 int fattn_dec2_threads(const fa_args & a);   // the launch's workgroup size (timeline slots)
 bool fattn_dec2_ok(const fa_args & a, int64_t nq3);
+// decode, D = 128, f16 cache of at most 256 positions (tg128's depths): every load issued at the
+// launch's start, two heads (one KV head) per 512-thread workgroup (GGML_MI355X_FA_DSH=0: dec2)
+bool fattn_dsh_ok(const fa_args & a, int64_t nq3);
+void launch_fattn_dsh(hipStream_t stream, const fa_args & a, int64_t nq3);
 // the prefill batch tile (k_fattn_pf) runs this batch and can quantize its output (qmode 1):
 // f16 cache, D = 128, a GQA group of 4, 8 or 16 heads
 bool fattn_pf_quant_ok(const fa_args & a);

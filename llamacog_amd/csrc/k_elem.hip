@@ -1207,7 +1207,7 @@ __global__ __launch_bounds__(1024) void k_moe_router(const moe_router_args a) {
 template <bool TINY>
 __global__ __launch_bounds__(256) void k_moe_router_mw(const moe_router_args a, int * cnt) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    kt_enter(a.kt);
+    kt_enter(a.kt, 5);
     __shared__ uint64_t etab[32];   // expf's table, fetched with the first loads
     const uint64_t et = lx_exp2f_tab[tid & 31];
     const int e = blockIdx.x;
@@ -1347,7 +1347,7 @@ __global__ __launch_bounds__(256) void k_moe_router_mw(const moe_router_args a, 
             moe_route16(a.r, t, lg);
         }
     }
-    kt_exit(a.kt);   // waves 1-3: the hand-off; wave 0 of the last workgroup: after the route
+    kt_exit(a.kt, 5);   // waves 1-3: the hand-off; wave 0 of the last workgroup: after the route
 }
 
 // One token, K = 64 KS, in ONE workgroup of 64 n_exp threads with no hand-off: wave e holds its
@@ -1359,7 +1359,7 @@ __global__ __launch_bounds__(1024) void k_moe_router1(const moe_router_args a) {
     constexpr int K = 64 * KS;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int NT = blockDim.x, n = a.r.n_exp;
-    kt_enter(a.kt);
+    kt_enter(a.kt, 1 + (unsigned) n);
     __shared__ uint64_t etab[32];
     __shared__ __attribute__((aligned(16))) float xs[K];
     __shared__ double wpart[16];

@@ -112,6 +112,9 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
         unsigned long long * kts = ctx.kt_take("fa_scores", (unsigned) (ceil_div(a.n_kv, (int64_t) FAL_PB) * a.Hkv), 256);
         a.kt = ctx.kt_take("fa_chain", (unsigned) (a.H * FAL_DSPLIT), FAL_THREADS);
         launch_fattn_long(ctx.stream, a, sco, kts);
+    } else if (fattn_dsh_ok(a, nq3)) {
+        a.kt = ctx.kt_take("fa_dsh", (unsigned) (a.H / 2 * nq3), 512);
+        launch_fattn_dsh(ctx.stream, a, nq3);
     } else if (fattn_dec2_ok(a, nq3)) {
         a.kt = ctx.kt_take("fa_dec2", (unsigned) (a.H / 2 * nq3), (unsigned) fattn_dec2_threads(a));
         launch_fattn_dec2(ctx.stream, a, nq3);

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
     constexpr int CH = C::CH, U = C::U, NM = D / 16, NB = D / 32;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int qd = tid & 3;                 // lane in the quad of a position (phase 1)
-    kt_enter(a.kt);
+    kt_enter(a.kt, 5);
     const int64_t iq1 = blockIdx.x;
     const int64_t h = blockIdx.y % a.H;
     const int64_t iq3 = blockIdx.y / a.H;
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(256, OCC) void k_fattn_exact(const fa_args a) {
             q8K_wave(q, lane, a.qs + iq1 * K + c0, a.qsum + iq1 * (K / 16) + c0 / 16, a.qd + iq1 * (K / 256) + c0 / 256);
         }
     }
-    kt_exit(a.kt);
+    kt_exit(a.kt, 5);
 }
 
 // ==== prefill: a block of query rows x the G query heads of one KV head per workgroup ========
@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_ar
     constexpr int D = 128, NM = D / 16, CH = DC_CH, U = DC_U;
     constexpr int PQ = CH / NQ, NPQ = PQ / 16;   // positions per producer wave, score passes over them
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    kt_enter(a.kt);
+    kt_enter(a.kt, 1 + 4 + 2 * NQ);
     const int64_t hp = blockIdx.x;          // head pair: heads 2 hp, 2 hp + 1
     const int64_t iq3 = blockIdx.y;
     const int64_t G = a.H / a.Hkv;
@@ -1334,7 +1334,7 @@ __global__ __launch_bounds__(64 * (4 + 2 * NQ), 1) void k_fattn_dec2(const fa_ar
             else q8_0_wave(q, lane, true, a.qs + c0, a.qd + c0 / 32, a.qsum + c0 / 32);
         }
     }
-    kt_exit(a.kt);
+    kt_exit(a.kt, 1 + 4 + 2 * NQ);
 }
 
 bool fattn_dec2_ok(const fa_args & a, int64_t nq3) {
@@ -1349,6 +1349,374 @@ void launch_fattn_dec2(hipStream_t st, const fa_args & a, int64_t nq3) {
     const dim3 grid((unsigned) (a.H / 2), (unsigned) nq3);
     if (a.n_kv > FA_DEC2_NQ4_MIN) hipLaunchKernelGGL(k_fattn_dec2<4>, grid, dim3(64 * (4 + 2 * 4)), 0, st, a);
     else hipLaunchKernelGGL(k_fattn_dec2<2>, grid, dim3(64 * (4 + 2 * 2)), 0, st, a);
+}
+
+// ==== decode, D = 128, f16 cache, at most DS_MAXKV cached positions (tg128's depths) ====
+// The arithmetic of k_fattn_dec2 (the AVX-512 ggml_vec_dot_f16 scores, the prefix-max (ms, vs)
+// coefficients, the f16 VKQ recurrence with the CPU's two roundings; ops.cpp:7015-7232), pipelined
+// in 16-position blocks so the serial recurrence starts after the first block's coefficients
+// instead of after every score of the cache (dec2 hands over 128-position chunks; at tg128's
+// depths that is one chunk, and its chains waited for all of it):
+//   * waves 0-3 are the chains: wave c runs the recurrence of head c / 2, dims 64 (c % 2) + lane.
+//     Each stages the V bytes it reads itself (its half of every row, LDS-DMA, its own copy), so
+//     its own vmcnt says which rows are in and no other wave waits on V;
+//   * waves 4-7 are producers: producer p owns blocks p, p + 4, p + 8, p + 12.  It loads the whole
+//     mask (the last live position bounds every later load), its first block's K rows and both
+//     heads' q at once, then the K of its later blocks; per block it forms both heads' scores
+//     from one K load, their running max (a 16-lane DPP scan inside the block; the maximum before
+//     the block handed over by the previous block's producer through LDS), the (ms, vs)
+//     coefficients with libm expf and a "general" flag per 8-position batch, and marks the block
+//     ready;
+//   * the two heads' 256 outputs (one Q8_K block) are quantized here for the following projection.
+// Both heads of a workgroup read one KV head (GQA group even), so K is fetched once.  The mask and V
+// loads are inline asm with explicit waits (the compiler puts no vmcnt wait of its own behind them).
+constexpr int DS_MAXKV = 256, DS_U = 8, DS_B = 16, DS_NB = DS_MAXKV / DS_B, DS_PAD = 2 * DS_U;
+constexpr int DS_NP = 4, DS_OWN = DS_NB / DS_NP;   // producers, blocks per producer
+constexpr int DS_VROWS = DS_MAXKV + DS_U;          // V rows staged (the chain reads one batch ahead)
+
+struct ds_smem {
+    float sc[2][DS_MAXKV + DS_PAD];        // [head] vs (0 where dead)
+    float cm[2][DS_MAXKV + DS_PAD];        // ms (1 where dead)
+    float mk[2][DS_MAXKV + DS_PAD];        // 0 live, -inf dead
+    float sr[DS_NP][DS_OWN][2][DS_B];      // [producer][its block][head] raw scores (-inf dead)
+    float carry[2][DS_NB];                 // [head] running max through block b
+    int cflag[DS_NB];                      // block b's carry is in
+    int ready[DS_NB];                      // block b's coefficients and flags are in
+    uint8_t bfl[2][2 * DS_NB + 8];         // [head][batch] general step
+    uint64_t etab[DS_NP][32];              // expf's table (lx_exp2f_tab), a copy per producer
+    float ol[2 * 128];
+    uint16_t vc[4][DS_VROWS * 64];         // [chain wave][position][its 64 dims]
+};
+
+// a bounded LDS spin: a hand-off that never completes traps rather than reading stale data
+__device__ __forceinline__ void ds_wait_flag(int * f) {
+    int guard = 0;
+    while (lds_ld(f) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++guard > (1 << 22)) __builtin_trap();
+    }
+    asm volatile("" ::: "memory");
+}
+
+// the mask word of position j (0xfc00 = -inf past the cache) as an asm load: the caller waits
+__device__ __forceinline__ uint32_t ds_mask_ld(const char * mask, int j, int n_kv) {
+    uint32_t v = 0xfc00;
+    if (j < n_kv) {
+        if (mask) asm volatile("global_load_ushort %0, %1, off" : "=v"(v) : "v"(mask + 2 * j) : "memory");
+        else v = 0;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(512, 1) void k_fattn_dsh(const fa_args a) {
+    constexpr int D = 128, NM = D / 16, U = DS_U, B = DS_B;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    kt_enter(a.kt, 9);
+    // mi355x_bench_op's phase split (workgroup (0, 0), waves 0 and 4): cycles from the start to
+    // each mark, kept in registers and added to a.prof at the end
+    const bool prof = a.prof && blockIdx.x == 0 && blockIdx.y == 0 && lane == 0 && (wave == 0 || wave == 4);
+    const unsigned long long t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto mark = [&](int i) { if (prof) pt[i] = __builtin_amdgcn_s_memtime() - t0; };
+    const int64_t hp = blockIdx.x;          // head pair: heads 2 hp, 2 hp + 1 (one KV head)
+    const int64_t iq3 = blockIdx.y;
+    const int64_t hk = (2 * hp) / (a.H / a.Hkv);
+    const int n_kv = (int) a.n_kv;
+    __shared__ __attribute__((aligned(16))) ds_smem sm;
+    const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
+    const char * vbase = a.v + hk * a.nbv2 + iq3 * a.nbv3;
+    // every wave reads the whole mask (4 positions a lane): nrun = the last live position + 1
+    uint32_t mk4[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mk4[k] = ds_mask_ld(a.mask, 64 * k + lane, n_kv);
+    if (tid < DS_NB) { sm.cflag[tid] = 0; sm.ready[tid] = 0; }
+    auto nrun_of = [&]() {
+        int last = -1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const unsigned long long bl = __ballot((mk4[k] & 0xffff) != 0xfc00);
+            if (bl) last = 64 * k + 63 - __clzll(bl);
+        }
+        return last + 1;
+    };
+
+    if (wave >= 4) {
+        // ================= producers =================
+        const int pw = wave - 4, qd = lane & 3;
+        const uint64_t etv = lx_exp2f_tab[lane & 31];
+        uint2 kh[DS_OWN][NM];
+        auto load_k = [&](int i) {   // block pw + DS_NP i: its K rows, 4 lanes a position
+            const int j = min(B * (pw + DS_NP * i) + (lane >> 2), n_kv - 1);
+            const char * krow = kbase + (int64_t) j * a.nbk1 + 8 * qd;
+#pragma unroll
+            for (int m = 0; m < NM; ++m) kh[i][m] = ld8(krow + 32 * m);
+        };
+        // the mask value of each owned block's position B b + lane / 4
+        uint32_t mkb[DS_OWN];
+#pragma unroll
+        for (int i = 0; i < DS_OWN; ++i) mkb[i] = ds_mask_ld(a.mask, B * (pw + DS_NP * i) + (lane >> 2), n_kv);
+        if (B * pw < n_kv) load_k(0);
+        float4 q4[2][NM];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float * qrow = (const float *) (a.q + (2 * hp + h) * a.nbq2 + iq3 * a.nbq3);
+#pragma unroll
+            for (int m = 0; m < NM; ++m) q4[h][m] = *(const float4 *) (qrow + 16 * m + 4 * qd);
+        }
+        __syncthreads();   // the flags' zeros (all waves), while the loads are in flight
+        // (the builtin, not asm: the compiler then knows these loads are in and puts no wait for
+        // them after the later blocks' loads below; the asm mask loads are older, so in too)
+        __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+        asm volatile("" : "+v"(mk4[0]), "+v"(mk4[1]), "+v"(mk4[2]), "+v"(mk4[3]), "+v"(mkb[0]), "+v"(mkb[1]), "+v"(mkb[2]),
+                     "+v"(mkb[3]));
+        mark(0);
+        if (lane < 32) sm.etab[pw][lane] = etv;
+        const int nrun = nrun_of(), nblk = (nrun + B - 1) / B;
+        const int nown = nblk > pw ? (nblk - pw + DS_NP - 1) / DS_NP : 0;
+#pragma unroll
+        for (int i = 1; i < DS_OWN; ++i)
+            if (i < nown) load_k(i);
+        float qf[2][NM][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                qf[h][m][0] = f16r(q4[h][m].x); qf[h][m][1] = f16r(q4[h][m].y);
+                qf[h][m][2] = f16r(q4[h][m].z); qf[h][m][3] = f16r(q4[h][m].w);
+            }
+        float nz = -0.0f;
+        asm volatile("" : "+v"(nz));
+        float slope[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t hh = 2 * hp + h;
+            slope[h] = a.max_bias > 0.0f
+                ? (float) ((uint32_t) hh < a.n_head_log2 ? pow((double) a.m0, (double) (hh + 1))
+                                                        : pow((double) a.m1, (double) (2 * ((uint32_t) hh - a.n_head_log2) + 1)))
+                : 1.0f;
+        }
+        mark(1);
+        const uint64_t * etab = sm.etab[pw];
+        // the scores of block i into sr (quad lane 0 of each position)
+        auto scores = [&](int i) {
+            const int b = pw + DS_NP * i;
+            const int j = B * b + (lane >> 2);
+            const float mv = h2f((uint16_t) mkb[i]);
+            const bool live = mv != -INFINITY && j < nrun;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float w = dot_f16_mix_d128(kh[i], qf[h], nz);
+                if (qd == 0) {
+                    float sv = __fmul_rn(w, a.scale);
+                    if (a.softcap != 0.0f) sv = __fmul_rn(a.softcap, tanhf(sv));
+                    sm.sr[pw][i][h][lane >> 2] = live ? __fadd_rn(sv, __fmul_rn(slope[h], mv)) : -INFINITY;
+                }
+            }
+        };
+        // block i's coefficients from its scores and the running max before it
+        auto coef = [&](int i) {
+            const int b = pw + DS_NP * i;
+            dc_wave_lds_order();
+            // lanes 0-31: head lane / 16, position B b + lane % 16
+            const int hc = (lane >> 4) & 1, pj = B * b + (lane & 15);
+            const float sj = sm.sr[pw][i][hc][lane & 15];
+            const bool lj = sj != -INFINITY;
+            const float inc = fmaxf(sj, dpp_ninf<0x111>(sj));
+            const float inc2 = fmaxf(inc, dpp_ninf<0x112>(inc));
+            const float inc3 = fmaxf(inc2, dpp_ninf<0x114>(inc2));
+            const float incl = fmaxf(inc3, dpp_ninf<0x118>(inc3));   // max over the row's lanes <= this one
+            const float excl = dpp_ninf<0x111>(incl);                 // ... < this one
+            const float bmax0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 15));
+            const float bmax1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 31));
+            float cin0 = -INFINITY, cin1 = -INFINITY;
+            if (b > 0) {
+                ds_wait_flag(&sm.cflag[b - 1]);
+                cin0 = sm.carry[0][b - 1];
+                cin1 = sm.carry[1][b - 1];
+            }
+            if (lane == 0) {
+                sm.carry[0][b] = fmaxf(cin0, bmax0);
+                sm.carry[1][b] = fmaxf(cin1, bmax1);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                lds_st(&sm.cflag[b], 1);
+            }
+            const float M = fmaxf(hc ? cin1 : cin0, excl);   // max over every live position before pj
+            float msv, vsv;
+            if (!lj) { msv = 1.0f; vsv = 0.0f; }
+            else if (sj > M) { msv = M == -INFINITY ? 0.0f : lx_expf_t(M - sj, etab); vsv = 1.0f; }
+            else { msv = 1.0f; vsv = lx_expf_t(sj - M, etab); }
+            const bool gen = pj < nrun ? (!lj || sj > M) : true;
+            const unsigned long long gb = __ballot(gen && lane < 32);
+            if (lane < 32) {
+                sm.sc[hc][pj] = vsv;
+                sm.cm[hc][pj] = msv;
+                sm.mk[hc][pj] = lj ? 0.0f : -INFINITY;
+            }
+            if (lane < 4) sm.bfl[lane >> 1][2 * b + (lane & 1)] = ((gb >> (8 * lane)) & 0xff) ? 1 : 0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) lds_st(&sm.ready[b], 1);
+        };
+        if (nown > 0) {
+            scores(0);
+            coef(0);
+            mark(2);
+#pragma unroll
+            for (int i = 1; i < DS_OWN; ++i)
+                if (i < nown) scores(i);
+#pragma unroll
+            for (int i = 1; i < DS_OWN; ++i)
+                if (i < nown) coef(i);
+        }
+        mark(3);
+    } else {
+        // ================= chains: head ch, dim d =================
+        const int ch = wave >> 1, half = wave & 1;
+        uint16_t * vme = sm.vc[wave];
+        // this wave's half of V rows [8 i, 8 i + 8): one 1-KiB LDS-DMA instruction
+        auto stage_v = [&](int i) {
+            const int jv = min(8 * i + (lane >> 3), n_kv - 1);
+            lds_dma16(vbase + (int64_t) jv * a.nbv1 + 128 * half + 16 * (lane & 7), vme + 512 * i);
+        };
+        // rows [0, 64) go out with the mask, the rest once the mask bounds them
+        const int n0 = min(8, (n_kv + 7) / 8);
+        for (int i = 0; i < n0; ++i) stage_v(i);
+        __syncthreads();   // the flags' zeros
+        eng_vm_wait_fa(n0);   // the mask (issued first)
+        asm volatile("" : "+v"(mk4[0]), "+v"(mk4[1]), "+v"(mk4[2]), "+v"(mk4[3]));
+        const int nrun = nrun_of(), nb = (nrun + U - 1) / U;
+        const int nvi = max(n0, min((nrun + U + 7) / 8, (DS_VROWS + 7) / 8));   // rows through the last batch read
+        for (int i = n0; i < nvi; ++i) stage_v(i);
+        mark(4);
+        const int d = half * 64 + lane;
+        uint32_t yb = 0;
+        float S = 0.0f;
+        const uint16_t * vrow = vme + lane;
+        const float * scp = sm.sc[ch];
+        const float * cmp = sm.cm[ch];
+        const float * mkp = sm.mk[ch];
+        auto ld4 = [&](const float * p, float (&o)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; u += 4) {
+                const float4 t = *(const float4 *) (p + u);
+                o[u] = t.x; o[u + 1] = t.y; o[u + 2] = t.z; o[u + 3] = t.w;
+            }
+        };
+        auto ldb = [&](int j, uint32_t (&vv)[U], float (&vs)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) vv[u] = vrow[(j + u) * 64];
+            ld4(scp + j, vs);
+        };
+        auto run = [&](const uint32_t (&vv)[U], const float (&vs)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                yb = f16_mad(vv[u], vs[u], yb);
+                S = __fadd_rn(S, vs[u]);   // not contracted on the CPU
+            }
+        };
+        // a dead position keeps the state (-0 must survive); an update (ms != 1) first rescales,
+        // y = f16(y*ms), S = S*ms (ops.cpp:7171-7190)
+        auto general = [&](int j) {
+            uint32_t vv[U];
+            float vs[U], ms[U], mv[U];
+            ldb(j, vv, vs);
+            ld4(cmp + j, ms);
+            ld4(mkp + j, mv);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool live = __float_as_uint(mv[u]) != 0xff800000u;
+                const bool upd = __float_as_uint(ms[u]) != 0x3f800000u;
+                float t = __fmul_rn(h2f((uint16_t) yb), ms[u]);
+                asm("" : "+v"(t));   // two roundings, as f16r
+                const uint32_t ys = upd ? (uint32_t) f2h(t) : yb;
+                const float Ss = upd ? __fmul_rn(S, ms[u]) : S;
+                const uint32_t yn = f16_mad(vv[u], vs[u], ys);
+                const float Sn = __fadd_rn(Ss, vs[u]);
+                yb = live ? yn : yb;
+                S = live ? Sn : S;
+            }
+        };
+        // V: rows [0, 64) before the first block, the rest (issued once the mask bounded them)
+        // before block 4; a block's ready flag and batch flags are read one block ahead, so their
+        // LDS latency hides under the previous block's steps
+        int rdy = 0, f0 = 0, f1 = 0;
+        if (nb > 0) {
+            eng_vm_wait_fa(nvi - n0);
+            ds_wait_flag(&sm.ready[0]);
+            mark(5);
+            f0 = sm.bfl[ch][0];
+            f1 = sm.bfl[ch][1];
+        }
+        for (int b = 0; 2 * b < nb; ++b) {
+            if (b == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int g0 = f0, g1 = f1;
+            const bool two = 2 * b + 1 < nb, more = 2 * b + 2 < nb;
+            if (more) {
+                rdy = lds_ld(&sm.ready[b + 1]);
+                asm volatile("" ::: "memory");
+                f0 = sm.bfl[ch][2 * b + 2];
+                f1 = sm.bfl[ch][2 * b + 3];
+            }
+            if (!g0 && !(two && g1)) {   // both batches fast (or one fast batch)
+                uint32_t va[U], vb[U];
+                float sa[U], sb[U];
+                ldb(B * b, va, sa);
+                if (two) ldb(B * b + U, vb, sb);
+                run(va, sa);
+                if (two) run(vb, sb);
+            } else {
+                if (g0) general(B * b);
+                else { uint32_t va[U]; float sa[U]; ldb(B * b, va, sa); run(va, sa); }
+                if (two) {
+                    if (g1) general(B * b + U);
+                    else { uint32_t vb[U]; float sb[U]; ldb(B * b + U, vb, sb); run(vb, sb); }
+                }
+            }
+            if (more && !rdy) {   // the producer was behind: wait, then re-read its flags
+                ds_wait_flag(&sm.ready[b + 1]);
+                f0 = sm.bfl[ch][2 * b + 2];
+                f1 = sm.bfl[ch][2 * b + 3];
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA of this wave outlives it
+        mark(6);
+        const int64_t h = 2 * hp + ch;
+        const float o = __fmul_rn(h2f((uint16_t) yb), 1.0f / S);
+        float * drow = (float *) ((char *) a.dst + h * a.nb1_dst + iq3 * a.nb2_dst);
+        drow[d] = o;
+        sm.ol[ch * D + d] = o;
+    }
+    // ---- the two heads' 256 outputs: quantized here for the following projection ----
+    if (a.qmode) {
+        __syncthreads();
+        if (wave == 0) {
+            float q[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = sm.ol[4 * lane + k];
+            const int64_t c0 = 256 * hp;
+            if (a.qmode == 1) q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
+            else q8_0_wave(q, lane, true, a.qs + c0, a.qd + c0 / 32, a.qsum + c0 / 32);
+            mark(7);
+        }
+    }
+    if (prof) {
+        for (int i = 0; i < 8; ++i) if (pt[i]) a.prof[i] += pt[i];
+    }
+    kt_exit(a.kt, 9);
+}
+
+// the short-context kernel applies: one query row, D = 128, f16 K and V, at most DS_MAXKV
+// positions, an even GQA group (both heads of a workgroup read one KV head), 16-B aligned V rows
+bool fattn_dsh_ok(const fa_args & a, int64_t nq3) {
+    static const bool on = !getenv("GGML_MI355X_FA_DSH") || atoi(getenv("GGML_MI355X_FA_DSH")) != 0;
+    const int64_t G = a.Hkv > 0 ? a.H / a.Hkv : 0;
+    return on && a.n_q == 1 && a.D == 128 && a.k_type == GGML_TYPE_F16 && a.v_type == GGML_TYPE_F16 && a.H % 2 == 0 &&
+           a.H % a.Hkv == 0 && G % 2 == 0 && a.n_kv >= 1 && a.n_kv <= DS_MAXKV && (a.qmode == 0 || nq3 == 1) &&
+           ((uintptr_t) a.v % 16) == 0 && a.nbv1 % 16 == 0 && a.nbv2 % 16 == 0 && a.nbv3 % 16 == 0 && a.nbk1 % 8 == 0 &&
+           ((uintptr_t) a.k % 8) == 0 && ((uintptr_t) a.q % 16) == 0 && a.nbq2 % 16 == 0 && a.nbq3 % 16 == 0;
+}
+
+void launch_fattn_dsh(hipStream_t st, const fa_args & a, int64_t nq3) {
+    hipLaunchKernelGGL(k_fattn_dsh, dim3((unsigned) (a.H / 2), (unsigned) nq3), dim3(512), 0, st, a);
 }
 
 bool fattn_pf_quant_ok(const fa_args & a) {
@@ -1433,7 +1801,7 @@ __global__ __launch_bounds__(256) void k_fal_scores(const fa_args a, float * __r
     constexpr int D = 128, NM = D / 16, NB = D / 32, NP = FAL_PB / 64;
     constexpr int KB = KT == 2 ? 18 : 34;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qd = tid & 3;
-    kt_enter(a.kt);
+    kt_enter(a.kt, 5);
     const int64_t j0 = (int64_t) blockIdx.x * FAL_PB;
     const int64_t hk = blockIdx.y % a.Hkv, iq3 = blockIdx.y / a.Hkv;
     const int G = (int) (a.H / a.Hkv);
@@ -1538,7 +1906,7 @@ __global__ __launch_bounds__(256) void k_fal_scores(const fa_args a, float * __r
             }
         }
     }
-    kt_exit(a.kt);
+    kt_exit(a.kt, 5);
 }
 
 // LDS of the chain kernel
@@ -1577,7 +1945,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
     using SM = fal_smem<VT, NM>;
     constexpr int D = 128, NB = D / 32, CV = SM::CV, U = FAL_U;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    kt_enter(a.kt);
+    kt_enter(a.kt, 1 + FAL_THREADS / 64);
     // FAL_DSPLIT workgroups per head, each the recurrence of DH of its dims: V is staged through
     // the CU's LDS-DMA at ~25 GB/s per CU (MI355X_MICROARCH.md ldsdma-fill), so one CU per head
     // spent most of the chain waiting for its V stages; the split halves every CU's bytes while
@@ -1998,7 +2366,7 @@ __global__ __launch_bounds__(FAL_THREADS, 1) void k_fal_chain(const fa_args a, c
             q8K_wave(q, lane, a.qs + c0, a.qsum + c0 / 16, a.qd + c0 / 256);
         }
     }
-    if (wave == 0) kt_exit(a.kt);
+    if (wave == 0) kt_exit(a.kt, 1 + FAL_THREADS / 64);
 }
 
 // the long-context pair applies: one query row, D = 128, a cache longer than FA_LONG_MIN (and

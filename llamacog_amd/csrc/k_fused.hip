@@ -30,6 +30,8 @@ struct norm_fused_args {
     int64_t nrows;
     // MoE combine source instead of a: x = (e[., 0, row] * cw[row, 0] + e[., 1, row] * cw[row, 1]) + b
     const float * e; const float * cw; int nu;
+    unsigned long long * kt;            // in-graph kernel timeline region (nullable)
+    unsigned kt_stride;                 // its slots per workgroup (1 + threads / 64)
 };
 
 // one workgroup of BT threads per row; thread t owns the float4s at element 4 (t + BT k), k < NV,
@@ -37,6 +39,7 @@ struct norm_fused_args {
 // output.  The mean is the CPU's sequential one (quant_act.h rms_mean_decided).
 template <int NV>
 __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
+    kt_enter(p.kt, p.kt_stride);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int BT = blockDim.x, NW = BT >> 6;
     const int64_t row = blockIdx.x;
@@ -120,6 +123,7 @@ __global__ __launch_bounds__(1024) void k_norm_fused(const norm_fused_args p) {
             q8_0_wave(q, lane, true, p.qs0 + ro + c0, p.qd0 + row * (p.ne0 / 32) + c0 / 32, p.qsum0 + row * (p.ne0 / 32) + c0 / 32);
         }
     }
+    kt_exit(p.kt, p.kt_stride);
 }
 
 // dst = a*b (same shape, contiguous) and its quantization; one wave per 256 elements.
@@ -132,7 +136,9 @@ template <int QMODE, bool SILU>
 __global__ __launch_bounds__(64) void k_mul_quant(const float * __restrict__ a, const float * __restrict__ b,
                                                   float * __restrict__ dst, int64_t K,
                                                   int8_t * __restrict__ qs, float * __restrict__ qd,
-                                                  int16_t * __restrict__ qsum, float * __restrict__ sdst) {
+                                                  int16_t * __restrict__ qsum, float * __restrict__ sdst,
+                                                  unsigned long long * kt) {
+    kt_enter(kt, 2);
     const int lane = threadIdx.x;
     const int64_t row = blockIdx.y;
     const int64_t nblk = (K + 255) / 256;
@@ -163,6 +169,7 @@ __global__ __launch_bounds__(64) void k_mul_quant(const float * __restrict__ a, 
     } else if constexpr (QMODE == 2) {
         q8_0_wave(q, lane, valid, qs + row * K + c0, qd + row * (K / 32) + c0 / 32, qsum + row * (K / 32) + c0 / 32);
     }
+    kt_exit(kt, 2);
 }
 
 // ---- host side -------------------------------------------------------------------------------
@@ -253,6 +260,8 @@ bool fused_norm(exec_ctx & ctx, const ggml_tensor * add, ggml_tensor * norm, ggm
     const dim3 block((unsigned) (ne0 / (4 * nv)));
     p.nrows = nrows;
     const dim3 grid((unsigned) nrows);
+    p.kt = nrows == 1 ? ctx.kt_take("norm_fused", 1, block.x) : nullptr;
+    p.kt_stride = 1 + block.x / 64;
     switch (nv) {
         case 1: hipLaunchKernelGGL(k_norm_fused<1>, grid, block, 0, ctx.stream, p); break;
         case 2: hipLaunchKernelGGL(k_norm_fused<2>, grid, block, 0, ctx.stream, p); break;
@@ -290,7 +299,8 @@ bool fused_silu_mul_quant(exec_ctx & ctx, ggml_tensor * silu, ggml_tensor * mul,
     const float * b = (const float *) mul->src[1]->data;
     float * d = store_mul ? (float *) mul->data : nullptr;
     float * sd = silu && store_silu ? (float *) silu->data : nullptr;
-#define MQ_LAUNCH(Q, S) hipLaunchKernelGGL((k_mul_quant<Q, S>), grid, dim3(64), 0, ctx.stream, a, b, d, K, act.qs, act.d, act.s, sd)
+    unsigned long long * kt = nrows == 1 ? ctx.kt_take("mul_quant", grid.x, 64) : nullptr;
+#define MQ_LAUNCH(Q, S) hipLaunchKernelGGL((k_mul_quant<Q, S>), grid, dim3(64), 0, ctx.stream, a, b, d, K, act.qs, act.d, act.s, sd, kt)
     if (silu) {
         if (qmode == 1) MQ_LAUNCH(1, true); else if (qmode == 2) MQ_LAUNCH(2, true); else MQ_LAUNCH(0, true);
     } else {

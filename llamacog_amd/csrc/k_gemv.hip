@@ -29,6 +29,7 @@
 
 namespace mi355x {
 
+typedef __attribute__((address_space(3))) void * gemv_lds_t;
 constexpr int GEMV_MAXMAT = 3;
 constexpr int GEMV_ROPE_MAXPAIRS = 256;   // fused rope: n_dims <= 512
 constexpr int GEMV_MAXG = 16;             // row groups per workgroup when epilogues park row sums
@@ -74,6 +75,19 @@ struct gemv_args {
     int64_t xqs_st, xd_st, xs_st;
 };
 
+// MI_KT_PHASE=1 (a profiling build, EXTRA=-DMI_KT_PHASE=1): thread 0 of every one-shot workgroup
+// stamps the chip's realtime counter at its phase boundaries into the timeline slots after the
+// waves' exit stamps (GGML_MI355X_KTRACE_RAW=<label> prints workgroup 0's; scripts/ktrace.py)
+#ifndef MI_KT_PHASE
+#define MI_KT_PHASE 0
+#endif
+constexpr int KT_NPH = 8;   // phase slots per workgroup in a MI_KT_PHASE build
+constexpr unsigned KT_STRIDE = 1 + 4 + (MI_KT_PHASE ? KT_NPH : 0);   // the one-shot kernels' slots per workgroup
+__device__ __forceinline__ void kt_phase(unsigned long long * kt, int k) {
+    if (MI_KT_PHASE && kt && threadIdx.x == 0) kt[KT_STRIDE * blockIdx.x + 5 + k] = __builtin_amdgcn_s_memrealtime();
+}
+static inline unsigned kt_threads() { return 256 + (MI_KT_PHASE ? 64 * KT_NPH : 0); }
+
 // ---- norm prologue ---------------------------------------------------------------------------------
 // A decode mat-vec whose input is RMS_NORM(x) [* w] (build_norm, src/llama-graph.cpp:464-497; x the
 // residual sum its producer stored, or an input of the graph) forms that activation itself: every
@@ -96,6 +110,62 @@ __device__ __forceinline__ bool pro_load(const gemv_args::pro_t & r, int ps, flo
     for (int k = 0; k < 4; ++k) {
         xv[k] = *(const float4 *) (r.x + e0 + 4 * k);
         wv[k] = r.w ? *(const float4 *) (r.w + e0 + 4 * k) : make_float4(1.f, 1.f, 1.f, 1.f);
+    }
+    return b < nb;
+}
+
+// Loads and LDS-DMAs the compiler does not see (inline asm), for the norm-prologue launches: the
+// compiler puts no vmcnt wait of its own behind them, so the prologue's sources are waited for
+// exactly (gemv_vm_wait: everything but this wave's n youngest weight DMAs) and the prologue
+// overlaps the weight stream.  With the builtins its wait for x was a vmcnt(0) behind every weight
+// DMA (their per-lane guards made its count conservative), and the rope table and KV-slot loads
+// issued after the prologue cost another round trip in front of the records.
+__device__ __forceinline__ float4 gemv_ald16(const void * p) {
+    float4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ uint2 gemv_ald8(const void * p) {
+    uint2 v;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+// 16 B per lane HBM -> LDS, non-temporal (read once per token), as __builtin_amdgcn_global_load_lds
+__device__ __forceinline__ void gemv_dma16(const void * src, const void * lds) {
+    const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) (gemv_lds_t) lds);
+    if (MI_WNT) asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(m), "v"(src) : "memory");
+    else asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(src) : "memory");
+}
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (<= 31)
+__device__ __forceinline__ void gemv_vm_wait(int n) {
+#define GW(k) case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(k) : "memory"); break;
+    switch (n) {
+        GW(0) GW(1) GW(2) GW(3) GW(4) GW(5) GW(6) GW(7) GW(8) GW(9) GW(10) GW(11) GW(12) GW(13) GW(14) GW(15)
+        GW(16) GW(17) GW(18) GW(19) GW(20) GW(21) GW(22) GW(23) GW(24) GW(25) GW(26) GW(27) GW(28) GW(29) GW(30) GW(31)
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef GW
+}
+
+// MI_PRO_ASM=0 builds the previous arrangement (builtin loads and DMAs, the epilogue's table loaded
+// after the prologue) for A/B runs
+#ifndef MI_PRO_ASM
+#define MI_PRO_ASM 1
+#endif
+
+// pro_load through gemv_ald16 (the caller waits)
+__device__ __forceinline__ bool pro_load_asm(const gemv_args::pro_t & r, int ps, float4 (&xv)[4], float4 (&wv)[4]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nb = (int) (r.n / 256);
+    const int b = 16 * ps + 4 * wave + (lane >> 4);
+    const int64_t e0 = 256 * (int64_t) min(b, nb - 1) + 16 * (lane & 15);
+    // (no branch on r.w: the weight-less norm loads x twice and the caller selects 1.0 after its
+    // wait, so no kernel-argument round trip sits between the loads)
+    const float * wsrc = r.w ? r.w : r.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        xv[k] = gemv_ald16(r.x + e0 + 4 * k);
+        wv[k] = gemv_ald16(wsrc + e0 + 4 * k);
     }
     return b < nb;
 }
@@ -157,14 +227,20 @@ __device__ __forceinline__ int pro_npass(const gemv_args::pro_t & r) { return (i
 // the whole activation into buf from pass 0's slice of x and w already in registers (loaded
 // before the weight DMA, so waiting for it leaves the DMA in flight; v0: the slice exists); the
 // later passes of n > 4096 are loaded here.  The mean needs every pass's squares first
-__device__ void pro_form_regs(const gemv_args::pro_t & r, uint8_t * buf, bool v0, const float4 (&xv)[4], const float4 (&wv)[4]) {
+__device__ void pro_form_regs(const gemv_args::pro_t & r, uint8_t * buf, bool v0, const float4 (&xv)[4], const float4 (&wv)[4],
+                              unsigned long long * kt = nullptr) {
     const int np = pro_npass(r);
     double s = v0 ? pro_sq(xv) : 0.0;
     for (int ps = 1; ps < np; ++ps) {
         float4 xo[4], wo[4];
         if (pro_load(r, ps, xo, wo)) s = __dadd_rn(s, pro_sq(xo));
     }
+    if (MI_KT_PHASE) {   // the squares are formed: x has arrived
+        asm volatile("" ::"v"(s));
+        kt_phase(kt, 1);
+    }
     const float scale = pro_scale(r, s);
+    kt_phase(kt, 2);
     pro_pass(r, scale, 0, xv, wv, buf);
     for (int ps = 1; ps < np; ++ps) {
         float4 xo[4], wo[4];
@@ -354,9 +430,9 @@ __device__ __forceinline__ void gemv_pipe_body(const gemv_args & p, const int64_
 template <class T, int R, int WPR, int MODE>
 __global__ __launch_bounds__(256) void k_gemv_pipe(const gemv_args p, const int64_t ngroups) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
-    kt_enter(p.kt);
+    kt_enter(p.kt, 5);
     gemv_pipe_body<T, R, WPR, MODE>(p, ngroups, blockIdx.x, gridDim.x, xr);
-    kt_exit(p.kt);
+    kt_exit(p.kt, 5);
 }
 
 // Q/K of one K-quant and V of another (Llama-3 Q4_K_M: Q4_K and Q6_K on 16 of 32 layers) in
@@ -366,10 +442,10 @@ template <class T1, class T2, int R2, int WPR>
 __global__ __launch_bounds__(256) void k_gemv_pipe2(const gemv_args p1, const int64_t ng1, const int64_t nwg1,
                                                     const gemv_args p2, const int64_t ng2) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
-    kt_enter(p1.kt);
+    kt_enter(p1.kt, 5);
     if ((int64_t) blockIdx.x < nwg1) gemv_pipe_body<T1, 2, WPR, 1>(p1, ng1, blockIdx.x, nwg1, xr);
     else gemv_pipe_body<T2, R2, WPR, 1>(p2, ng2, (int64_t) blockIdx.x - nwg1, (int64_t) gridDim.x - nwg1, xr);
-    kt_exit(p1.kt);
+    kt_exit(p1.kt, 5);
 }
 
 // ---- one-shot body: one row group per workgroup, weights staged by LDS-DMA ----------------------
@@ -385,7 +461,6 @@ template <class T> struct os_geo {
     static constexpr int NI = (SEG + 1023) / 1024;                        // DMA instructions per slice
     static constexpr int SLICE = NI * 1024;                               // LDS bytes per slice
 };
-typedef __attribute__((address_space(3))) void * gemv_lds_t;
 
 template <class T, int R, int WPR, int MODE, bool PRO, bool ID = false>
 __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t g, uint8_t * wl, uint32_t * xr) {
@@ -408,7 +483,29 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     // ---- activation sources first: pass 0 of x and w for the norm prologue ----
     float4 pxv[4], pwv[4];
     bool pv0 = false;
-    if constexpr (PRO) pv0 = pro_load(p.pro, 0, pxv, pwv);
+    constexpr bool PA = PRO && MI_PRO_ASM;
+    if constexpr (PA) pv0 = pro_load_asm(p.pro, 0, pxv, pwv);
+    else if constexpr (PRO) pv0 = pro_load(p.pro, 0, pxv, pwv);
+    // the epilogue's rope table and KV-slot pointers, loaded with the prologue's sources (PRO)
+    uint2 rtv = make_uint2(0, 0), fpv = make_uint2(0, 0);
+    const bool has_rt = PA && MODE && ((p.need_pairs != 0) & ((int) threadIdx.x < p.rp.n_dims / 2));
+    uint16_t * const * fslot = nullptr;
+    if constexpr (PA && MODE != 0) {
+        // (selected from the six uniform kernel arguments: a per-lane index into them is a vector
+        // load of the kernarg segment and a wait in front of the DMAs)
+        const int ti = threadIdx.x;
+        uint16_t * const * sl = nullptr;
+#pragma unroll
+        for (int k = 0; k < GEMV_MAXMAT; ++k) {
+            sl = ti == 2 * k ? p.f16out[k] : sl;
+            sl = ti == 2 * k + 1 ? p.rope_f16[k] : sl;
+        }
+        fslot = sl;
+        // unconditional loads (a harmless address where there is nothing to load), no branches on
+        // kernel arguments between them
+        rtv = gemv_ald8(has_rt ? (const void *) (p.rtab_g + threadIdx.x) : (const void *) p.pro.x);
+        fpv = gemv_ald8(fslot ? (const void *) fslot : (const void *) p.pro.x);
+    }
     const int wr = lane / T::LPR, ws = lane % T::LPR;
     const int wrc = wr < R ? wr : 0;
     // one walking wave (W1): after every wave's records, wave 0 walks all RPG rows of the group
@@ -436,20 +533,40 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
             for (int i = 0; i < G::NI; ++i) {
                 const int off = min(i * 1024 + 16 * lane, seg - 16);
                 // lanes past the slice write nothing (a compact stride leaves no padding after it)
-                if (i * 1024 + 16 * lane < seg)
-                    __builtin_amdgcn_global_load_lds((const void *) (src + off), (gemv_lds_t) (mine + r * p.sls + i * 1024), 16, 0,
-                                                     MI_WNT ? 2 : 0);
+                if (i * 1024 + 16 * lane < seg) {
+                    if constexpr (PA) gemv_dma16(src + off, mine + r * p.sls + i * 1024);
+                    else __builtin_amdgcn_global_load_lds((const void *) (src + off), (gemv_lds_t) (mine + r * p.sls + i * 1024), 16, 0,
+                                                          MI_WNT ? 2 : 0);
+                }
+            }
+        }
+        if constexpr (PA) {
+            // the prologue's sources and the epilogue's table are in; this wave's R * ceil(seg / 1 KiB)
+            // weight DMAs (lane 0 of every one of them is inside the slice) stay in flight
+            gemv_vm_wait(R * ((seg + 1023) / 1024));
+            // (the values are used only after the wait)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                asm volatile("" : "+v"(pxv[k].x), "+v"(pxv[k].y), "+v"(pxv[k].z), "+v"(pxv[k].w));
+                asm volatile("" : "+v"(pwv[k].x), "+v"(pwv[k].y), "+v"(pwv[k].z), "+v"(pwv[k].w));
+            }
+            asm volatile("" : "+v"(rtv.x), "+v"(rtv.y), "+v"(fpv.x), "+v"(fpv.y));
+            if (!p.pro.w) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) pwv[k] = make_float4(1.f, 1.f, 1.f, 1.f);
             }
         }
     }
+    kt_phase(p.kt, 0);
     // the activation slice after the DMAs: T::load computes on what it loads (bsum pairs, the
     // Q6_K -32 sums), and a wait for a load issued BEFORE the DMAs would hold the DMA issue back
     // by an L2 round trip (the one-shot kernel's rec stage took ~35 % longer that way)
     typename T::act x;
     if constexpr (PRO) {
         uint8_t * buf = (uint8_t *) xr + p.pro.lds_off;
-        pro_form_regs(p.pro, buf, pv0, pxv, pwv);
+        pro_form_regs(p.pro, buf, pv0, pxv, pwv, p.kt);
         __syncthreads();
+        kt_phase(p.kt, 3);
         T::load(pro_act(p.pro, buf), tt, x);
     } else if constexpr (ID) {   // this slot's column
         const gemv_act A = {p.A.qs + xsl * p.xqs_st, p.A.d + xsl * p.xd_st, p.A.s + xsl * p.xs_st};
@@ -459,7 +576,10 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     }
     __shared__ float2 rtab[MODE ? GEMV_ROPE_MAXPAIRS : 1];
     __shared__ uint16_t * f16p[2 * GEMV_MAXMAT];
-    if (MODE) {
+    if constexpr (PA && MODE != 0) {   // loaded before the weight DMAs
+        if (threadIdx.x < 2 * GEMV_MAXMAT) f16p[threadIdx.x] = fslot ? (uint16_t *) (((uint64_t) fpv.y << 32) | fpv.x) : nullptr;
+        if (has_rt) rtab[threadIdx.x] = make_float2(__uint_as_float(rtv.x), __uint_as_float(rtv.y));
+    } else if (MODE) {
         if (threadIdx.x < 2 * GEMV_MAXMAT) {
             const int m2 = threadIdx.x >> 1;
             uint16_t * const * slot = (threadIdx.x & 1) ? p.rope_f16[m2] : p.f16out[m2];
@@ -471,6 +591,7 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     }
     // ---- this wave's weights are in LDS (the issuing wave's vmcnt covers its own DMAs) ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    kt_phase(p.kt, 4);
     uint32_t * xb = xr + p.rec_off / 4;
     const int rst = (int) p.rec_st;
     if (WPR > 1 && R > 1 && p.rec_bar) {
@@ -501,6 +622,7 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
         }
         return;
     }
+    kt_phase(p.kt, 5);
     if constexpr (WPR > 1 || MODE != 0) __syncthreads();
     else wave_lds_sync();
     __shared__ float res[MODE ? RPG : 1];
@@ -530,6 +652,7 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
     }
     if constexpr (MODE >= 1) {
         __syncthreads();
+        kt_phase(p.kt, 6);
         for (int i = threadIdx.x; i < RPG; i += NT) {
             const int64_t row = (g - p.blk0[mi]) * RPG + i;
             // rope partner row ^ 1 lies in the same group (RPG is even whenever rope is fused)
@@ -543,19 +666,19 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
 template <class T, int R, int WPR, int MODE, bool PRO, bool ID>
 __global__ __launch_bounds__(256) void k_gemv_os(const gemv_args p) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
-    kt_enter(p.kt);
+    kt_enter(p.kt, KT_STRIDE);
     gemv_os_body<T, R, WPR, MODE, PRO, ID>(p, blockIdx.x, (uint8_t *) xr + p.wl_off, xr);
-    kt_exit(p.kt);
+    kt_exit(p.kt, KT_STRIDE);
 }
 
 template <class T1, class T2, int R2, int WPR, bool PRO, int R1 = 2, int WPR2 = WPR>
 __global__ __launch_bounds__(256) void k_gemv_os2(const gemv_args p1, const int64_t ng1, const gemv_args p2) {
     extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
-    kt_enter(p1.kt);
+    kt_enter(p1.kt, KT_STRIDE);
     const int64_t b = blockIdx.x;
     if (b < ng1) gemv_os_body<T1, R1, WPR, 1, PRO>(p1, b, (uint8_t *) xr + p1.wl_off, xr);
     else gemv_os_body<T2, R2, WPR2, 1, PRO>(p2, b - ng1, (uint8_t *) xr + p2.wl_off, xr);
-    kt_exit(p1.kt);
+    kt_exit(p1.kt, KT_STRIDE);
 }
 
 
@@ -715,7 +838,7 @@ static void launch_os_m(hipStream_t st, gemv_args & a, int nmat) {
     const int64_t ng = set_groups(a, nmat, RPG);
     const size_t lds = os_lds_layout<T, R, WPR>(a);
     const int64_t grid = ng;
-    a.kt = g_kt_ctx ? g_kt_ctx->kt_take(gemv_kt_name(a, MODE), (unsigned) grid, 256) : nullptr;
+    a.kt = g_kt_ctx ? g_kt_ctx->kt_take(gemv_kt_name(a, MODE), (unsigned) grid, kt_threads()) : nullptr;
 #define OS_LAUNCH(P)                                                                                              \
     if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P, false>), dim3((unsigned) grid), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a); \
     else hipLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P, false>), dim3((unsigned) grid), dim3(256), lds, st, a)
@@ -779,7 +902,7 @@ static void launch_os_id_v(hipStream_t st, gemv_args & a, int nmat) {
     constexpr int RPG = (4 / WPR) * R;
     const int64_t ng = set_groups(a, nmat, RPG);
     const size_t lds = os_lds_layout<T, R, WPR>(a);
-    a.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv_id", (unsigned) ng, 256) : nullptr;
+    a.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv_id", (unsigned) ng, kt_threads()) : nullptr;
     if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os<T, R, WPR, 0, false, true>), dim3((unsigned) ng), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a);
     else hipLaunchKernelGGL((k_gemv_os<T, R, WPR, 0, false, true>), dim3((unsigned) ng), dim3(256), lds, st, a);
 }
@@ -830,7 +953,7 @@ static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2,
     os_plain_geo<T2, R2, WPR>(a2);
     const size_t lds = off + std::max((size_t) 4 * R1 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
     const unsigned grid = (unsigned) (ng1 + ng2);
-    a1.kt = g_kt_ctx ? g_kt_ctx->kt_take(a1.pro.kind ? "gemv2+pro+epi" : "gemv2+epi", grid, 64 * NWV) : nullptr;
+    a1.kt = g_kt_ctx ? g_kt_ctx->kt_take(a1.pro.kind ? "gemv2+pro+epi" : "gemv2+epi", grid, kt_threads()) : nullptr;
 #define OS2_LAUNCH(P)                                                                                                 \
     if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P, R1>), dim3(grid), dim3(64 * NWV), lds, st, t_ev_beg, \
                                         t_ev_end, 0, a1, ng1, a2);                                                        \
@@ -852,7 +975,7 @@ static void launch_os2m_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2
     os_plain_geo<T2, R2, WPR2>(a2);
     const size_t lds = off + std::max((size_t) 4 * R1 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
     const unsigned grid = (unsigned) (ng1 + ng2);
-    a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv2+epi", grid, 64 * NWV) : nullptr;
+    a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv2+epi", grid, kt_threads()) : nullptr;
     if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR1, false, R1, WPR2>), dim3(grid), dim3(64 * NWV), lds, st,
                                         t_ev_beg, t_ev_end, 0, a1, ng1, a2);
     else hipLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR1, false, R1, WPR2>), dim3(grid), dim3(64 * NWV), lds, st, a1, ng1, a2);
