@@ -227,7 +227,7 @@ static enum ggml_status mi_buf_init_tensor(ggml_backend_buffer_t buffer, ggml_te
 
 // GGML_MI355X_HOSTPROF=1: host time inside the plugin's entry points, summed per kind and printed
 // every 64 graph computes (diagnostic; what libllama spends outside them is the rest of a step)
-enum { HP_SUPPORTS, HP_SET_ASYNC, HP_GET_ASYNC, HP_SET, HP_GET, HP_COMPUTE, HP_SYNC, HP_N };
+enum { HP_SUPPORTS, HP_SET_ASYNC, HP_GET_ASYNC, HP_SET, HP_GET, HP_COMPUTE, HP_SYNC, HP_C_FENCE, HP_C_DYN, HP_C_SIG, HP_C_LAUNCH, HP_N };
 static const bool g_hostprof = getenv("GGML_MI355X_HOSTPROF") && atoi(getenv("GGML_MI355X_HOSTPROF")) != 0;
 static std::atomic<long long> g_hp_ns[HP_N];
 static std::atomic<long long> g_hp_cnt[HP_N];
@@ -241,7 +241,8 @@ struct hp_scope {
     }
 };
 static void hp_report() {
-    static const char * nm[HP_N] = {"supports_op", "set_async", "get_async", "buf_set", "buf_get", "graph_compute", "synchronize"};
+    static const char * nm[HP_N] = {"supports_op", "set_async", "get_async", "buf_set", "buf_get", "graph_compute", "synchronize",
+                                    "gc:fence", "gc:dyn", "gc:signature", "gc:launch"};
     fprintf(stderr, "[hostprof]");
     for (int k = 0; k < HP_N; ++k) {
         // swap-and-read: scopes still closing on other threads land in the next report
@@ -1267,7 +1268,10 @@ static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
         }
     }
     static thread_local std::vector<int64_t> sig;
-    graph_signature(cgraph, sig);
+    {
+        hp_scope hps(HP_C_SIG);
+        graph_signature(cgraph, sig);
+    }
     graph_entry * e = nullptr;
     for (auto & g : ctx->graphs) {
         if (g.sig == sig) { e = &g; break; }
@@ -1288,6 +1292,7 @@ static bool graph_compute_hipgraph(mi_backend_ctx * ctx, ggml_cgraph * cgraph) {
     }
     e->last_use = ++ctx->use_clock;
     if (e->exec) {
+        hp_scope hpl(HP_C_LAUNCH);
         MI_CHECK(hipGraphLaunch(e->exec, ctx->ex.stream));
         ctx->ex.kt_list = e->kt_list;
         ctx->ex.kt_off = e->kt_off;
@@ -1328,7 +1333,10 @@ static enum ggml_status mi_backend_graph_compute(ggml_backend_t backend, ggml_cg
     hp_scope hp_(HP_COMPUTE);
     auto * ctx = (mi_backend_ctx *) backend->context;
     MI_CHECK(hipSetDevice(ctx->device));
-    up_fence(ctx->device, ctx->ex.stream, ctx->up_seen);   // the graph's inputs (set_tensor) are in
+    {
+        hp_scope hpf(HP_C_FENCE);
+        up_fence(ctx->device, ctx->ex.stream, ctx->up_seen);   // the graph's inputs (set_tensor) are in
+    }
     ctx->ex.timing = g_timing.load(std::memory_order_relaxed) != 0;
     // whole-graph timing (kind TK_GRAPH: device time between events around the graph;
     // TK_GRAPH_HOST: host time spent in this call) — works with hipGraph replay
@@ -1339,7 +1347,11 @@ static enum ggml_status mi_backend_graph_compute(ggml_backend_t backend, ggml_cg
         gbeg = ctx->ex.get_event();
         MI_CHECK(hipEventRecord(gbeg, ctx->ex.stream));
     }
-    const bool dyn_ok = ctx->ex.prepare_dyn(cgraph);
+    bool dyn_ok;
+    {
+        hp_scope hpd(HP_C_DYN);
+        dyn_ok = ctx->ex.prepare_dyn(cgraph);
+    }
     const bool ktrace = ktrace_enabled();
     if (ktrace) {
         if (!ctx->ex.kt_buf) {

@@ -38,12 +38,12 @@ bool fattn_supported(const ggml_tensor * op) {
 
 bool mmv_q_supported_type(ggml_type t);
 
-void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
+void fa_args_of(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm, fa_args & a, q8_act & act, int64_t & nq3) {
     const ggml_tensor * q = dst->src[0];
     const ggml_tensor * k = dst->src[1];
     const ggml_tensor * v = dst->src[2];
     const ggml_tensor * mask = dst->src[3];
-    fa_args a;
+    a = {};
     a.q = (const char *) q->data; a.nbq1 = q->nb[1]; a.nbq2 = q->nb[2]; a.nbq3 = q->nb[3];
     a.k = (const char *) k->data; a.nbk1 = k->nb[1]; a.nbk2 = k->nb[2]; a.nbk3 = k->nb[3];
     a.v = (const char *) v->data; a.nbv1 = v->nb[1]; a.nbv2 = v->nb[2]; a.nbv3 = v->nb[3];
@@ -63,7 +63,7 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     a.dst = (float *) dst->data;
     a.nb1_dst = dst->nb[1];
     a.nb2_dst = dst->nb[3];  // batch stride (dst ne = [D, H, n_q, ne3])
-    const int64_t nq3 = q->ne[3];
+    nq3 = q->ne[3];
 
     a.chunk = a.n_kv;
     a.nchunks = 1;
@@ -73,12 +73,7 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     a.kt = nullptr;
     a.qs = nullptr; a.qd = nullptr; a.qsum = nullptr;
     a.cnt = nullptr;
-
-    hipEvent_t ev = nullptr;
-    const double bytes = (double) (ggml_nbytes(k) + ggml_nbytes(v)) + (double) ggml_nbytes(q) + (double) ggml_nbytes(dst);
-    if (ctx.timing) ctx.time_begin(TK_FATTN, bytes, ev);
     // fused quantization of the output for the next MUL_MAT (decode: one row)
-    q8_act act;
     if (mm && a.n_q == 1 && nq3 == 1 && mmv_q_supported_type(mm->src[0]->type) &&
         mm->src[1]->ne[0] == a.H * a.D && ggml_nrows(mm->src[1]) == 1 && ggml_is_contiguous(dst)) {
         const ggml_type wt = mm->src[0]->type;
@@ -103,15 +98,39 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
         a.qmode = 1;
         a.qs = act.qs; a.qd = act.d; a.qsum = act.s;
     }
-    // decode (one query row): two heads per workgroup with the scores produced under the
-    // recurrence (k_fattn_dec2) where it applies, else k_fattn_exact, one workgroup per head;
-    // batches: k_fattn_exact's prefill tiles
+}
+
+// the Q/K/V launch can carry this attention (fa_dsh4.h): the short-context kernel's conditions, one
+// batch, at most 64 head pairs (fewer than the CUs), GGML_MI355X_FA_CARRY=0 keeps it a launch of
+// its own
+bool fattn_carry_ok(const fa_args & a, int64_t nq3) {
+    static const bool on = !getenv("GGML_MI355X_FA_CARRY") || atoi(getenv("GGML_MI355X_FA_CARRY")) != 0;
+    return on && nq3 == 1 && a.H / 2 <= 64 && fattn_dsh_ok(a, nq3);
+}
+
+void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
+    fa_args a;
+    q8_act act;
+    int64_t nq3 = 1;
+    fa_args_of(ctx, dst, mm, a, act, nq3);
+    const ggml_tensor * q = dst->src[0];
+    const ggml_tensor * k = dst->src[1];
+    const ggml_tensor * v = dst->src[2];
+    hipEvent_t ev = nullptr;
+    const double bytes = (double) (ggml_nbytes(k) + ggml_nbytes(v)) + (double) ggml_nbytes(q) + (double) ggml_nbytes(dst);
+    if (ctx.timing) ctx.time_begin(TK_FATTN, bytes, ev);
+    // decode (one query row): the short-context kernel (k_fattn_dsh) or the two-heads-per-workgroup
+    // one (k_fattn_dec2) where they apply, the long-context pair past FA_LONG_MIN, else
+    // k_fattn_exact, one workgroup per head; batches: k_fattn_exact's prefill tiles
     if (fattn_long_ok(a, nq3)) {
         // long cache: scores by a wide grid, then the exact recurrence (k_fattn_exact.hip)
         float * sco = (float *) ctx.scratch(1, (size_t) a.H * a.n_kv * sizeof(float));
         unsigned long long * kts = ctx.kt_take("fa_scores", (unsigned) (ceil_div(a.n_kv, (int64_t) FAL_PB) * a.Hkv), 256);
         a.kt = ctx.kt_take("fa_chain", (unsigned) (a.H * FAL_DSPLIT), FAL_THREADS);
         launch_fattn_long(ctx.stream, a, sco, kts);
+    } else if (fattn_dsh_ok(a, nq3) && fattn_dsh4_standalone()) {
+        a.kt = ctx.kt_take("fa_dsh4", (unsigned) (a.H / 2 * nq3), 256);
+        launch_fattn_dsh4(ctx.stream, a, nq3);
     } else if (fattn_dsh_ok(a, nq3)) {
         a.kt = ctx.kt_take("fa_dsh", (unsigned) (a.H / 2 * nq3), 512);
         launch_fattn_dsh(ctx.stream, a, nq3);
