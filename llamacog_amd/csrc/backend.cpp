@@ -1220,6 +1220,19 @@ static void kt_collect(mi_backend_ctx * ctx) {
             for (unsigned k = 1; k < l.stride; ++k) fprintf(stderr, " %.2f", r[k] >= r[0] ? (r[k] - r[0]) * tick_ns / 1e3 : -1.0);
             fprintf(stderr, "\n");
         }
+        // GGML_MI355X_KTRACE_DIST=<name>: every workgroup's start and end of that launch, in us from its
+        // first start (workgroup order)
+        static const char * dist = getenv("GGML_MI355X_KTRACE_DIST");
+        if (dist && strcmp(dist, l.name) == 0) {
+            fprintf(stderr, "[ktdist] %s:", l.name);
+            for (unsigned w = 0; w < l.nwg; ++w) {
+                const unsigned long long * r = h.data() + l.off + (size_t) w * l.stride;
+                unsigned long long we = 0;
+                for (unsigned k = 1; k < l.stride; ++k) we = std::max(we, r[k]);
+                fprintf(stderr, " %.2f,%.2f", r[0] ? (r[0] - s0) * tick_ns / 1e3 : -1.0, we ? (we - s0) * tick_ns / 1e3 : -1.0);
+            }
+            fprintf(stderr, "\n");
+        }
         g_kt_samples.push_back({gs, (int) i, l.name, l.nwg, (s0 - base) * tick_ns, (sl - base) * tick_ns, (e1 - base) * tick_ns,
                                 w0e ? (w0e - base) * tick_ns : 0.0, nl ? life / nl * tick_ns : 0.0});
     }

@@ -612,7 +612,8 @@ static bool plan_fa_carry(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_te
     fa_args_of(ctx, fa, mmo, fal.a, act, nq3);
     if (dbg) fprintf(stderr, "[mi355x]   fa carry: out-proj %d carry_ok %d\n", mmo != nullptr, fattn_carry_ok(fal.a, nq3));
     if (!fattn_carry_ok(fal.a, nq3) || fal.a.H / 2 > exec_ctx::FA4_CNT) return false;
-    fal.fz = {ctx.fa4_cnt, (int) (4 * fal.a.D), (uint16_t * const *) epi.rope_f16[rk], (uint16_t * const *) epi.f16out[rv]};
+    static const int fa4_print = getenv("GGML_MI355X_FA4_PRINT") ? atoi(getenv("GGML_MI355X_FA4_PRINT")) : 0;
+    fal.fz = {ctx.fa4_cnt, (int) (4 * fal.a.D), (uint16_t * const *) epi.rope_f16[rk], (uint16_t * const *) epi.f16out[rv], fa4_print};
     fal.nfa = (int) (fal.a.H / 2);
     fal.role[rq] = 0; fal.role[rk] = 1; fal.role[rv] = 2;
     fal.done = false;

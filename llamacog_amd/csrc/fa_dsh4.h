@@ -28,7 +28,8 @@ constexpr int D4_MAXKV = 256, D4_U = 8, D4_B = 16, D4_NB = D4_MAXKV / D4_B, D4_P
 constexpr int D4_OWN = D4_NB / 2;          // blocks per producer
 constexpr int D4_SLOTS = 5;                // K blocks a producer holds in registers at once (the rest
                                            // reuse a slot once its block is scored)
-constexpr int D4_VROWS = D4_MAXKV + D4_U;  // V rows staged
+constexpr int D4_VROWS = D4_MAXKV;         // V rows staged (the chains read no row past the last batch;
+                                           // two workgroups of the two-type launch share a CU with it)
 
 struct ds4_smem {
     float sc[2][D4_MAXKV + D4_PAD];        // [head] vs (0 where dead)
@@ -52,6 +53,10 @@ template <bool FUSED>
 __device__ __forceinline__ void fa_dsh4_body(const fa_args & a, int64_t hp, int64_t iq3, const fa_fuse & fz, ds4_smem & sm) {
     constexpr int D = 128, NM = D / 16, U = D4_U, B = D4_B;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool pr = FUSED && fz.dbg && blockIdx.x == 0 && lane == 0;
+    const unsigned long long t0 = pr ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long tm[6] = {0, 0, 0, 0, 0, 0};
+    auto mark = [&](int i) { if (pr) tm[i] = __builtin_amdgcn_s_memtime() - t0; };
     const int64_t hk = (2 * hp) / (a.H / a.Hkv);
     const int n_kv = (int) a.n_kv;
     const char * kbase = a.k + hk * a.nbk2 + iq3 * a.nbk3;
@@ -111,18 +116,22 @@ __device__ __forceinline__ void fa_dsh4_body(const fa_args & a, int64_t hp, int6
             }
         }
         __syncthreads();   // the flags' zeros and the expf table (all waves)
+        mark(0);
         int jfk = -1, jfv = -1;   // the token's own K / V row (stored by this launch), if it is in the cache view
         if constexpr (FUSED) {
             // every projection row of this head pair is stored (write-through) and counted
             if (lane == 0) {
                 int guard = 0;
-                while (__hip_atomic_load(fz.cnt + hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fz.expect) {
+                // (a returning atomic reads the counter where the adds land; a load poll may be served
+                // from this XCD's L2 copy for microseconds)
+                while (__hip_atomic_fetch_add(fz.cnt + hp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fz.expect) {
                     __builtin_amdgcn_s_sleep(2);
                     if (++guard > (1 << 22)) break;   // a miscount shows as wrong output, never as a hang
                 }
             }
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
+            mark(1);
             const char * kd = fz.kslot ? (const char *) *fz.kslot : nullptr;
             const char * vd = fz.vslot ? (const char *) *fz.vslot : nullptr;
             if (kd) {
@@ -189,6 +198,7 @@ __device__ __forceinline__ void fa_dsh4_body(const fa_args & a, int64_t hp, int6
                 }
             }
         }
+        mark(2);
         float nz = -0.0f;
         asm volatile("" : "+v"(nz));
         float slope[2];
@@ -275,6 +285,9 @@ __device__ __forceinline__ void fa_dsh4_body(const fa_args & a, int64_t hp, int6
             for (int i = 1; i < D4_OWN; ++i)
                 if (i < nown) coef(i);
         }
+        mark(3);
+        if (pr && wave == 2) printf("[fa4] hp0 jfk %d jfv %d n_kv %d nrun %d nown %d | cycles: loads+sync %llu wait %llu q/K/V %llu coef %llu\n",
+                                    jfk, jfv, n_kv, nrun, nown, tm[0], tm[1], tm[2], tm[3]);
     } else {
         // ================= chains: head 2 hp + wave, dims 2 lane, 2 lane + 1 =================
         const int ch = wave;
@@ -371,6 +384,8 @@ __device__ __forceinline__ void fa_dsh4_body(const fa_args & a, int64_t hp, int6
                 f1 = sm.bfl[ch][2 * b + 3];
             }
         }
+        mark(4);
+        if (pr && wave == 0) printf("[fa4] hp0 chain end %llu\n", tm[4]);
         const int64_t h = 2 * hp + ch;
         const float rS = 1.0f / S;
         const float o0 = __fmul_rn(h2f((uint16_t) y0), rS), o1 = __fmul_rn(h2f((uint16_t) y1), rS);

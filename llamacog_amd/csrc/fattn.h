@@ -36,6 +36,7 @@ struct fa_args {
 struct fa_fuse {
     int * cnt; int expect;
     uint16_t * const * kslot; uint16_t * const * vslot;
+    int dbg;   // GGML_MI355X_FA4_PRINT=1: workgroup 0 prints its phase times (diagnostics)
 };
 
 // an attention the Q/K/V launch carries (gemv_group's fal): its arguments, the hand-off, its

@@ -101,10 +101,11 @@ void fa_args_of(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm, fa_ar
 }
 
 // the Q/K/V launch can carry this attention (fa_dsh4.h): the short-context kernel's conditions, one
-// batch, at most 64 head pairs (fewer than the CUs), GGML_MI355X_FA_CARRY=0 keeps it a launch of
-// its own
+// batch, at most 64 head pairs (fewer than the CUs).  Opt-in (GGML_MI355X_FA_CARRY=1): measured
+// slower so far (8B tg 2.44 vs 2.16 ms/token: the projection's K/V workgroups end 2-6 us later in
+// the carried launch and the attention waits for the last of them)
 bool fattn_carry_ok(const fa_args & a, int64_t nq3) {
-    static const bool on = !getenv("GGML_MI355X_FA_CARRY") || atoi(getenv("GGML_MI355X_FA_CARRY")) != 0;
+    static const bool on = getenv("GGML_MI355X_FA_CARRY") && atoi(getenv("GGML_MI355X_FA_CARRY")) != 0;
     return on && nq3 == 1 && a.H / 2 <= 64 && fattn_dsh_ok(a, nq3);
 }
 

@@ -750,12 +750,20 @@ static thread_local exec_ctx * g_kt_ctx = nullptr;
 // the attention to carry in this gemv_group's launch (gemv_group's fal), done once it is launched
 static thread_local gemv_fa * t_fa = nullptr;
 
-// dynamic LDS above 64 KiB needs the kernel's attribute raised once
+// the carried launch's workgroups (static + dynamic LDS) fit two to a CU, so its projection rows all
+// start at once (one to a CU, the two-type launch's second half started 8-11 us late); the
+// attribute raise for dynamic LDS above 64 KiB is advisory on ROCm (it may refuse the call)
 template <class K>
-static void fa_lds_attr(K kernel, size_t lds) {
+static bool fa_lds_fits(K kernel, size_t lds) {
     static std::once_flag once;
-    std::call_once(once, [&] { MI_CHECK(hipFuncSetAttribute((const void *) kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); });
-    GGML_ASSERT(lds <= 160 * 1024);
+    static size_t st = 160 * 1024;
+    std::call_once(once, [&] {
+        (void) hipFuncSetAttribute((const void *) kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
+        hipFuncAttributes fa;
+        if (hipFuncGetAttributes(&fa, (const void *) kernel) == hipSuccess) st = fa.sharedSizeBytes;
+        (void) hipGetLastError();
+    });
+    return 2 * (st + lds) <= 160 * 1024;
 }
 
 static int g_gemv_wgs = -1;    // the pipelined kernel's persistent grid (2048: 8 per CU)
@@ -908,11 +916,12 @@ static void launch_os_m(hipStream_t st, gemv_args & a, int nmat) {
     const int64_t grid = ng;
     if constexpr (MODE == 1 && WPR == 1) {
         // the attention rides in this launch (a workgroup's rows lie in one head: its counter add)
-        if (t_fa && !t_fa->done && a.pro.kind && t_fa->a.D % RPG == 0) {
-            const size_t lf = std::max(lds, sizeof(ds4_smem));
+        const size_t lf = std::max(lds, sizeof(ds4_smem));
+        if (t_fa && !t_fa->done && a.pro.kind && t_fa->a.D % RPG == 0 && fa_lds_fits(k_gemv_os_fa<T, R, WPR>, lf)) {
+            if (getenv("GGML_MI355X_DEBUG_FUSE")) fprintf(stderr, "[mi355x]   fused launch: lds %zu, body %zu, grid %lld + %d\n", lds, sizeof(ds4_smem), (long long) grid, t_fa->nfa);
             a.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv+pro+epi+fa", (unsigned) (grid + t_fa->nfa), kt_threads()) : nullptr;
-            fa_lds_attr(k_gemv_os_fa<T, R, WPR>, lf);
             hipLaunchKernelGGL((k_gemv_os_fa<T, R, WPR>), dim3((unsigned) (grid + t_fa->nfa)), dim3(256), lf, st, a, t_fa->a, t_fa->fz, t_fa->nfa);
+            MI_CHECK(hipPeekAtLastError());
             t_fa->done = true;
             return;
         }
@@ -1032,12 +1041,14 @@ static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2,
     os_plain_geo<T2, R2, WPR>(a2);
     const size_t lds = off + std::max((size_t) 4 * R1 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
     const unsigned grid = (unsigned) (ng1 + ng2);
-    if (t_fa && !t_fa->done && a1.pro.kind && t_fa->a.D % ((NWV / WPR) * R1) == 0 && t_fa->a.D % ((NWV / WPR) * R2) == 0) {
-        const size_t lf = std::max(lds, sizeof(ds4_smem));
+    const size_t lf = std::max(lds, sizeof(ds4_smem));
+    if (t_fa && !t_fa->done && a1.pro.kind && t_fa->a.D % ((NWV / WPR) * R1) == 0 && t_fa->a.D % ((NWV / WPR) * R2) == 0 &&
+        fa_lds_fits(k_gemv_os2_fa<T1, T2, R2, WPR, R1>, lf)) {
+        if (getenv("GGML_MI355X_DEBUG_FUSE")) fprintf(stderr, "[mi355x]   fused launch (2 types): lds %zu, body %zu, grid %u + %d\n", lds, sizeof(ds4_smem), grid, t_fa->nfa);
         a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv2+pro+epi+fa", grid + t_fa->nfa, kt_threads()) : nullptr;
-        fa_lds_attr(k_gemv_os2_fa<T1, T2, R2, WPR, R1>, lf);
         hipLaunchKernelGGL((k_gemv_os2_fa<T1, T2, R2, WPR, R1>), dim3(grid + t_fa->nfa), dim3(64 * NWV), lf, st, a1, ng1, a2, t_fa->a,
                            t_fa->fz, t_fa->nfa);
+        MI_CHECK(hipPeekAtLastError());
         t_fa->done = true;
         return;
     }
