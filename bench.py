@@ -41,7 +41,7 @@ MFMA_I8_PEAK_TOPS = 5000.0
 # output (last token) + attention
 PP512_FLOP = 7.22e12
 # HBM bytes per decode-GEMV launch from a separate rocprofv3 --pmc FETCH_SIZE pass of the SAME
-# model (scripts/gpu_r06_bench.sh, scripts/pmc_traffic.py), one file per --config
+# model (scripts/gpu_r06_pmc.sh, scripts/pmc_traffic.py), one file per --config
 TRAFFIC_DIR = os.path.join("profiles", "r06", "pmc")
 
 
@@ -381,7 +381,7 @@ def emit(a, la, gguf_synth, cfg, suffix, ws, gpu, n_ctx, r):
             "peak_measured": round(hbm, 1) if hbm > 0 else None,
             "frac_of_measured": round(achieved / hbm, 4) if achieved and hbm > 0 else None,
             "traffic": traffic,
-            "traffic_source": f"{tf}: a separate rocprofv3 --pmc FETCH_SIZE pass of {a.config} (scripts/gpu_r06_bench.sh), not this run" if traffic else None,
+            "traffic_source": f"{tf}: a separate rocprofv3 --pmc FETCH_SIZE pass of {a.config} (scripts/gpu_r06_pmc.sh), not this run" if traffic else None,
             # the event-timed pass runs eagerly (hipGraph replay off, so every GEMV launch carries
             # its own events); the replayed product path's per-launch times are in the in-graph
             # timeline (scripts/ktrace.py, profiles/r04/ktrace_base.txt)
