@@ -501,7 +501,8 @@ static void plan_resid(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tenso
     // output head) that is thousands of redundant norms, and the stand-alone norm kernel plus a
     // prologue-free launch measured faster (round 3 kernel timeline: gate/up 27.0 us with the
     // prologue vs 15 + 4 without); Q/K/V keep it
-    if (rows > 16384) return;
+    static const long max_rows = getenv("GGML_MI355X_PRO_MAXROWS") ? atol(getenv("GGML_MI355X_PRO_MAXROWS")) : 16384;
+    if (rows > max_rows) return;
     if (!dead_after(g, n, pl + 1, last, readers)) return;
     if (mul && !dead_after(g, n, pn + 1, nm, {mul})) return;
     epi.rres = (const float *) res->data;
