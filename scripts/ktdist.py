@@ -16,6 +16,8 @@ if not S0:
     sys.exit("no [ktdist] lines")
 for nm, a in (("wg<split start", S0), ("wg<split end", E0), ("wg>=split start", S1), ("wg>=split end", E1)):
     a = np.concatenate(a)
+    if a.size == 0:
+        continue
     print(f"{nm:16s} n {len(a):6d}  p10 {np.percentile(a, 10):6.2f}  p50 {np.percentile(a, 50):6.2f}  p90 {np.percentile(a, 90):6.2f}  max {a.max():6.2f}")
 # the latest-ending workgroups of the rest, by index (mean over launches)
 e1 = np.mean(np.stack(E1), axis=0)
