@@ -6,7 +6,6 @@
 // node loop (the hot loop of SURVEY.md §3.1) and applies the fusions documented in
 // DESIGN.md (RMS_NORM + MUL).
 #include "ops.h"
-#include "fattn.h"
 #include <atomic>
 #include <mutex>
 
@@ -549,78 +548,6 @@ static bool plan_norm_prologue(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
 // projection, the NORM-mode ROPE of a projection, and f16 KV-cache stores (CPY) of a
 // projection or of its rope.  Every hoisted node's outputs are checked against what the
 // skipped-over nodes read and write, and against the other outputs of the launch.
-// The decode attention that reads this Q/K/V launch's outputs rides in the launch (k_gemv.hip
-// k_gemv_os_fa, fa_dsh4.h): the launch's three matrices are Q (rope output stored), K (rope stored
-// to the cache) and V (stored to the cache); the first FLASH_ATTN_EXT after it, with nothing but
-// views and this launch's own nodes in between, reads that Q rope and views of those two caches;
-// the four-wave attention applies (fattn_carry_ok).  fal, fa, mmo (the output projection that
-// takes its quantized output) and act (that quantization) are set for the launch.
-static bool plan_fa_carry(exec_ctx & ctx, ggml_cgraph * g, int i, int n, ggml_tensor * const * mms, int nm,
-                          const gemv_epi & epi, const std::vector<const ggml_tensor *> & absorbed,
-                          const std::vector<const ggml_tensor *> & outs, gemv_fa & fal,
-                          ggml_tensor *& fa, const ggml_tensor *& mmo, q8_act & act) {
-    if (ctx.timing || !epi.px || nm != 3) return false;
-    int rq = -1, rk = -1, rv = -1;
-    for (int m = 0; m < 3; ++m) {
-        if (epi.rope[m] && !epi.rope_f16[m] && !epi.elide_rope[m] && rq < 0) rq = m;
-        else if (epi.rope[m] && epi.rope_f16[m] && rk < 0) rk = m;
-        else if (!epi.rope[m] && epi.f16out[m] && rv < 0) rv = m;
-    }
-    static const bool dbg = getenv("GGML_MI355X_DEBUG_FUSE") != nullptr;
-    if (dbg) fprintf(stderr, "[mi355x]   fa carry: roles q=%d k=%d v=%d\n", rq, rk, rv);
-    if (rq < 0 || rk < 0 || rv < 0) return false;
-    // the caches the K and V stores write (their CPY nodes are absorbed by this launch)
-    const ggml_tensor * kc = nullptr, * vc = nullptr;
-    for (const ggml_tensor * t : absorbed) {
-        if (t->op != GGML_OP_CPY) continue;
-        if (base_of(t->src[0]) == epi.rope[rk]) kc = base_of(t->src[1]);
-        if (base_of(t->src[0]) == mms[rv]) vc = base_of(t->src[1]);
-    }
-    fa = nullptr;
-    for (int k = i + 1; k < n && k <= i + 32; ++k) {
-        ggml_tensor * t = ggml_graph_node(g, k);
-        if (t->op == GGML_OP_FLASH_ATTN_EXT) { fa = t; break; }
-        if (is_view_op(t) || ggml_is_empty(t) || std::find(absorbed.begin(), absorbed.end(), t) != absorbed.end()) continue;
-        bool mine = false;
-        for (int m = 0; m < nm; ++m) mine = mine || t == mms[m];
-        if (!mine) return false;   // a node of its own runs between the launch and the attention
-    }
-    if (dbg) fprintf(stderr, "[mi355x]   fa carry: caches %d/%d attention %s q=%d k=%d v=%d\n", kc != nullptr, vc != nullptr,
-                     fa ? fa->name : "-", fa && base_of(fa->src[0]) == epi.rope[rq], fa && base_of(fa->src[1]) == kc,
-                     fa && base_of(fa->src[2]) == vc);
-    if (!fa || base_of(fa->src[0]) != epi.rope[rq] || base_of(fa->src[1]) != kc || base_of(fa->src[2]) != vc) return false;
-    // the attention's output is written while other workgroups of the launch still read the
-    // prologue input and store their rows: it may alias none of them
-    const char * xb = (const char *) epi.px, * xe = xb + epi.pn * sizeof(float);
-    const char * ob = (const char *) fa->data, * oe = ob + ggml_nbytes(fa);
-    if (overlaps_any(fa, outs) || (ob < xe && xb < oe)) return false;
-    // the output projection that takes the attention's quantized output (op_compute's own rule)
-    mmo = nullptr;
-    const int fi = node_index(g, fa);
-    ggml_tensor * r = at(g, fi + 1, n);
-    ggml_tensor * c = at(g, fi + 2, n);
-    if (r && c && (r->op == GGML_OP_RESHAPE || r->op == GGML_OP_VIEW) && r->view_src == fa && r->data == fa->data &&
-        ggml_is_contiguous(r) && c->op == GGML_OP_MUL_MAT && c->src[1] == r && (gemv_supported(c) || mmq_supported(c))) {
-        mmo = c;
-    }
-    if (!ctx.fa4_cnt) {
-        if (ctx.capturing) return false;
-        MI_CHECK(hipMalloc(&ctx.fa4_cnt, exec_ctx::FA4_CNT * sizeof(int)));
-        MI_CHECK(hipMemsetAsync(ctx.fa4_cnt, 0, exec_ctx::FA4_CNT * sizeof(int), ctx.stream));
-    }
-    if (!kc || !vc) return false;
-    int64_t nq3 = 1;
-    fa_args_of(ctx, fa, mmo, fal.a, act, nq3);
-    if (dbg) fprintf(stderr, "[mi355x]   fa carry: out-proj %d carry_ok %d\n", mmo != nullptr, fattn_carry_ok(fal.a, nq3));
-    if (!fattn_carry_ok(fal.a, nq3) || fal.a.H / 2 > exec_ctx::FA4_CNT) return false;
-    static const int fa4_print = getenv("GGML_MI355X_FA4_PRINT") ? atoi(getenv("GGML_MI355X_FA4_PRINT")) : 0;
-    fal.fz = {ctx.fa4_cnt, (int) (4 * fal.a.D), (uint16_t * const *) epi.rope_f16[rk], (uint16_t * const *) epi.f16out[rv], fa4_print};
-    fal.nfa = (int) (fal.a.H / 2);
-    fal.role[rq] = 0; fal.role[rk] = 1; fal.role[rv] = 2;
-    fal.done = false;
-    return true;
-}
-
 int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     ggml_tensor * mm0 = ggml_graph_node(g, i);
     ggml_tensor * mms[3] = {mm0, nullptr, nullptr};
@@ -743,17 +670,7 @@ int op_gemv_grouped(exec_ctx & ctx, ggml_cgraph * g, int i, int n) {
     }
     if (resid && prologues_enabled() && plain && nm == 1) plan_resid(ctx, g, i, n, mm0, epi, absorbed);
     if (dbg && (epi.rres || epi.px)) fprintf(stderr, "[mi355x]   resid=%d prologue=%d\n", epi.rres != nullptr, epi.px != nullptr);
-    // the decode attention of these Q/K/V rows, carried in the same launch
-    gemv_fa fal = {};
-    ggml_tensor * fa = nullptr;
-    const ggml_tensor * fa_mm = nullptr;
-    q8_act fa_act = {};
-    const bool try_fa = plan_fa_carry(ctx, g, i, n, mms, nm, epi, absorbed, outs, fal, fa, fa_mm, fa_act);
-    if (gemv_group(ctx, mms, nm, &epi, try_fa ? &fal : nullptr)) {
-        absorbed.push_back(fa);
-        if (fal.a.qmode) ctx.qcache_put(fa_mm->src[1], fal.a.qmode == 1, fa_act);
-        if (dbg) fprintf(stderr, "[mi355x]   attention %s carried in the launch\n", fa->name);
-    }
+    gemv_group(ctx, mms, nm, &epi);
     // node i+1 when it is node i's SiLU is consumed here; everything else is skipped later
     const bool next_absorbed = epi.silu[0] && epi.silu[0] == at(g, i + 1, n);
     for (const ggml_tensor * t : absorbed) {

@@ -30,26 +30,9 @@ struct fa_args {
     unsigned long long * kt;
 };
 
-// the hand-off of an attention carried in the Q/K/V launch (fa_dsh4.h; k_gemv.hip k_gemv_os_fa):
-// cnt[hp] reaches `expect` once every projection row this head pair reads is stored
-// write-through; kslot / vslot hold the token's K / V cache-row destinations
-struct fa_fuse {
-    int * cnt; int expect;
-    uint16_t * const * kslot; uint16_t * const * vslot;
-    int dbg;   // GGML_MI355X_FA4_PRINT=1: workgroup 0 prints its phase times (diagnostics)
-};
-
-// an attention the Q/K/V launch carries (gemv_group's fal): its arguments, the hand-off, its
-// workgroups, the role of each of the launch's matrices (0 Q, 1 K, 2 V), launched or not
-struct gemv_fa {
-    fa_args a; fa_fuse fz; int nfa; int role[3]; bool done;
-};
-
 // the FLASH_ATTN_EXT node's arguments (and the quantization of its output for the output
 // projection mm, act); op_flash_attn launches them
 void fa_args_of(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm, fa_args & a, q8_act & act, int64_t & nq3);
-// the attention can be carried in the Q/K/V launch (the four-wave body, fa_dsh4.h)
-bool fattn_carry_ok(const fa_args & a, int64_t nq3);
 
 // set by mi355x_bench_op (capi.cpp) only; copied into fa_args.prof
 extern unsigned long long * g_fa_prof;
@@ -65,9 +48,6 @@ bool fattn_dec2_ok(const fa_args & a, int64_t nq3);
 // decode, D = 128, f16 cache of at most 256 positions (tg128's depths): every load issued at the
 // launch's start, two heads (one KV head) per 512-thread workgroup (GGML_MI355X_FA_DSH=0: dec2)
 bool fattn_dsh_ok(const fa_args & a, int64_t nq3);
-// the four-wave body (fa_dsh4.h) as its own launch: GGML_MI355X_FA_DSH4=1 (parity runs)
-bool fattn_dsh4_standalone();
-void launch_fattn_dsh4(hipStream_t stream, const fa_args & a, int64_t nq3);
 void launch_fattn_dsh(hipStream_t stream, const fa_args & a, int64_t nq3);
 // the prefill batch tile (k_fattn_pf) runs this batch and can quantize its output (qmode 1):
 // f16 cache, D = 128, a GQA group of 4, 8 or 16 heads

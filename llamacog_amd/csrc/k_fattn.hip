@@ -100,15 +100,6 @@ void fa_args_of(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm, fa_ar
     }
 }
 
-// the Q/K/V launch can carry this attention (fa_dsh4.h): the short-context kernel's conditions, one
-// batch, at most 64 head pairs (fewer than the CUs).  Opt-in (GGML_MI355X_FA_CARRY=1): measured
-// slower so far (8B tg 2.44 vs 2.16 ms/token: the projection's K/V workgroups end 2-6 us later in
-// the carried launch and the attention waits for the last of them)
-bool fattn_carry_ok(const fa_args & a, int64_t nq3) {
-    static const bool on = getenv("GGML_MI355X_FA_CARRY") && atoi(getenv("GGML_MI355X_FA_CARRY")) != 0;
-    return on && nq3 == 1 && a.H / 2 <= 64 && fattn_dsh_ok(a, nq3);
-}
-
 void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
     fa_args a;
     q8_act act;
@@ -129,9 +120,6 @@ void op_flash_attn(exec_ctx & ctx, ggml_tensor * dst, const ggml_tensor * mm) {
         unsigned long long * kts = ctx.kt_take("fa_scores", (unsigned) (ceil_div(a.n_kv, (int64_t) FAL_PB) * a.Hkv), 256);
         a.kt = ctx.kt_take("fa_chain", (unsigned) (a.H * FAL_DSPLIT), FAL_THREADS);
         launch_fattn_long(ctx.stream, a, sco, kts);
-    } else if (fattn_dsh_ok(a, nq3) && fattn_dsh4_standalone()) {
-        a.kt = ctx.kt_take("fa_dsh4", (unsigned) (a.H / 2 * nq3), 256);
-        launch_fattn_dsh4(ctx.stream, a, nq3);
     } else if (fattn_dsh_ok(a, nq3)) {
         a.kt = ctx.kt_take("fa_dsh", (unsigned) (a.H / 2 * nq3), 512);
         launch_fattn_dsh(ctx.stream, a, nq3);

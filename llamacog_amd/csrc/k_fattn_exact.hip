@@ -38,7 +38,6 @@
 #include "qtypes.h"
 #include "fa_chain.h"
 #include "fa_util.h"
-#include "fa_dsh4.h"
 
 #include <cmath>
 
@@ -1545,25 +1544,6 @@ __global__ __launch_bounds__(512, 1) void k_fattn_dsh(const fa_args a) {
         for (int i = 0; i < 8; ++i) if (pt[i]) a.prof[i] += pt[i];
     }
     kt_exit(a.kt, 9);
-}
-
-// the four-wave body of fa_dsh4.h as its own launch (GGML_MI355X_FA_DSH4=1; the Q/K/V launch
-// carries the same body when it takes the attention, k_gemv.hip)
-__global__ __launch_bounds__(256, 1) void k_fattn_dsh4(const fa_args a) {
-    __shared__ __attribute__((aligned(16))) ds4_smem sm4;
-    kt_enter(a.kt, 5);
-    const fa_fuse fz = {};
-    fa_dsh4_body<false>(a, blockIdx.x, blockIdx.y, fz, sm4);
-    kt_exit(a.kt, 5);
-}
-
-bool fattn_dsh4_standalone() {
-    static const bool on = getenv("GGML_MI355X_FA_DSH4") && atoi(getenv("GGML_MI355X_FA_DSH4")) != 0;
-    return on;
-}
-
-void launch_fattn_dsh4(hipStream_t st, const fa_args & a, int64_t nq3) {
-    hipLaunchKernelGGL(k_fattn_dsh4, dim3((unsigned) (a.H / 2), (unsigned) nq3), dim3(256), 0, st, a);
 }
 
 // the short-context kernel applies: one query row, D = 128, f16 K and V, at most DS_MAXKV

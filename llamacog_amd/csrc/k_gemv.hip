@@ -26,7 +26,6 @@
 #include "rope.h"
 #include "qtypes.h"
 #include "quant_act.h"
-#include "fa_dsh4.h"
 
 namespace mi355x {
 
@@ -74,10 +73,6 @@ struct gemv_args {
     // same slots are two such matrices of one launch
     const char * xids; int64_t xids_nb0, xnb02, xme; int xn_as;
     int64_t xqs_st, xd_st, xs_st;
-    // the fused attention's hand-off (k_gemv_os_fa): matrix i is the launch's Q (0), K (1) or V (2)
-    // projection (-1: none); a workgroup adds its stored rows to fa_cnt of every head pair that
-    // reads them (fa_hd rows per head, fa_g query heads per KV head)
-    int * fa_cnt; int fa_role[GEMV_MAXMAT]; int fa_hd, fa_g;
 };
 
 // MI_KT_PHASE=1 (a profiling build, EXTRA=-DMI_KT_PHASE=1): thread 0 of every one-shot workgroup
@@ -273,23 +268,11 @@ static inline uint32_t pro_lds_bytes(int64_t n, int qmode) {
     return (uint32_t) (n + 4 * nd + ((2 * ns + 15) / 16) * 16);
 }
 
-// write-through stores (sc1): a reader in the same launch sees them once they are drained
-__device__ __forceinline__ void st_wt(float * p, float v) { asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory"); }
-__device__ __forceinline__ void st_wt(uint16_t * p, uint16_t v) {
-    asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"((uint32_t) v) : "memory");
-}
-template <bool WT, class V> __device__ __forceinline__ void st_ep(V * p, V v) {
-    if constexpr (WT) st_wt(p, v);
-    else *p = v;
-}
-
-// epilogue of one output row; v = this row's value, vp = the value of its rope partner row^1;
-// WT: every store write-through (the fused attention reads them in the same launch)
-template <bool WT = false>
+// epilogue of one output row; v = this row's value, vp = the value of its rope partner row^1
 __device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t M, int64_t row, float v, float vp,
                                            const float2 * rtab, uint16_t * const * f16p) {
-    if (p.dst[mi]) st_ep<WT>(p.dst[mi] + row, v);
-    if (p.f16out[mi]) st_ep<WT>(f16p[2 * mi] + row, f2h(v));
+    if (p.dst[mi]) p.dst[mi][row] = v;
+    if (p.f16out[mi]) f16p[2 * mi][row] = f2h(v);
     if (p.silu[mi]) {
         // ggml_vec_silu_f32 (vec.cpp:233): AVX-512 ggml_v_silu on 16-element chunks, libm tail
         const int64_t nvec = (M / 16) * 16;
@@ -305,8 +288,8 @@ __device__ __forceinline__ void gemv_store(const gemv_args & p, int mi, int64_t 
             rope_rotate(odd ? vp : v, odd ? v : vp, c, sn, o0, o1);
             o = odd ? o1 : o0;
         }
-        if (p.rope_out[mi]) st_ep<WT>(p.rope_out[mi] + row, o);
-        if (p.rope_f16[mi]) st_ep<WT>(f16p[2 * mi + 1] + row, f2h(o));
+        if (p.rope_out[mi]) p.rope_out[mi][row] = o;
+        if (p.rope_f16[mi]) f16p[2 * mi + 1][row] = f2h(o);
     }
 }
 
@@ -479,7 +462,7 @@ template <class T> struct os_geo {
     static constexpr int SLICE = NI * 1024;                               // LDS bytes per slice
 };
 
-template <class T, int R, int WPR, int MODE, bool PRO, bool ID = false, bool FAC = false>
+template <class T, int R, int WPR, int MODE, bool PRO, bool ID = false>
 __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t g, uint8_t * wl, uint32_t * xr) {
     constexpr int NWV = 4;
     constexpr int NT = 64 * NWV;
@@ -673,22 +656,7 @@ __device__ __forceinline__ void gemv_os_body(const gemv_args & p, const int64_t 
         for (int i = threadIdx.x; i < RPG; i += NT) {
             const int64_t row = (g - p.blk0[mi]) * RPG + i;
             // rope partner row ^ 1 lies in the same group (RPG is even whenever rope is fused)
-            if (row < M) gemv_store<FAC>(p, mi, M, row, res[i], res[RPG > 1 ? i ^ 1 : i], rtab, f16p);
-        }
-        if constexpr (FAC) {
-            // the group's rows are stored write-through and drained: count them for every head pair
-            // of the fused attention that reads them (a Q row: its head's pair; a K / V row: the
-            // pairs of its KV head's group)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            const int role = p.fa_role[mi];
-            if (threadIdx.x == 0 && role >= 0) {
-                const int64_t r0 = (g - p.blk0[mi]) * RPG;
-                const int nr = (int) min<int64_t>(RPG, M - r0);
-                const int h = (int) (r0 / p.fa_hd);
-                if (role == 0) atomicAdd(p.fa_cnt + h / 2, nr);
-                else for (int hp = h * p.fa_g / 2; hp < (h + 1) * p.fa_g / 2; ++hp) atomicAdd(p.fa_cnt + hp, nr);
-            }
+            if (row < M) gemv_store(p, mi, M, row, res[i], res[RPG > 1 ? i ^ 1 : i], rtab, f16p);
         }
     }
 }
@@ -713,32 +681,6 @@ __global__ __launch_bounds__(256) void k_gemv_os2(const gemv_args p1, const int6
     kt_exit(p1.kt, KT_STRIDE);
 }
 
-// The Q/K/V projection with the decode attention of its heads in the same launch (fa_dsh4.h):
-// workgroups [0, nfa) are the attention's (one per head pair), the rest the projection's row groups
-// (the norm prologue, the rope and KV-store epilogues, stores write-through and counted per head
-// pair).  The attention workgroups wait only on the counters, and are at most 64 (fewer than the
-// CUs, each holding one CU's LDS at most half): every projection workgroup can always run, so the
-// launch cannot deadlock whatever the dispatch order.
-template <class T, int R, int WPR>
-__global__ __launch_bounds__(256) void k_gemv_os_fa(const gemv_args p, const fa_args fa, const fa_fuse fz, const int nfa) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
-    kt_enter(p.kt, KT_STRIDE);
-    if ((int) blockIdx.x < nfa) fa_dsh4_body<true>(fa, blockIdx.x, 0, fz, *(ds4_smem *) xr);
-    else gemv_os_body<T, R, WPR, 1, true, false, true>(p, (int64_t) blockIdx.x - nfa, (uint8_t *) xr + p.wl_off, xr);
-    kt_exit(p.kt, KT_STRIDE);
-}
-
-template <class T1, class T2, int R2, int WPR, int R1>
-__global__ __launch_bounds__(256) void k_gemv_os2_fa(const gemv_args p1, const int64_t ng1, const gemv_args p2, const fa_args fa,
-                                                     const fa_fuse fz, const int nfa) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t xr[];
-    kt_enter(p1.kt, KT_STRIDE);
-    const int64_t b = (int64_t) blockIdx.x - nfa;
-    if (b < 0) fa_dsh4_body<true>(fa, blockIdx.x, 0, fz, *(ds4_smem *) xr);
-    else if (b < ng1) gemv_os_body<T1, R1, WPR, 1, true, false, true>(p1, b, (uint8_t *) xr + p1.wl_off, xr);
-    else gemv_os_body<T2, R2, WPR, 1, true, false, true>(p2, b - ng1, (uint8_t *) xr + p2.wl_off, xr);
-    kt_exit(p1.kt, KT_STRIDE);
-}
 
 // ---- host ----------------------------------------------------------------------------------------
 // kernel-timing mode: the GEMV kernel itself is launched with start/stop events
@@ -747,24 +689,6 @@ __global__ __launch_bounds__(256) void k_gemv_os2_fa(const gemv_args p1, const i
 static thread_local hipEvent_t t_ev_beg = nullptr, t_ev_end = nullptr;
 // the launching context while a gemv_group runs (kernel timeline regions come from it)
 static thread_local exec_ctx * g_kt_ctx = nullptr;
-// the attention to carry in this gemv_group's launch (gemv_group's fal), done once it is launched
-static thread_local gemv_fa * t_fa = nullptr;
-
-// the carried launch's workgroups (static + dynamic LDS) fit two to a CU, so its projection rows all
-// start at once (one to a CU, the two-type launch's second half started 8-11 us late); the
-// attribute raise for dynamic LDS above 64 KiB is advisory on ROCm (it may refuse the call)
-template <class K>
-static bool fa_lds_fits(K kernel, size_t lds) {
-    static std::once_flag once;
-    static size_t st = 160 * 1024;
-    std::call_once(once, [&] {
-        (void) hipFuncSetAttribute((const void *) kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds);
-        hipFuncAttributes fa;
-        if (hipFuncGetAttributes(&fa, (const void *) kernel) == hipSuccess) st = fa.sharedSizeBytes;
-        (void) hipGetLastError();
-    });
-    return 2 * (st + lds) <= 160 * 1024;
-}
 
 static int g_gemv_wgs = -1;    // the pipelined kernel's persistent grid (2048: 8 per CU)
 static int g_num_cu = 0;
@@ -914,18 +838,6 @@ static void launch_os_m(hipStream_t st, gemv_args & a, int nmat) {
     const int64_t ng = set_groups(a, nmat, RPG);
     const size_t lds = os_lds_layout<T, R, WPR>(a);
     const int64_t grid = ng;
-    if constexpr (MODE == 1 && WPR == 1) {
-        // the attention rides in this launch (a workgroup's rows lie in one head: its counter add)
-        const size_t lf = std::max(lds, sizeof(ds4_smem));
-        if (t_fa && !t_fa->done && a.pro.kind && t_fa->a.D % RPG == 0 && fa_lds_fits(k_gemv_os_fa<T, R, WPR>, lf)) {
-            if (getenv("GGML_MI355X_DEBUG_FUSE")) fprintf(stderr, "[mi355x]   fused launch: lds %zu, body %zu, grid %lld + %d\n", lds, sizeof(ds4_smem), (long long) grid, t_fa->nfa);
-            a.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv+pro+epi+fa", (unsigned) (grid + t_fa->nfa), kt_threads()) : nullptr;
-            hipLaunchKernelGGL((k_gemv_os_fa<T, R, WPR>), dim3((unsigned) (grid + t_fa->nfa)), dim3(256), lf, st, a, t_fa->a, t_fa->fz, t_fa->nfa);
-            MI_CHECK(hipPeekAtLastError());
-            t_fa->done = true;
-            return;
-        }
-    }
     a.kt = g_kt_ctx ? g_kt_ctx->kt_take(gemv_kt_name(a, MODE), (unsigned) grid, kt_threads()) : nullptr;
 #define OS_LAUNCH(P)                                                                                              \
     if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os<T, R, WPR, MODE, P, false>), dim3((unsigned) grid), dim3(256), lds, st, t_ev_beg, t_ev_end, 0, a); \
@@ -1041,17 +953,6 @@ static void launch_os2_v(hipStream_t st, gemv_args & a1, int n1, gemv_args & a2,
     os_plain_geo<T2, R2, WPR>(a2);
     const size_t lds = off + std::max((size_t) 4 * R1 * os_geo<T1>::SLICE, (size_t) 4 * R2 * os_geo<T2>::SLICE);
     const unsigned grid = (unsigned) (ng1 + ng2);
-    const size_t lf = std::max(lds, sizeof(ds4_smem));
-    if (t_fa && !t_fa->done && a1.pro.kind && t_fa->a.D % ((NWV / WPR) * R1) == 0 && t_fa->a.D % ((NWV / WPR) * R2) == 0 &&
-        fa_lds_fits(k_gemv_os2_fa<T1, T2, R2, WPR, R1>, lf)) {
-        if (getenv("GGML_MI355X_DEBUG_FUSE")) fprintf(stderr, "[mi355x]   fused launch (2 types): lds %zu, body %zu, grid %u + %d\n", lds, sizeof(ds4_smem), grid, t_fa->nfa);
-        a1.kt = g_kt_ctx ? g_kt_ctx->kt_take("gemv2+pro+epi+fa", grid + t_fa->nfa, kt_threads()) : nullptr;
-        hipLaunchKernelGGL((k_gemv_os2_fa<T1, T2, R2, WPR, R1>), dim3(grid + t_fa->nfa), dim3(64 * NWV), lf, st, a1, ng1, a2, t_fa->a,
-                           t_fa->fz, t_fa->nfa);
-        MI_CHECK(hipPeekAtLastError());
-        t_fa->done = true;
-        return;
-    }
     a1.kt = g_kt_ctx ? g_kt_ctx->kt_take(a1.pro.kind ? "gemv2+pro+epi" : "gemv2+epi", grid, kt_threads()) : nullptr;
 #define OS2_LAUNCH(P)                                                                                                 \
     if (t_ev_beg) hipExtLaunchKernelGGL((k_gemv_os2<T1, T2, R2, WPR, P, R1>), dim3(grid), dim3(64 * NWV), lds, st, t_ev_beg, \
@@ -1217,10 +1118,9 @@ bool gemv_epilogue_ok(const ggml_tensor * mm) { return gemv_supported(mm); }
 
 // one launch for up to three MUL_MATs sharing src1 (all gemv_supported, same K; a second
 // K-quant type joins as the second body of k_gemv_pipe2)
-bool gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi, gemv_fa * fal) {
+void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi) {
     GGML_ASSERT(nmat >= 1 && nmat <= GEMV_MAXMAT);
     gemv_init();
-    t_fa = fal;
     g_kt_ctx = ctx.kt_buf && ktrace_enabled() ? &ctx : nullptr;
     const ggml_tensor * src1 = mms[0]->src[1];
     const ggml_type wt = mms[0]->src[0]->type;
@@ -1263,10 +1163,6 @@ bool gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         }
     }
     a.A = {act.qs, act.d, act.s};
-    a.fa_cnt = fal ? fal->fz.cnt : nullptr;
-    for (int i = 0; i < GEMV_MAXMAT; ++i) a.fa_role[i] = fal && i < nmat ? fal->role[i] : -1;
-    a.fa_hd = fal ? (int) fal->a.D : 0;
-    a.fa_g = fal ? (int) (fal->a.H / fal->a.Hkv) : 0;
     if (pro) {
         GGML_ASSERT(epi->pn == src1->ne[0] && epi->pn % 256 == 0 && epi->pkind == 1);
         auto & r = a.pro;
@@ -1320,7 +1216,6 @@ bool gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
                 d.W[k] = a.W[s]; d.nb01[k] = a.nb01[s]; d.M[k] = a.M[s];
                 d.dst[k] = a.dst[s]; d.silu[k] = a.silu[s]; d.f16out[k] = a.f16out[s];
                 d.rope_out[k] = a.rope_out[s]; d.rope_f16[k] = a.rope_f16[s];
-                d.fa_role[k] = k < cnt ? a.fa_role[s] : -1;
                 if (k < cnt && epi && epi->rope[s]) d.need_pairs = 1;
             }
             d.ntasks = (int) (nblk * 4);
@@ -1351,8 +1246,6 @@ bool gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_
         t_ev_beg = t_ev_end = nullptr;
     }
     g_kt_ctx = nullptr;
-    t_fa = nullptr;
-    return fal && fal->done;
 }
 
 // ---- MUL_MAT_ID of one token on the one-shot kernel ----------------------------------------------

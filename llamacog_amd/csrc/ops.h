@@ -42,10 +42,6 @@ struct exec_ctx {
     // arrival counters of the flash-attention output quantization (k_fattn_exact.hip)
     static constexpr int FA_CNT = 1024;
     int *   fa_cnt = nullptr;
-    // per-head-pair counters of the attention carried in the Q/K/V launch (k_gemv_os_fa; zeroed
-    // once, reset by their attention workgroup)
-    static constexpr int FA4_CNT = 256;
-    int *   fa4_cnt = nullptr;
     // arrival counters of the multi-workgroup MoE router, one per token (k_elem.hip)
     static constexpr int MOE_CNT = 4096;
     int *   moe_cnt = nullptr;
@@ -249,9 +245,7 @@ struct gemv_epi {
 };
 bool gemv_supported(const ggml_tensor * mm);
 bool gemv_epilogue_ok(const ggml_tensor * mm);   // the kernel path that carries epilogues applies
-struct gemv_fa;   // fattn.h: a decode attention to carry in the launch
-// true: fal's attention was launched with the matrices (fal->done)
-bool gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi, gemv_fa * fal = nullptr);
+void gemv_group(exec_ctx & ctx, ggml_tensor * const * mms, int nmat, const gemv_epi * epi);
 bool gemv_mixed_ok(const ggml_tensor * mm0, const ggml_tensor * c);   // c may join mm0's launch as a second weight type
 
 // lays out a q8_act (qs | d | s, 256-B aligned) in `base`
