@@ -114,6 +114,36 @@ __device__ __forceinline__ float dot_f16_mix_d128(const uint2 (&kh)[8], const fl
     return __fadd_rn(__fadd_rn(w[0], w[2]), __fadd_rn(w[1], w[3]));
 }
 
+// mixfma with q as well held as an f16 half: fma(f32(k half SK), f32(q half SQ), acc), one rounding
+template <int SK, int SQ>
+__device__ __forceinline__ float mixfma_h(uint32_t kbits, uint32_t qbits, float acc) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[%4,%5,0] op_sel_hi:[1,1,0]" : "=v"(r) : "v"(kbits), "v"(qbits), "v"(acc), "n"(SK), "n"(SQ));
+    return r;
+}
+
+// dot_f16_mix_d128 with q as packed f16 pairs: qh[m][h] = (q[16m + 4qd + 2h], q[16m + 4qd + 2h + 1]) rounded to
+// f16 (the CPU's Q conversion), half the registers of the f32 copy; the same products and order
+__device__ __forceinline__ float dot_f16_mix_d128_h(const uint2 (&kh)[8], const uint32_t (&qh)[8][2], float nz) {
+    float w[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float acc[4];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const uint32_t k0 = c < 2 ? kh[jj].x : kh[jj].y, k1 = c < 2 ? kh[4 + jj].x : kh[4 + jj].y;
+            float t = (c & 1) ? mixfma_h<1, 1>(k0, qh[jj][c >> 1], nz) : mixfma_h<0, 0>(k0, qh[jj][c >> 1], nz);
+            acc[jj] = (c & 1) ? mixfma_h<1, 1>(k1, qh[4 + jj][c >> 1], t) : mixfma_h<0, 0>(k1, qh[4 + jj][c >> 1], t);
+        }
+        w[c] = __fadd_rn(__fadd_rn(acc[0], acc[2]), __fadd_rn(acc[1], acc[3]));
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = __fadd_rn(w[c], quad_from_plus2(w[c]));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w[c] = __fadd_rn(w[c], quad_from_plus1(w[c]));
+    return __fadd_rn(__fadd_rn(w[0], w[2]), __fadd_rn(w[1], w[3]));
+}
+
 // wave-wide inclusive max-scan by DPP (rows by row_shr 1/2/4/8, then row_bcast:15 / :31 —
 // GFX9 DPP), and the exclusive shift by one lane (wave_shr:1); absent sources read -inf
 template <int CTRL, int ROWS = 0xf>

@@ -548,14 +548,17 @@ __device__ __forceinline__ float2 f32x2_mul(float2 a, float2 b) {
     return r;
 }
 
-template <int G>
-__global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
+template <int G, int CH = PF_CH, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void k_fattn_pf(const fa_args a) {
     constexpr int D = 128, NM = D / 16, QB = PF_P / G;
-    __shared__ __attribute__((aligned(16))) uint16_t kl[2][PF_CH * D];
-    __shared__ __attribute__((aligned(16))) uint16_t vl[2][PF_CH * D];
-    __shared__ __attribute__((aligned(16))) uint16_t ml[2][QB * PF_CH];   // mask values (f16)
-    __shared__ __attribute__((aligned(16))) float sc[PF_CH * PF_P];       // scores -> vs, [pos][pair]
-    __shared__ __attribute__((aligned(16))) float cm[PF_CH * PF_P];       // ms, [pos][pair]
+    // the 32-position variant: 4-position batches and q held as packed f16 pairs (its VGPR budget)
+    constexpr int U = CH == 32 ? 4 : PF_U;
+    constexpr bool QH = CH == 32;
+    __shared__ __attribute__((aligned(16))) uint16_t kl[2][CH * D];
+    __shared__ __attribute__((aligned(16))) uint16_t vl[2][CH * D];
+    __shared__ __attribute__((aligned(16))) uint16_t ml[2][QB * CH];   // mask values (f16)
+    __shared__ __attribute__((aligned(16))) float sc[CH * PF_P];       // scores -> vs, [pos][pair]
+    __shared__ __attribute__((aligned(16))) float cm[CH * PF_P];       // ms, [pos][pair]
     __shared__ int wend[4];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -590,7 +593,7 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
         __syncthreads();
         nend = max(max(wend[0], wend[1]), max(wend[2], wend[3])) + 1;
     }
-    const int nchunk = (int) ((nend + PF_CH - 1) / PF_CH);
+    const int nchunk = (int) ((nend + CH - 1) / CH);
     // microbenchmark hook: per-phase s_memtime cycles of workgroup (0, 0) wave 0 (capi.cpp op 302)
     const bool prof = a.prof && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0;
     unsigned long long tp = prof ? __builtin_amdgcn_s_memtime() : 0, pc[6] = {0, 0, 0, 0, 0, 0};
@@ -600,9 +603,9 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
 
     // ---- staging: K (swizzled) and V rows of a chunk by LDS-DMA, its mask through registers -----
     auto issue_kv = [&](int c, int s) {
-        const int64_t c0 = (int64_t) c * PF_CH;
+        const int64_t c0 = (int64_t) c * CH;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < CH / 16; ++k) {
             const int i = wave + 4 * k;                       // 1 KiB piece: rows 4i .. 4i+3
             const int r = 4 * i + (lane >> 4), cs = lane & 15;
             const int64_t row = min(c0 + r, a.n_kv - 1);
@@ -612,15 +615,15 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
                                              (lds_ptr_t) (vl[s] + 512 * i), 16, 0, 0);
         }
     };
-    constexpr int MPT = (QB * PF_CH + 255) / 256;   // mask values per thread
+    constexpr int MPT = (QB * CH + 255) / 256;   // mask values per thread
     uint16_t mreg[MPT];
     auto load_mask = [&](int c) {
-        const int64_t c0 = (int64_t) c * PF_CH;
+        const int64_t c0 = (int64_t) c * CH;
 #pragma unroll
         for (int k = 0; k < MPT; ++k) {
-            const int e = tid + 256 * k, qi = e / PF_CH, j = e % PF_CH;
+            const int e = tid + 256 * k, qi = e / CH, j = e % CH;
             uint16_t v = 0xfc00;
-            if (e < QB * PF_CH && c0 + j < a.n_kv) {
+            if (e < QB * CH && c0 + j < a.n_kv) {
                 v = 0;
                 if (a.mask) v = *(const uint16_t *) (a.mask + (min(q0 + qi, a.n_q - 1) % a.mask_ne1) * a.nbm1 + 2 * (c0 + j));
             }
@@ -631,15 +634,30 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
 #pragma unroll
         for (int k = 0; k < MPT; ++k) {
             const int e = tid + 256 * k;
-            if (e < QB * PF_CH) ml[s][e] = mreg[k];
+            if (e < QB * CH) ml[s][e] = mreg[k];
         }
     };
 
     // ---- phase-1 role: quad qi = lane / 4 scores pair 4w + (qi & 3) at positions 4r + qi / 4 --
     const int qd = lane & 3, qi = lane >> 2;
     const int p1 = 4 * wave + (qi & 3), r1 = qi >> 2;
-    float qf[NM][4];
-    {
+    // (QH: quad qi scores pairs 4w + 2 (qi & 1) and the next one at positions 8r + qi / 2 — each K
+    // row read from LDS once for two pairs; q of both as packed f16 pairs)
+    const int pa = 4 * wave + 2 * (qi & 1), ra = qi >> 1;
+    float qf[QH ? 1 : NM][4];
+    uint32_t qh[QH ? 2 : 1][QH ? NM : 1][2];
+    if constexpr (QH) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float * qr = (const float *) (a.q + qrow_of(pa + e) * a.nbq1 + head_of(pa + e) * a.nbq2 + iq3 * a.nbq3);
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                const float4 t = *(const float4 *) (qr + 16 * m + 4 * qd);
+                qh[e][m][0] = (uint32_t) f2h(t.x) | ((uint32_t) f2h(t.y) << 16);
+                qh[e][m][1] = (uint32_t) f2h(t.z) | ((uint32_t) f2h(t.w) << 16);
+            }
+        }
+    } else {
         const float * qr = (const float *) (a.q + qrow_of(p1) * a.nbq1 + head_of(p1) * a.nbq2 + iq3 * a.nbq3);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
@@ -647,6 +665,7 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
             qf[m][0] = f16r(t.x); qf[m][1] = f16r(t.y); qf[m][2] = f16r(t.z); qf[m][3] = f16r(t.w);
         }
     }
+    const float slope_a = slope_of(pa), slope_b = slope_of(pa + 1);
     const float slope1 = slope_of(p1);
     float nz = -0.0f;
     asm volatile("" : "+v"(nz));
@@ -665,7 +684,7 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
     }
     for (int c = 0; c < nchunk; ++c) {
         const int s = c & 1;
-        const int64_t c0 = (int64_t) c * PF_CH;
+        const int64_t c0 = (int64_t) c * CH;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();   // stage s (K, V, mask) is in; every wave is done with stage s^1
         const bool more = c + 1 < nchunk;
@@ -677,18 +696,36 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
         const uint16_t * ks = kl[s];
         const uint16_t * ms = ml[s];
         // ---- phase 1: scores of the wave's 4 pairs x 64 positions --------------------------
-#pragma unroll 4
-        for (int r = 0; r < PF_CH / 4; ++r) {
-            const int j = 4 * r + r1;
-            uint2 kh[NM];
+        auto score_of = [&](float w, float slope, int p, int j) {
+            float sv = __fmul_rn(w, a.scale);
+            if (a.softcap != 0.0f) sv = __fmul_rn(a.softcap, tanhf(sv));
+            sc[j * PF_P + p] = __fadd_rn(sv, __fmul_rn(slope, h2f(ms[(p / G) * CH + j])));
+        };
+        if constexpr (QH) {
+#pragma unroll 2
+            for (int r = 0; r < CH / 8; ++r) {
+                const int j = 8 * r + ra;
+                uint2 kh[NM];
 #pragma unroll
-            for (int m = 0; m < NM; ++m)
-                kh[m] = *(const uint2 *) ((const char *) ks + j * 256 + 16 * ((2 * m + (qd >> 1)) ^ (2 * (j & 3))) + 8 * (qd & 1));
-            const float w = dot_f16_mix_d128(kh, qf, nz);
-            if (qd == 0) {
-                float sv = __fmul_rn(w, a.scale);
-                if (a.softcap != 0.0f) sv = __fmul_rn(a.softcap, tanhf(sv));
-                sc[j * PF_P + p1] = __fadd_rn(sv, __fmul_rn(slope1, h2f(ms[(p1 / G) * PF_CH + j])));
+                for (int m = 0; m < NM; ++m)
+                    kh[m] = *(const uint2 *) ((const char *) ks + j * 256 + 16 * ((2 * m + (qd >> 1)) ^ (2 * (j & 3))) + 8 * (qd & 1));
+                const float wa = dot_f16_mix_d128_h(kh, qh[0], nz);
+                const float wb = dot_f16_mix_d128_h(kh, qh[1], nz);
+                if (qd == 0) {
+                    score_of(wa, slope_a, pa, j);
+                    score_of(wb, slope_b, pa + 1, j);
+                }
+            }
+        } else {
+#pragma unroll 4
+            for (int r = 0; r < CH / 4; ++r) {
+                const int j = 4 * r + r1;
+                uint2 kh[NM];
+#pragma unroll
+                for (int m = 0; m < NM; ++m)
+                    kh[m] = *(const uint2 *) ((const char *) ks + j * 256 + 16 * ((2 * m + (qd >> 1)) ^ (2 * (j & 3))) + 8 * (qd & 1));
+                const float w = dot_f16_mix_d128(kh, qf, nz);
+                if (qd == 0) score_of(w, slope1, p1, j);
             }
         }
         asm volatile("" ::: "memory");
@@ -696,45 +733,83 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
         // ---- phase 2: per pair, the prefix max and the (ms, vs) coefficient of every position -
         // per pair: positions that update the running max / that are masked (uniform)
         uint64_t upd[4], dead[4];
+        if constexpr (CH == 32) {
+            // two pairs per pass: lanes 0-31 pair 2 ii, lanes 32-63 pair 2 ii + 1 (a scan segmented
+            // at 32 lanes: the row_bcast:31 step left out, the exclusive shift cut at lane 32)
+            const int hf = lane >> 5, j = lane & 31;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int p = 4 * wave + i, j = lane;
-            const bool live = c0 + j < nend && ms[(p / G) * PF_CH + j] != 0xfc00;
-            const float sj = live ? sc[j * PF_P + p] : -INFINITY;
-            const float sm = wave_scan_max(sj);
-            const float M = fmaxf(mc[i], dpp_ninf<0x138>(sm));   // max over every position before j
-            float vs, mv;
-            if (!live) { mv = 1.0f; vs = 0.0f; }
-            else if (sj > M) { mv = M == -INFINITY ? 0.0f : expf_cr(M - sj); vs = 1.0f; }
-            else { mv = 1.0f; vs = expf_cr(sj - M); }
-            cm[j * PF_P + p] = mv;
-            sc[j * PF_P + p] = vs;
-            upd[i] = __ballot(live && sj > M);
-            dead[i] = __ballot(!live);
-            mc[i] = fmaxf(mc[i], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), 63)));
+            for (int ii = 0; ii < 2; ++ii) {
+                const int i = 2 * ii + hf, p = 4 * wave + i;
+                const bool live = c0 + j < nend && ms[(p / G) * CH + j] != 0xfc00;
+                const float sj = live ? sc[j * PF_P + p] : -INFINITY;
+                float sm = sj;
+                sm = fmaxf(sm, dpp_ninf<0x111>(sm));
+                sm = fmaxf(sm, dpp_ninf<0x112>(sm));
+                sm = fmaxf(sm, dpp_ninf<0x114>(sm));
+                sm = fmaxf(sm, dpp_ninf<0x118>(sm));
+                sm = fmaxf(sm, dpp_ninf<0x142, 0xa>(sm));
+                const float ex = dpp_ninf<0x138>(sm);
+                float m_lo = mc[2 * ii], m_hi = mc[2 * ii + 1];
+                asm volatile("" : "+v"(m_lo), "+v"(m_hi));   // (a select of two array loads would become an indexed, scratch, access)
+                const float mci = hf ? m_hi : m_lo;
+                const float M = fmaxf(mci, j == 0 ? -INFINITY : ex);   // max over every position before j
+                float vs, mv;
+                if (!live) { mv = 1.0f; vs = 0.0f; }
+                else if (sj > M) { mv = M == -INFINITY ? 0.0f : expf_cr(M - sj); vs = 1.0f; }
+                else { mv = 1.0f; vs = expf_cr(sj - M); }
+                cm[j * PF_P + p] = mv;
+                sc[j * PF_P + p] = vs;
+                const uint64_t bu = __ballot(live && sj > M), bd = __ballot(!live);
+                upd[2 * ii] = bu & 0xffffffffull;
+                upd[2 * ii + 1] = bu >> 32;
+                dead[2 * ii] = bd & 0xffffffffull;
+                dead[2 * ii + 1] = bd >> 32;
+                mc[2 * ii] = fmaxf(mc[2 * ii], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), 31)));
+                mc[2 * ii + 1] = fmaxf(mc[2 * ii + 1], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), 63)));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int p = 4 * wave + i, j = lane;
+                const bool live = j < CH && c0 + j < nend && ms[(p / G) * CH + j] != 0xfc00;
+                const float sj = live ? sc[j * PF_P + p] : -INFINITY;
+                const float sm = wave_scan_max(sj);
+                const float M = fmaxf(mc[i], dpp_ninf<0x138>(sm));   // max over every position before j
+                float vs, mv;
+                if (!live) { mv = 1.0f; vs = 0.0f; }
+                else if (sj > M) { mv = M == -INFINITY ? 0.0f : expf_cr(M - sj); vs = 1.0f; }
+                else { mv = 1.0f; vs = expf_cr(sj - M); }
+                if (j < CH) {
+                    cm[j * PF_P + p] = mv;
+                    sc[j * PF_P + p] = vs;
+                }
+                upd[i] = __ballot(live && sj > M);
+                dead[i] = __ballot(!live);
+                mc[i] = fmaxf(mc[i], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sm), 63)));
+            }
         }
         asm volatile("" ::: "memory");
         mark(2);
         // ---- phase 3: the f16 recurrence, 2 dims x 4 pairs per lane (V from LDS) ------------
         {
-            const int nrun = (int) min((int64_t) PF_CH, nend - c0);
+            const int nrun = (int) min((int64_t) CH, nend - c0);
             const uint32_t * vrow = (const uint32_t *) vl[s] + lane;   // dims 2 lane, 2 lane + 1
             const float * scw = sc + 4 * wave;
             const float * cmw = cm + 4 * wave;
             // batch j0's V values and coefficients are read while batch j0 - U computes (a read
             // past the chunk end lands in other LDS data and is never used)
-            auto ldb = [&](int j0, uint32_t (&vv)[PF_U], float4 (&vs)[PF_U]) __attribute__((always_inline)) {
+            auto ldb = [&](int j0, uint32_t (&vv)[U], float4 (&vs)[U]) __attribute__((always_inline)) {
 #pragma unroll
-                for (int u = 0; u < PF_U; ++u) {
+                for (int u = 0; u < U; ++u) {
                     vv[u] = vrow[(j0 + u) * (D / 2)];
                     vs[u] = *(const float4 *) (scw + (j0 + u) * PF_P);
                 }
             };
-            auto run = [&](int j0, const uint32_t (&vv)[PF_U], const float4 (&vs)[PF_U]) __attribute__((always_inline)) {
+            auto run = [&](int j0, const uint32_t (&vv)[U], const float4 (&vs)[U]) __attribute__((always_inline)) {
                 const uint64_t ev = (upd[0] | upd[1] | upd[2] | upd[3] | dead[0] | dead[1] | dead[2] | dead[3]) >> j0;
-                if ((ev & ((1ull << PF_U) - 1)) == 0) {
+                if ((ev & ((1ull << U) - 1)) == 0) {
 #pragma unroll
-                    for (int u = 0; u < PF_U; ++u) {
+                    for (int u = 0; u < U; ++u) {
                         const float v4[4] = {vs[u].x, vs[u].y, vs[u].z, vs[u].w};
 #pragma unroll
                         for (int i = 0; i < 4; ++i) y[i] = f16x2_mad(vv[u], v4[i], y[i]);
@@ -749,7 +824,7 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
                     // value times 1 rounds back to itself, S*1 = S), and a masked step selects
                     // the old state
 #pragma unroll
-                    for (int u = 0; u < PF_U; ++u) {
+                    for (int u = 0; u < U; ++u) {
                         const int j = j0 + u;
                         const float v4[4] = {vs[u].x, vs[u].y, vs[u].z, vs[u].w};
                         const float4 m4 = *(const float4 *) (cmw + j * PF_P);
@@ -769,15 +844,15 @@ __global__ __launch_bounds__(256, 2) void k_fattn_pf(const fa_args a) {
                     }
                 }
             };
-            uint32_t va[PF_U], vb[PF_U];
-            float4 sa[PF_U], sb[PF_U];
+            uint32_t va[U], vb[U];
+            float4 sa[U], sb[U];
             ldb(0, va, sa);
-            for (int j0 = 0; j0 < nrun; j0 += 2 * PF_U) {
-                ldb(j0 + PF_U, vb, sb);
+            for (int j0 = 0; j0 < nrun; j0 += 2 * U) {
+                ldb(j0 + U, vb, sb);
                 run(j0, va, sa);
-                if (j0 + PF_U >= nrun) break;
-                ldb(j0 + 2 * PF_U, va, sa);
-                run(j0 + PF_U, vb, sb);
+                if (j0 + U >= nrun) break;
+                ldb(j0 + 2 * U, va, sa);
+                run(j0 + U, vb, sb);
             }
         }
         if (more) store_mask(s ^ 1);   // published by the next chunk's barrier
@@ -1605,6 +1680,20 @@ void launch_fattn_exact(hipStream_t st, const fa_args & a0, int64_t nq3) {
     if (a.D == 128 && a.n_q >= 16 && (a.qmode == 0 || (a.qmode == 1 && fattn_pf_quant_ok(a))) &&
         (G == 1 || G == 2 || G == 4 || G == 8 || G == 16)) {
         const dim3 g((unsigned) ceil_div(a.n_q, (int64_t) PF_P / G), (unsigned) (a.Hkv * nq3));
+        // 32-position chunks at three workgroups per CU (half the LDS stage, a 168-VGPR budget: q
+        // as packed f16, two pairs per scoring quad, two pairs per coefficient pass; n = 512:
+        // 213 -> 171 us, probe_fa_pf.py); GGML_MI355X_PF_CH=64: 64-position chunks at two
+        static const int pfch = getenv("GGML_MI355X_PF_CH") ? atoi(getenv("GGML_MI355X_PF_CH")) : 32;
+        if (pfch == 32) {
+            switch (G) {
+                case 1:  hipLaunchKernelGGL((k_fattn_pf<1, 32, 3>), g, dim3(256), 0, st, a); break;
+                case 2:  hipLaunchKernelGGL((k_fattn_pf<2, 32, 3>), g, dim3(256), 0, st, a); break;
+                case 4:  hipLaunchKernelGGL((k_fattn_pf<4, 32, 3>), g, dim3(256), 0, st, a); break;
+                case 8:  hipLaunchKernelGGL((k_fattn_pf<8, 32, 3>), g, dim3(256), 0, st, a); break;
+                default: hipLaunchKernelGGL((k_fattn_pf<16, 32, 3>), g, dim3(256), 0, st, a); break;
+            }
+            return;
+        }
         switch (G) {
             case 1:  hipLaunchKernelGGL(k_fattn_pf<1>, g, dim3(256), 0, st, a); break;
             case 2:  hipLaunchKernelGGL(k_fattn_pf<2>, g, dim3(256), 0, st, a); break;

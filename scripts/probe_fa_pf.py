@@ -11,7 +11,7 @@ lib = la.plugin_lib()
 f = lib.mi355x_bench_op
 f.restype = ctypes.c_double
 f.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
-tag = " ".join(f"{k[12:]}={v}" for k, v in os.environ.items() if k.startswith("GGML_MI355X_FA")) or "default"
+tag = " ".join(f"{k[12:]}={v}" for k, v in os.environ.items() if k.startswith("GGML_MI355X_FA") or k.startswith("GGML_MI355X_PF")) or "default"
 out = [f"n{n} {f(302, n, 0, 10):7.1f}us" for n in (128, 512, 2048)]
 print(f"[{tag}] " + " | ".join(out), flush=True)
 f(302, 512, 1, 3)
