@@ -310,6 +310,40 @@ def test_flash_attn_f16_decode_short_vs_oracle(K, n_kv, live, pattern):
     assert_bits(out, ref, f"flash_attn f16 short decode {pattern} n_kv={n_kv} live={live}")
 
 
+@pytest.mark.parametrize("n_kv,n_q,Hkv,G,pattern", [(300, 37, 2, 4, "holes"), (200, 16, 4, 1, "causal"),
+                                                    (130, 23, 2, 2, "sparse"), (1000, 64, 8, 8, "causal"),
+                                                    (64, 40, 1, 16, "dead_prefix"), (97, 33, 2, 4, "increasing"),
+                                                    (515, 48, 8, 4, "holes")])
+def test_flash_attn_f16_prefill_masks_vs_oracle(K, n_kv, n_q, Hkv, G, pattern):
+    """The prefill tile (k_fattn_pf, a batch of >= 16 query rows: 32-position chunks, two pairs per
+    scoring quad and per coefficient pass): every GQA group size, row counts that leave a partial
+    workgroup, cache lengths off the chunk grid, and masks beyond the causal tail — holes, a sparse
+    mask, a dead prefix, and scores rising with the position (a running-max update at every step)."""
+    rng = np.random.default_rng(n_kv * 31 + n_q * 7 + G)
+    D, H = 128, Hkv * G
+    q = (rng.standard_normal((n_q, H, D)) * 2).astype(np.float32)
+    kf = rng.standard_normal((n_kv, Hkv, D)).astype(np.float32)
+    if pattern == "increasing":
+        for hk in range(Hkv):
+            qd = q[0, hk * G] / np.linalg.norm(q[0, hk * G])
+            kf[:, hk, :] = 0.005 * kf[:, hk, :] + np.arange(n_kv, dtype=np.float32)[:, None] * 0.05 * qd[None, :]
+    k = kf.astype(np.float16)
+    v = rng.standard_normal((n_kv, Hkv, D)).astype(np.float16)
+    m = np.zeros((n_q, n_kv), dtype=np.float16)
+    for r in range(n_q):
+        last = n_kv - n_q + r
+        m[r, last + 1:] = -np.inf
+        if pattern == "holes":
+            m[r, :last][rng.random(last) < 0.3] = -np.inf
+        elif pattern == "sparse":
+            m[r, :last][rng.random(last) < 0.9] = -np.inf
+        elif pattern == "dead_prefix":
+            m[r, :min(40, last)] = -np.inf
+    out = K.flash_attn(q, k.view(np.uint8), v.view(np.uint8), m.view(np.uint16), O.F16, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    ref = O.flash_attn(q, k.view(np.uint8), v.view(np.uint8), m.view(np.uint16), O.F16, D, H, Hkv, n_kv, 1 / np.sqrt(D))
+    assert_bits(out, ref, f"flash_attn f16 prefill {pattern} n_kv={n_kv} n_q={n_q} G={G}")
+
+
 @pytest.mark.parametrize("name,Kd,M", [("q4_K", 4096, 256), ("q5_K", 4096, 200), ("q6_K", 4096, 136),
                                         ("q4_K", 14336, 128), ("q6_K", 14336, 64), ("q4_K", 4096, 100)])
 def test_mul_mat_prefill_bit_exact(K, name, Kd, M):
